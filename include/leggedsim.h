@@ -1,0 +1,260 @@
+/*
+ * leggedsim.h — C ABI of the MI355X-native vectorised legged-robot simulator.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json
+ * (`LeggedRobot.step()`: PD -> rigid-body dynamics + contact x decimation ->
+ * obs / reward / done / reset).  It replaces two reference interfaces:
+ *
+ *  (1) the IsaacGym tensor API the env calls:
+ *        gym.create_sim / prepare_sim          legged_robot.py:240, base_task.py:56
+ *        acquire_*_tensor + wrap_tensor        legged_robot.py:83-92,104-120, h1_env.py:37
+ *        refresh_*_tensor                      legged_robot.py:639,678-679, h1_env.py:49
+ *        set_dof_actuation_force_tensor        legged_robot.py:629
+ *        simulate / fetch_results              legged_robot.py:630,637-638
+ *        set_actor_root_state_tensor_indexed   legged_robot.py:553-555,592-594
+ *        set_dof_state_tensor_indexed          legged_robot.py:570-572
+ *        per-env shape friction / base mass    legged_robot.py:412-440,472-483
+ *  (2) the whole control step `LeggedRobot.step` (legged_robot.py:615-647) with
+ *      `post_physics_step` (:673-709) fused into ONE launch (lgs_step), so the
+ *      Python side keeps the VecEnv contract but issues no per-op kernels and
+ *      no device->host syncs (the reference's nonzero() calls at :511,:545,:697
+ *      become in-kernel masks).
+ *
+ * Conventions
+ *  - All state / env buffers are DEVICE pointers, fp32, env-major, contiguous:
+ *      root_states [N,13] = pos(3) quat xyzw(4) lin vel of the root COM(3) ang vel(3)
+ *      dof_state   [N*D,2] = (q, qd)
+ *      net_contact_forces [N*B,3]   (from the last substep, like PhysX)
+ *      rigid_body_states  [N*B,13]  (origin pos, quat, COM lin vel, ang vel)
+ *    The caller owns these buffers and binds them once (lgs_bind_state);
+ *    the simulator reads and writes them in place, so refresh_* is a no-op
+ *    and a torch tensor view is always current.
+ *  - Booleans (reset, time_out, last_contacts) are 1 byte (torch.bool).
+ *  - Host-side descriptors (model, params) are copied at call time.
+ *  - Every call returns LGS_OK (0) or a negative status; lgs_last_error()
+ *    gives a thread-local message.  No call aborts the process.
+ *  - Work is enqueued on the stream set with lgs_set_stream (default stream 0);
+ *    nothing synchronises the host except lgs_synchronize.  Launches are
+ *    hipGraph-capturable (no allocation or sync inside lgs_step/lgs_simulate).
+ *  - One host thread per lgs_sim.
+ */
+#ifndef LEGGEDSIM_H
+#define LEGGEDSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define LGS_EXTERN extern "C"
+#else
+#define LGS_EXTERN
+#endif
+#define LGS_API LGS_EXTERN __attribute__((visibility("default")))
+
+#define LGS_OK 0
+#define LGS_ERR_ARG (-1)
+#define LGS_ERR_HIP (-2)
+#define LGS_ERR_STATE (-3)
+
+#define LGS_MAX_BODIES 32
+#define LGS_MAX_DOFS 26
+#define LGS_MAX_DEPTH 10
+#define LGS_MAX_FEET 4
+#define LGS_MAX_CONTACT_BODIES 16
+#define LGS_MAX_OBS 128
+#define LGS_MAX_REWARDS 24
+
+/* ---- articulated model (host pointers; see leggedsim/model.py) ---------- */
+typedef struct lgs_model_desc {
+    int32_t num_bodies;       /* B (after fixed-joint collapse)          */
+    int32_t num_dofs;         /* D (revolute joints, DFS order)          */
+    int32_t num_points;       /* P contact candidate points              */
+    const int32_t* parent;    /* [B]  -1 for the floating root            */
+    const int32_t* dof;       /* [B]  dof of the joint to the parent or -1 */
+    const int32_t* subtree_end; /* [B] subtree(b) = [b, subtree_end[b])    */
+    const int32_t* depth;     /* [B]                                     */
+    const int32_t* chain;     /* [B][LGS_MAX_DEPTH] root..b, -1 padded    */
+    const float* joint_rot;   /* [B][9] parent frame -> joint frame (row-major) */
+    const float* joint_pos;   /* [B][3]                                  */
+    const float* axis;        /* [B][3] joint axis in the child frame     */
+    const float* mass;        /* [B]                                     */
+    const float* com;         /* [B][3] body frame                        */
+    const float* inertia;     /* [B][6] Ixx Iyy Izz Ixy Ixz Iyz about com  */
+    const int32_t* dof_body;  /* [D]                                     */
+    const float* dof_lower;   /* [D] URDF limits                          */
+    const float* dof_upper;
+    const float* dof_effort;
+    const float* dof_velocity;
+    const int32_t* pt_body;   /* [P]                                     */
+    const float* pt_pos;      /* [P][3] body frame                        */
+    const float* pt_radius;   /* [P]                                     */
+} lgs_model_desc;
+
+/* ---- simulation parameters: cfg.sim + cfg.sim.physx + cfg.asset
+ *      (legged_robot_config.py:131-143, 225-242)                         */
+typedef struct lgs_sim_params {
+    float dt;                        /* sim.dt (0.005; H1_2 0.0025)        */
+    float gravity[3];                /* (0,0,-9.81), z up                  */
+    int32_t solver_iterations;       /* contact/limit PGS sweeps per substep */
+    float contact_offset;            /* physx.contact_offset  (0.01 m)     */
+    float rest_offset;               /* physx.rest_offset     (0.0)        */
+    float max_depenetration_velocity;/* physx (1.0 m/s)                    */
+    float baumgarte;                 /* penetration fraction corrected per substep */
+    float ground_friction;           /* plane static/dynamic friction (1.0), averaged with shape friction */
+    float armature;                  /* asset.armature (H1_2: 1e-3)        */
+    int32_t clamp_joint_velocity;    /* clamp |qd| to the URDF velocity limit */
+    int32_t max_contacts;            /* contact slots per env               */
+    int32_t max_rows;                /* constraint rows per env (<= compiled capacity);
+                                        joint-limit rows are capped at max_rows - 3*max_contacts */
+} lgs_sim_params;
+
+/* ---- task (env) parameters: everything post_physics_step reads from cfg ---- */
+enum lgs_obs_layout {
+    LGS_OBS_QUADRUPED = 0,   /* legged_robot.py:800-807  [v*s, w*s, g, cmd*s, dq, qd*s, a]          */
+    LGS_OBS_HUMANOID = 1     /* h1_env.py:68-95 / g1_env.py:108-141  obs=[w,g,cmd,dq,qd,a,sin,cos], priv=[v, obs] */
+};
+
+/* reward term ids; the task lists the active ones in alphabetical order
+ * (class_to_dict uses dir(), legged_robot.py:822-836)                     */
+enum lgs_reward_id {
+    LGS_REW_ACTION_RATE = 0, LGS_REW_ALIVE, LGS_REW_ANG_VEL_XY, LGS_REW_BASE_HEIGHT,
+    LGS_REW_COLLISION, LGS_REW_CONTACT, LGS_REW_CONTACT_NO_VEL, LGS_REW_DOF_ACC,
+    LGS_REW_DOF_POS_LIMITS, LGS_REW_DOF_VEL, LGS_REW_DOF_VEL_LIMITS, LGS_REW_FEET_AIR_TIME,
+    LGS_REW_FEET_CONTACT_FORCES, LGS_REW_FEET_STUMBLE, LGS_REW_FEET_SWING_HEIGHT,
+    LGS_REW_HIP_POS, LGS_REW_LIN_VEL_Z, LGS_REW_ORIENTATION, LGS_REW_STAND_STILL,
+    LGS_REW_TORQUE_LIMITS, LGS_REW_TORQUES, LGS_REW_TRACKING_ANG_VEL, LGS_REW_TRACKING_LIN_VEL,
+    LGS_REW_COUNT
+};
+
+typedef struct lgs_task_params {
+    int32_t obs_layout;            /* lgs_obs_layout                        */
+    int32_t num_obs;               /* O                                     */
+    int32_t num_privileged_obs;    /* P or 0                                */
+    int32_t num_actions;           /* A (== D)                              */
+    int32_t decimation;
+    int32_t control_type;          /* 0 P, 1 V, 2 T (legged_robot.py:663-670) */
+    float action_scale;
+    float clip_actions, clip_observations;
+    float control_dt;              /* decimation * sim.dt                   */
+    float p_gains[LGS_MAX_DOFS], d_gains[LGS_MAX_DOFS];
+    float default_dof_pos[LGS_MAX_DOFS];
+    float torque_limits[LGS_MAX_DOFS];
+    float soft_dof_pos_lower[LGS_MAX_DOFS], soft_dof_pos_upper[LGS_MAX_DOFS];
+    float dof_vel_limits[LGS_MAX_DOFS];
+    float obs_scale_lin_vel, obs_scale_ang_vel, obs_scale_dof_pos, obs_scale_dof_vel;
+    float commands_scale[3];
+    int32_t add_noise;
+    float noise_vec[LGS_MAX_OBS];
+    /* episode / commands / pushes */
+    float max_episode_length;      /* ceil(episode_length_s / dt)            */
+    float max_episode_length_s;
+    int32_t resample_interval;     /* int(resampling_time / dt)              */
+    int32_t heading_command;
+    float cmd_lin_vel_x[2], cmd_lin_vel_y[2], cmd_ang_vel_yaw[2], cmd_heading[2];
+    int32_t push_robots;
+    int32_t push_interval;         /* int(ceil(push_interval_s / dt))        */
+    float max_push_vel_xy;
+    float base_init_state[13];
+    /* bodies selected by name substring (legged_robot.py:346-407) */
+    int32_t num_feet, feet_idx[LGS_MAX_FEET];
+    int32_t num_penalised, penalised_idx[LGS_MAX_CONTACT_BODIES];
+    int32_t num_termination, termination_idx[LGS_MAX_CONTACT_BODIES];
+    int32_t num_hip, hip_dofs[8];
+    /* rewards */
+    int32_t num_rewards;
+    int32_t reward_ids[LGS_MAX_REWARDS];
+    float reward_scales[LGS_MAX_REWARDS];   /* already multiplied by dt      */
+    int32_t has_termination_reward;
+    float termination_scale;
+    int32_t only_positive_rewards;
+    float tracking_sigma, base_height_target, max_contact_force;
+    float soft_dof_vel_limit, soft_torque_limit;
+    /* humanoid gait phase (h1_env.py:55-65) */
+    float phase_period, phase_offset, stance_threshold, swing_height_target;
+    uint64_t seed;
+} lgs_task_params;
+
+/* ---- per-env buffers of the VecEnv (device pointers; torch owns them) ---- */
+typedef struct lgs_env_buffers {
+    float* actions;          /* [N,A] in: raw policy actions; out: clipped env.actions (0 on reset) */
+    float* last_actions;     /* [N,A] */
+    float* last_dof_vel;     /* [N,D] */
+    float* last_root_vel;    /* [N,6] */
+    float* torques;          /* [N,D] last substep's torques */
+    float* commands;         /* [N,4] */
+    float* feet_air_time;    /* [N,F] */
+    uint8_t* last_contacts;  /* [N,F] bool */
+    int64_t* episode_length; /* [N] */
+    float* obs;              /* [N,O] */
+    float* priv_obs;         /* [N,P] or NULL */
+    float* rew;              /* [N]   */
+    uint8_t* reset;          /* [N] bool */
+    uint8_t* time_out;       /* [N] bool */
+    float* episode_sums;     /* [num_rewards(+1 termination), N] */
+    float* episode_acc;      /* [num_sums + 1]: sums over envs reset this step, then the count */
+    float* base_lin_vel;     /* [N,3] */
+    float* base_ang_vel;     /* [N,3] */
+    float* projected_gravity;/* [N,3] */
+    float* rpy;              /* [N,3] */
+    float* env_origins;      /* [N,3] */
+    float* phase;            /* [N]   humanoid, else NULL */
+    float* leg_phase;        /* [N,2] humanoid, else NULL */
+    float* rew_terms;        /* [num_rewards, N] per-term reward of this step (diagnostics) or NULL */
+} lgs_env_buffers;
+
+typedef struct lgs_sim lgs_sim;
+
+LGS_API const char* lgs_last_error(void);
+LGS_API int lgs_version(void);
+
+/* gym.create_sim + load_asset + create_env/actor x N (legged_robot.py:240,328,364-381) */
+LGS_API int lgs_create_sim(const lgs_model_desc* model, const lgs_sim_params* params,
+                           int32_t num_envs, int32_t device_id, lgs_sim** out);
+LGS_API int lgs_destroy_sim(lgs_sim* sim);
+LGS_API int lgs_set_stream(lgs_sim* sim, void* hip_stream);
+LGS_API int lgs_synchronize(lgs_sim* sim);
+
+/* _process_rigid_shape_props / _process_rigid_body_props (legged_robot.py:412-440, 472-483):
+ * per-env shape friction and added root-body mass (host arrays [N]; NULL = unchanged) */
+LGS_API int lgs_set_env_properties(lgs_sim* sim, const float* shape_friction, const float* added_base_mass);
+
+/* bind the caller-owned state tensors (acquire_* + wrap_tensor) */
+LGS_API int lgs_bind_state(lgs_sim* sim, float* root_states, float* dof_state,
+                           float* net_contact_forces, float* rigid_body_states);
+
+/* refresh_* : no-ops kept for API parity (the bound views are written in place) */
+LGS_API int lgs_refresh(lgs_sim* sim);
+
+/* set_dof_actuation_force_tensor: torques [N*D] used by the next lgs_simulate */
+LGS_API int lgs_set_dof_actuation_force(lgs_sim* sim, const float* torques);
+/* gym.simulate: ONE physics substep of every env (dynamics + contact + integrate) */
+LGS_API int lgs_simulate(lgs_sim* sim);
+/* forward kinematics only: rigid_body_states from root/dof state */
+LGS_API int lgs_forward_kinematics(lgs_sim* sim);
+
+/* set_*_tensor_indexed: copy rows `ids` (int32, device) from src into the bound state.
+ * When src is the bound buffer itself this is a no-op. */
+LGS_API int lgs_set_actor_root_state_indexed(lgs_sim* sim, const float* root_src, const int32_t* ids, int32_t n);
+LGS_API int lgs_set_dof_state_indexed(lgs_sim* sim, const float* dof_src, const int32_t* ids, int32_t n);
+
+/* task setup + the fused control step (LeggedRobot.step + post_physics_step) */
+LGS_API int lgs_set_task(lgs_sim* sim, const lgs_task_params* task);
+LGS_API int lgs_step(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* reset_idx(all) as used by BaseTask.reset (base_task.py:82-86) */
+LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+
+/* name/index queries */
+LGS_API int lgs_get_counts(lgs_sim* sim, int32_t* num_envs, int32_t* num_bodies, int32_t* num_dofs);
+
+/* counter-based RNG used by every random draw of the step (Philox4x32-10);
+ * exposed so tests and the oracle can reproduce the draws bit-exactly. */
+LGS_API float lgs_uniform(uint64_t seed, uint32_t env, uint32_t step, uint32_t stream, uint32_t index);
+
+/* random draw streams */
+#define LGS_STREAM_NOISE 0u
+#define LGS_STREAM_CMD 1u
+#define LGS_STREAM_RESET_DOF 2u
+#define LGS_STREAM_RESET_ROOT 3u
+#define LGS_STREAM_RESET_CMD 4u
+#define LGS_STREAM_PUSH 5u
+
+#endif /* LEGGEDSIM_H */

@@ -1,0 +1,927 @@
+/*
+ * lgs_oracle.c — CPU ORACLE (test infrastructure only; never shipped or measured
+ * as the product).  Plain serial C restatement of the hot path so that the HIP
+ * implementation in unitree-rl-gym_amd/csrc can be checked against it.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ *
+ * Two halves, with different parity status:
+ *
+ *  A. post-physics stack (PD torque, base-frame quantities, commands, termination,
+ *     rewards, reset, push, observations) — a restatement of the reference:
+ *       legged_gym/envs/base/legged_robot.py  (cited per function below)
+ *       legged_gym/envs/h1/h1_env.py, g1/g1_env.py, h1_2/h1_2_env.py
+ *       legged_gym/utils/isaacgym_utils.py, utils/math.py
+ *     PINNED against golden vectors produced by running the reference's own
+ *     Python code (tests/golden/, generator oracle/gen_golden.py).
+ *
+ *  B. rigid-body dynamics + contact (what IsaacGym/PhysX's gym.simulate does,
+ *     legged_robot.py:630).  PhysX is closed source and absent, so this half is
+ *     the build's own algorithm, stated once here and once (wave-parallel) in HIP:
+ *       floating-base reduced coordinates, world-aligned Plücker frame at the root
+ *       origin; composite-rigid-body mass matrix, recursive Newton-Euler bias,
+ *       dense Cholesky; joint limits + point contacts vs the z=0 plane as
+ *       unilateral rows solved by projected Gauss-Seidel with a circular friction
+ *       cone; semi-implicit Euler.  PARITY UNPINNED vs PhysX; pinned only by
+ *       analytic tests (free fall, resting height, momentum) and HIP==oracle.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/leggedsim.h"
+
+#define NMAX (6 + LGS_MAX_DOFS)
+#define ROWMAX 64
+#define LGS_PI_F 3.14159265358979323846f
+
+/* ----------------------------------------------------------------- RNG -- */
+/* Philox4x32-10, counter = (env, step, stream, index), key = seed.         */
+static void philox_round(uint32_t c[4], uint32_t k[2]) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k[0];
+    uint32_t n2 = hi0 ^ c[3] ^ k[1];
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k[0] += 0x9E3779B9u; k[1] += 0xBB67AE85u;
+}
+
+float orc_uniform(uint64_t seed, uint32_t env, uint32_t step, uint32_t stream, uint32_t index) {
+    uint32_t c[4] = {env, step, stream, index};
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int r = 0; r < 10; ++r) philox_round(c, k);
+    return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+/* torch_rand_float(lo, hi) = (hi - lo) * rand + lo  (isaacgym.torch_utils) */
+static float rand_range(float lo, float hi, float u) { return (hi - lo) * u + lo; }
+
+/* ------------------------------------------------------------ 3-vectors -- */
+static void cross3(const float a[3], const float b[3], float o[3]) {
+    float x = a[1] * b[2] - a[2] * b[1];
+    float y = a[2] * b[0] - a[0] * b[2];
+    float z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void matvec(const float R[9], const float v[3], float o[3]) {
+    float x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    float y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    float z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static void matmul(const float A[9], const float B[9], float C[9]) {
+    float T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof(T));
+}
+static void quat_to_mat(const float q[4], float R[9]) {
+    float x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+}
+static void mat_to_quat(const float R[9], float q[4]) {
+    float tr = R[0] + R[4] + R[8];
+    if (tr > 0.f) {
+        float s = sqrtf(tr + 1.f) * 2.f;
+        q[3] = 0.25f * s; q[0] = (R[7] - R[5]) / s; q[1] = (R[2] - R[6]) / s; q[2] = (R[3] - R[1]) / s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        float s = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f;
+        q[3] = (R[7] - R[5]) / s; q[0] = 0.25f * s; q[1] = (R[1] + R[3]) / s; q[2] = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        float s = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f;
+        q[3] = (R[2] - R[6]) / s; q[0] = (R[1] + R[3]) / s; q[1] = 0.25f * s; q[2] = (R[5] + R[7]) / s;
+    } else {
+        float s = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f;
+        q[3] = (R[3] - R[1]) / s; q[0] = (R[2] + R[6]) / s; q[1] = (R[5] + R[7]) / s; q[2] = 0.25f * s;
+    }
+}
+/* rotation by angle about unit axis a (Rodrigues) */
+static void axis_angle(const float a[3], float ang, float R[9]) {
+    float c = cosf(ang), s = sinf(ang), t = 1.f - c;
+    float x = a[0], y = a[1], z = a[2];
+    R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
+    R[3] = t * x * y + s * z; R[4] = t * y * y + c;     R[5] = t * y * z - s * x;
+    R[6] = t * x * z - s * y; R[7] = t * y * z + s * x; R[8] = t * z * z + c;
+}
+
+/* --------------------------------------------------- spatial algebra ---- */
+/* motion vector (w, v) at O; force vector (n, f) at O.
+ * spatial inertia at O kept as (m, h = m*(c - O), Ib = Icom + m[(r.r)1 - r r^T]) */
+typedef struct { float m, h[3], I[6]; } sinertia; /* I: xx yy zz xy xz yz */
+
+static void sin_apply(const sinertia* S, const float w[3], const float v[3], float n[3], float f[3]) {
+    float Iw0 = S->I[0] * w[0] + S->I[3] * w[1] + S->I[4] * w[2];
+    float Iw1 = S->I[3] * w[0] + S->I[1] * w[1] + S->I[5] * w[2];
+    float Iw2 = S->I[4] * w[0] + S->I[5] * w[1] + S->I[2] * w[2];
+    float hv[3], hw[3];
+    cross3(S->h, v, hv);
+    cross3(S->h, w, hw);
+    n[0] = Iw0 + hv[0]; n[1] = Iw1 + hv[1]; n[2] = Iw2 + hv[2];
+    f[0] = S->m * v[0] - hw[0]; f[1] = S->m * v[1] - hw[1]; f[2] = S->m * v[2] - hw[2];
+}
+
+/* ------------------------------------------------------------- model --- */
+typedef struct {
+    const lgs_model_desc* md;
+    int B, D, P, n;
+} omodel;
+
+typedef struct {
+    float R[LGS_MAX_BODIES][9], p[LGS_MAX_BODIES][3];
+    float aw[LGS_MAX_BODIES][3];   /* joint axis, world */
+    float cw[LGS_MAX_BODIES][3];   /* com, world */
+} okin;
+
+/* forward kinematics (URDF: child = parent * origin * Rot(axis, q)) */
+static void fk(const lgs_model_desc* md, const float* root13, const float* dofq, okin* K) {
+    int B = md->num_bodies;
+    quat_to_mat(root13 + 3, K->R[0]);
+    K->p[0][0] = root13[0]; K->p[0][1] = root13[1]; K->p[0][2] = root13[2];
+    K->aw[0][0] = K->aw[0][1] = K->aw[0][2] = 0.f;
+    for (int b = 1; b < B; ++b) {
+        int P = md->parent[b];
+        float Rj[9], t[3];
+        matmul(K->R[P], md->joint_rot + 9 * b, Rj);
+        matvec(K->R[P], md->joint_pos + 3 * b, t);
+        K->p[b][0] = K->p[P][0] + t[0]; K->p[b][1] = K->p[P][1] + t[1]; K->p[b][2] = K->p[P][2] + t[2];
+        int j = md->dof[b];
+        if (j >= 0) {
+            float Ra[9];
+            matvec(Rj, md->axis + 3 * b, K->aw[b]);
+            axis_angle(md->axis + 3 * b, dofq[2 * j], Ra);
+            matmul(Rj, Ra, K->R[b]);
+        } else {
+            memcpy(K->R[b], Rj, sizeof(Rj));
+            K->aw[b][0] = K->aw[b][1] = K->aw[b][2] = 0.f;
+        }
+    }
+    for (int b = 0; b < B; ++b) {
+        float c[3];
+        matvec(K->R[b], md->com + 3 * b, c);
+        K->cw[b][0] = K->p[b][0] + c[0]; K->cw[b][1] = K->p[b][1] + c[1]; K->cw[b][2] = K->p[b][2] + c[2];
+    }
+}
+
+/* dense Cholesky in place (lower), n <= NMAX */
+static void cholesky(float* M, int n) {
+    for (int k = 0; k < n; ++k) {
+        float d = M[k * NMAX + k];
+        for (int s = 0; s < k; ++s) d -= M[k * NMAX + s] * M[k * NMAX + s];
+        d = sqrtf(fmaxf(d, 1e-12f));
+        M[k * NMAX + k] = d;
+        for (int i = k + 1; i < n; ++i) {
+            float v = M[i * NMAX + k];
+            for (int s = 0; s < k; ++s) v -= M[i * NMAX + s] * M[k * NMAX + s];
+            M[i * NMAX + k] = v / d;
+        }
+    }
+}
+static void fwd_sub(const float* L, int n, float* x) {
+    for (int i = 0; i < n; ++i) {
+        float v = x[i];
+        for (int s = 0; s < i; ++s) v -= L[i * NMAX + s] * x[s];
+        x[i] = v / L[i * NMAX + i];
+    }
+}
+static void bwd_sub(const float* L, int n, float* x) {
+    /* subtraction order s = n-1 .. i+1 (the order a column sweep produces) */
+    for (int i = n - 1; i >= 0; --i) {
+        float v = x[i];
+        for (int s = n - 1; s > i; --s) v -= L[s * NMAX + i] * x[s];
+        x[i] = v / L[i * NMAX + i];
+    }
+}
+
+/* One physics substep of one env (gym.simulate, legged_robot.py:630).
+ * root13/dof (in/out), tau [D], contact forces out [B][3], added base mass, friction. */
+void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* root13, float* dofs,
+                     const float* tau, float* cforce, float added_mass, float shape_friction) {
+    const int B = md->num_bodies, D = md->num_dofs, n = 6 + D;
+    const float dt = sp->dt;
+    okin K;
+    fk(md, root13, dofs, &K);
+    const float* O = K.p[0];
+    /* root origin velocity from COM velocity */
+    float w0[3] = {root13[10], root13[11], root13[12]};
+    float rc[3] = {K.cw[0][0] - O[0], K.cw[0][1] - O[1], K.cw[0][2] - O[2]};
+    float wxr[3];
+    cross3(w0, rc, wxr);
+    float vO[3] = {root13[7] - wxr[0], root13[8] - wxr[1], root13[9] - wxr[2]};
+
+    /* spatial inertias at O */
+    sinertia Sb[LGS_MAX_BODIES], Ic[LGS_MAX_BODIES];
+    for (int b = 0; b < B; ++b) {
+        float m = md->mass[b];
+        float scale = 1.f;
+        if (b == 0 && added_mass != 0.f && m > 0.f) { scale = (m + added_mass) / m; m = m + added_mass; }
+        const float* Il = md->inertia + 6 * b;
+        float IL[9] = {Il[0] * scale, Il[3] * scale, Il[4] * scale, Il[3] * scale, Il[1] * scale,
+                       Il[5] * scale, Il[4] * scale, Il[5] * scale, Il[2] * scale};
+        float T[9], Iw[9], Rt[9];
+        const float* R = K.R[b];
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rt[3 * i + j] = R[3 * j + i];
+        matmul(R, IL, T);
+        matmul(T, Rt, Iw);
+        float r[3] = {K.cw[b][0] - O[0], K.cw[b][1] - O[1], K.cw[b][2] - O[2]};
+        float rr = dot3(r, r);
+        Sb[b].m = m;
+        Sb[b].h[0] = m * r[0]; Sb[b].h[1] = m * r[1]; Sb[b].h[2] = m * r[2];
+        Sb[b].I[0] = Iw[0] + m * (rr - r[0] * r[0]);
+        Sb[b].I[1] = Iw[4] + m * (rr - r[1] * r[1]);
+        Sb[b].I[2] = Iw[8] + m * (rr - r[2] * r[2]);
+        Sb[b].I[3] = Iw[1] - m * r[0] * r[1];
+        Sb[b].I[4] = Iw[2] - m * r[0] * r[2];
+        Sb[b].I[5] = Iw[5] - m * r[1] * r[2];
+    }
+    /* motion subspaces S_j = (a, (p_j - O) x a) */
+    float Sw[LGS_MAX_BODIES][3], Sv[LGS_MAX_BODIES][3];
+    for (int b = 1; b < B; ++b) {
+        float r[3] = {K.p[b][0] - O[0], K.p[b][1] - O[1], K.p[b][2] - O[2]};
+        memcpy(Sw[b], K.aw[b], sizeof(float) * 3);
+        cross3(r, K.aw[b], Sv[b]);
+    }
+    /* velocities and bias accelerations (RNEA, qdd = 0, gravity as base accel) */
+    float Vw[LGS_MAX_BODIES][3], Vv[LGS_MAX_BODIES][3], Aw[LGS_MAX_BODIES][3], Av[LGS_MAX_BODIES][3];
+    float Fn[LGS_MAX_BODIES][3], Ff[LGS_MAX_BODIES][3];
+    for (int b = 0; b < B; ++b) {
+        if (b == 0) {
+            memcpy(Vw[0], w0, 12); memcpy(Vv[0], vO, 12);
+            Aw[0][0] = Aw[0][1] = Aw[0][2] = 0.f;
+            Av[0][0] = -sp->gravity[0]; Av[0][1] = -sp->gravity[1]; Av[0][2] = -sp->gravity[2];
+        } else {
+            int P = md->parent[b], j = md->dof[b];
+            memcpy(Vw[b], Vw[P], 12); memcpy(Vv[b], Vv[P], 12);
+            memcpy(Aw[b], Aw[P], 12); memcpy(Av[b], Av[P], 12);
+            if (j >= 0) {
+                float qd = dofs[2 * j + 1];
+                float sw[3] = {Sw[b][0] * qd, Sw[b][1] * qd, Sw[b][2] * qd};
+                float sv[3] = {Sv[b][0] * qd, Sv[b][1] * qd, Sv[b][2] * qd};
+                /* A += V_parent x (S qd):  (w x sw, w x sv + v x sw) */
+                float t1[3], t2[3], t3[3];
+                cross3(Vw[P], sw, t1);
+                cross3(Vw[P], sv, t2);
+                cross3(Vv[P], sw, t3);
+                for (int k = 0; k < 3; ++k) {
+                    Aw[b][k] += t1[k];
+                    Av[b][k] += t2[k] + t3[k];
+                    Vw[b][k] += sw[k];
+                    Vv[b][k] += sv[k];
+                }
+            }
+        }
+        /* f = I A + V x* (I V) ; (w,v) x* (n,f) = (w x n + v x f, w x f) */
+        float IAn[3], IAf[3], IVn[3], IVf[3], a1[3], a2[3], a3[3];
+        sin_apply(&Sb[b], Aw[b], Av[b], IAn, IAf);
+        sin_apply(&Sb[b], Vw[b], Vv[b], IVn, IVf);
+        cross3(Vw[b], IVn, a1);
+        cross3(Vv[b], IVf, a2);
+        cross3(Vw[b], IVf, a3);
+        for (int k = 0; k < 3; ++k) {
+            Fn[b][k] = IAn[k] + a1[k] + a2[k];
+            Ff[b][k] = IAf[k] + a3[k];
+        }
+    }
+    /* composites: subtree(b) is the DFS range [b, subtree_end[b]); summed last to first */
+    float CFn[LGS_MAX_BODIES][3], CFf[LGS_MAX_BODIES][3];
+    for (int b = 0; b < B; ++b) {
+        memset(&Ic[b], 0, sizeof(sinertia));
+        for (int k = 0; k < 3; ++k) CFn[b][k] = CFf[b][k] = 0.f;
+        for (int x = md->subtree_end[b] - 1; x >= b; --x) {
+            Ic[b].m += Sb[x].m;
+            for (int k = 0; k < 3; ++k) { Ic[b].h[k] += Sb[x].h[k]; CFn[b][k] += Fn[x][k]; CFf[b][k] += Ff[x][k]; }
+            for (int k = 0; k < 6; ++k) Ic[b].I[k] += Sb[x].I[k];
+        }
+    }
+    /* mass matrix + bias */
+    static __thread float M[NMAX * NMAX];
+    float C[NMAX];
+    memset(M, 0, sizeof(M));
+    {
+        const sinertia* S = &Ic[0];
+        float I3[9] = {S->I[0], S->I[3], S->I[4], S->I[3], S->I[1], S->I[5], S->I[4], S->I[5], S->I[2]};
+        const float* h = S->h;
+        float H[9] = {0, -h[2], h[1], h[2], 0, -h[0], -h[1], h[0], 0}; /* [h]x */
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                M[i * NMAX + j] = I3[3 * i + j];
+                M[i * NMAX + 3 + j] = H[3 * i + j];
+                M[(3 + i) * NMAX + j] = H[3 * j + i];
+                M[(3 + i) * NMAX + 3 + j] = (i == j) ? S->m : 0.f;
+            }
+        for (int k = 0; k < 3; ++k) { C[k] = CFn[0][k]; C[3 + k] = CFf[0][k]; }
+    }
+    for (int b = 1; b < B; ++b) {
+        int j = md->dof[b];
+        if (j < 0) continue;
+        float cn[3], cf[3];
+        sin_apply(&Ic[b], Sw[b], Sv[b], cn, cf);
+        for (int k = 0; k < 3; ++k) {
+            M[k * NMAX + 6 + j] = M[(6 + j) * NMAX + k] = cn[k];
+            M[(3 + k) * NMAX + 6 + j] = M[(6 + j) * NMAX + 3 + k] = cf[k];
+        }
+        C[6 + j] = dot3(Sw[b], CFn[b]) + dot3(Sv[b], CFf[b]);
+        /* ancestors (and self) along the chain */
+        for (int d = 1; d <= md->depth[b]; ++d) {
+            int a = md->chain[b * LGS_MAX_DEPTH + d];
+            int i = md->dof[a];
+            if (i < 0) continue;
+            float v = dot3(Sw[a], cn) + dot3(Sv[a], cf);
+            M[(6 + i) * NMAX + 6 + j] = v;
+            M[(6 + j) * NMAX + 6 + i] = v;
+        }
+        M[(6 + j) * NMAX + 6 + j] += sp->armature;
+    }
+    float rhs[NMAX];
+    for (int k = 0; k < 6; ++k) rhs[k] = -C[k];
+    for (int j = 0; j < D; ++j) rhs[6 + j] = tau[j] - C[6 + j];
+    cholesky(M, n);
+    fwd_sub(M, n, rhs);
+    bwd_sub(M, n, rhs); /* rhs = qdd */
+
+    /* free velocity (classical velocity of the root origin after dt) */
+    float qf[NMAX];
+    float wxv[3];
+    cross3(w0, vO, wxv);
+    for (int k = 0; k < 3; ++k) {
+        qf[k] = w0[k] + dt * rhs[k];
+        qf[3 + k] = vO[k] + dt * (rhs[3 + k] + wxv[k]);
+    }
+    for (int j = 0; j < D; ++j) qf[6 + j] = dofs[2 * j + 1] + dt * rhs[6 + j];
+
+    /* ---- constraint rows: joint limits then contacts (n, t1, t2) ---- */
+    static __thread float J[ROWMAX][NMAX];
+    float tgt[ROWMAX], lam[ROWMAX], v[ROWMAX];
+    int kind[ROWMAX]; /* 0 unilateral, 1 friction pair head, 2 friction pair tail */
+    int cb[ROWMAX / 3 + 1];
+    float mu = 0.5f * (sp->ground_friction + shape_friction);
+    int nr = 0;
+    const float beta = sp->baumgarte;
+    const int max_rows = sp->max_rows < ROWMAX ? sp->max_rows : ROWMAX;
+    const int max_limit = max_rows - 3 * sp->max_contacts;
+    for (int j = 0; j < D && nr < max_limit; ++j) {
+        float q = dofs[2 * j], lo = md->dof_lower[j], hi = md->dof_upper[j];
+        float qn = q + dt * qf[6 + j];
+        if (qn < lo) {
+            memset(J[nr], 0, sizeof(float) * n);
+            J[nr][6 + j] = 1.f;
+            float gap = q - lo;
+            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            kind[nr++] = 0;
+        } else if (qn > hi) {
+            memset(J[nr], 0, sizeof(float) * n);
+            J[nr][6 + j] = -1.f;
+            float gap = hi - q;
+            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            kind[nr++] = 0;
+        }
+    }
+    int nlimit = nr, nc = 0;
+    float cpt[ROWMAX / 3 + 1][3];
+    for (int k = 0; k < md->num_points; ++k) {
+        if (nc >= sp->max_contacts || nr + 3 > max_rows) break;
+        int b = md->pt_body[k];
+        float c[3];
+        matvec(K.R[b], md->pt_pos + 3 * k, c);
+        c[0] += K.p[b][0]; c[1] += K.p[b][1]; c[2] += K.p[b][2];
+        float sep = c[2] - md->pt_radius[k] - sp->rest_offset;
+        if (!(sep < sp->contact_offset)) continue;
+        float pc[3] = {c[0], c[1], c[2] - md->pt_radius[k]};
+        float r[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]};
+        static const float dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+        for (int dd = 0; dd < 3; ++dd) {
+            const float* d = dirs[dd];
+            float* row = J[nr + dd];
+            memset(row, 0, sizeof(float) * n);
+            cross3(r, d, row);
+            row[3] = d[0]; row[4] = d[1]; row[5] = d[2];
+            for (int l = 1; l <= md->depth[b]; ++l) {
+                int a = md->chain[b * LGS_MAX_DEPTH + l];
+                int j = md->dof[a];
+                if (j < 0) continue;
+                float rp[3] = {pc[0] - K.p[a][0], pc[1] - K.p[a][1], pc[2] - K.p[a][2]}, t[3];
+                cross3(K.aw[a], rp, t);
+                row[6 + j] = dot3(d, t);
+            }
+        }
+        tgt[nr] = sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp->max_depenetration_velocity);
+        tgt[nr + 1] = tgt[nr + 2] = 0.f;
+        kind[nr] = 0; kind[nr + 1] = 1; kind[nr + 2] = 2;
+        cb[nc] = b;
+        memcpy(cpt[nc], pc, 12);
+        nr += 3;
+        ++nc;
+    }
+    /* Y = L^-1 J^T ; A = Y^T Y ; v = J qf */
+    static __thread float Y[ROWMAX][NMAX];
+    static __thread float A[ROWMAX][ROWMAX];
+    for (int r = 0; r < nr; ++r) {
+        memcpy(Y[r], J[r], sizeof(float) * n);
+        fwd_sub(M, n, Y[r]);
+        float s = 0.f;
+        for (int i = 0; i < n; ++i) s += J[r][i] * qf[i];
+        v[r] = s;
+        lam[r] = 0.f;
+    }
+    for (int r = 0; r < nr; ++r)
+        for (int s = 0; s <= r; ++s) {
+            float a = 0.f;
+            for (int i = 0; i < n; ++i) a += Y[r][i] * Y[s][i];
+            A[r][s] = A[s][r] = a;
+        }
+    for (int it = 0; it < sp->solver_iterations; ++it) {
+        for (int r = 0; r < nr; ++r) {
+            if (kind[r] == 0) {
+                float ln = fmaxf(0.f, lam[r] + (tgt[r] - v[r]) / (A[r][r] + 1e-9f));
+                float d = ln - lam[r];
+                lam[r] = ln;
+                if (d != 0.f) for (int s = 0; s < nr; ++s) v[s] += A[s][r] * d;
+            } else if (kind[r] == 1) {
+                float lim = mu * lam[r - 1];
+                float l1 = lam[r] - v[r] / (A[r][r] + 1e-9f);
+                float l2 = lam[r + 1] - v[r + 1] / (A[r + 1][r + 1] + 1e-9f);
+                float nrm = sqrtf(l1 * l1 + l2 * l2);
+                if (nrm > lim) {
+                    float s = nrm > 0.f ? lim / nrm : 0.f;
+                    l1 *= s; l2 *= s;
+                }
+                float d1 = l1 - lam[r], d2 = l2 - lam[r + 1];
+                lam[r] = l1; lam[r + 1] = l2;
+                for (int s = 0; s < nr; ++s) v[s] += A[s][r] * d1 + A[s][r + 1] * d2;
+            }
+        }
+    }
+    /* qd' = qf + L^-T (Y lambda) */
+    float z[NMAX];
+    for (int i = 0; i < n; ++i) {
+        float s = 0.f;
+        for (int r = 0; r < nr; ++r) s += Y[r][i] * lam[r];
+        z[i] = s;
+    }
+    bwd_sub(M, n, z);
+    float qn[NMAX];
+    for (int i = 0; i < n; ++i) qn[i] = qf[i] + z[i];
+    if (sp->clamp_joint_velocity)
+        for (int j = 0; j < D; ++j) {
+            float lim = md->dof_velocity[j];
+            if (lim > 0.f) qn[6 + j] = fminf(fmaxf(qn[6 + j], -lim), lim);
+        }
+    /* contact forces (last substep), world frame */
+    for (int b = 0; b < B; ++b) cforce[3 * b] = cforce[3 * b + 1] = cforce[3 * b + 2] = 0.f;
+    for (int c = 0; c < nc; ++c) {
+        int r = nlimit + 3 * c;
+        float* F = cforce + 3 * cb[c];
+        F[0] += lam[r + 1] / dt;
+        F[1] += lam[r + 2] / dt;
+        F[2] += lam[r] / dt;
+    }
+    (void)cpt;
+    /* integrate (semi-implicit Euler) */
+    for (int k = 0; k < 3; ++k) root13[k] += dt * qn[3 + k];
+    {
+        float* q = root13 + 3;
+        const float* w = qn;
+        float dq[4];
+        dq[0] = 0.5f * dt * (q[3] * w[0] + (w[1] * q[2] - w[2] * q[1]));
+        dq[1] = 0.5f * dt * (q[3] * w[1] + (w[2] * q[0] - w[0] * q[2]));
+        dq[2] = 0.5f * dt * (q[3] * w[2] + (w[0] * q[1] - w[1] * q[0]));
+        dq[3] = 0.5f * dt * (-(w[0] * q[0] + w[1] * q[1] + w[2] * q[2]));
+        float nn = 0.f;
+        for (int k = 0; k < 4; ++k) { q[k] += dq[k]; nn += q[k] * q[k]; }
+        nn = 1.f / sqrtf(nn);
+        for (int k = 0; k < 4; ++k) q[k] *= nn;
+    }
+    for (int j = 0; j < D; ++j) {
+        dofs[2 * j + 1] = qn[6 + j];
+        dofs[2 * j] += dt * qn[6 + j];
+    }
+    {
+        float R[9], c[3], wc[3];
+        quat_to_mat(root13 + 3, R);
+        matvec(R, md->com, c);
+        cross3(qn, c, wc);
+        for (int k = 0; k < 3; ++k) { root13[10 + k] = qn[k]; root13[7 + k] = qn[3 + k] + wc[k]; }
+    }
+}
+
+/* rigid_body_states [B][13] of one env from its state */
+void orc_body_states_env(const lgs_model_desc* md, const float* root13, const float* dofs, float* rbs) {
+    okin K;
+    fk(md, root13, dofs, &K);
+    const int B = md->num_bodies;
+    const float* O = K.p[0];
+    float w0[3] = {root13[10], root13[11], root13[12]};
+    float rc[3] = {K.cw[0][0] - O[0], K.cw[0][1] - O[1], K.cw[0][2] - O[2]}, t[3];
+    cross3(w0, rc, t);
+    float Vw[LGS_MAX_BODIES][3], Vv[LGS_MAX_BODIES][3];
+    Vw[0][0] = w0[0]; Vw[0][1] = w0[1]; Vw[0][2] = w0[2];
+    for (int k = 0; k < 3; ++k) Vv[0][k] = root13[7 + k] - t[k];
+    for (int b = 1; b < B; ++b) {
+        int P = md->parent[b], j = md->dof[b];
+        memcpy(Vw[b], Vw[P], 12); memcpy(Vv[b], Vv[P], 12);
+        if (j >= 0) {
+            float qd = dofs[2 * j + 1], r[3] = {K.p[b][0] - O[0], K.p[b][1] - O[1], K.p[b][2] - O[2]}, sv[3];
+            cross3(r, K.aw[b], sv);
+            for (int k = 0; k < 3; ++k) { Vw[b][k] += K.aw[b][k] * qd; Vv[b][k] += sv[k] * qd; }
+        }
+    }
+    for (int b = 0; b < B; ++b) {
+        float* o = rbs + 13 * b;
+        o[0] = K.p[b][0]; o[1] = K.p[b][1]; o[2] = K.p[b][2];
+        mat_to_quat(K.R[b], o + 3);
+        float r[3] = {K.cw[b][0] - O[0], K.cw[b][1] - O[1], K.cw[b][2] - O[2]}, wr[3];
+        cross3(Vw[b], r, wr);
+        for (int k = 0; k < 3; ++k) { o[7 + k] = Vv[b][k] + wr[k]; o[10 + k] = Vw[b][k]; }
+    }
+}
+
+/* ===================================================== post-physics ==== */
+
+/* isaacgym.torch_utils.quat_rotate_inverse, op order of the torch code */
+static void quat_rotate_inverse(const float q[4], const float v[3], float o[3]) {
+    float w = q[3];
+    float s = 2.0f * w * w - 1.0f;
+    float c[3];
+    cross3(q, v, c);
+    float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+    for (int k = 0; k < 3; ++k) o[k] = v[k] * s - c[k] * w * 2.0f + q[k] * d * 2.0f;
+}
+/* isaacgym.torch_utils.quat_apply */
+static void quat_apply(const float q[4], const float v[3], float o[3]) {
+    float t[3], u[3];
+    cross3(q, v, t);
+    t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
+    cross3(q, t, u);
+    for (int k = 0; k < 3; ++k) o[k] = v[k] + q[3] * t[k] + u[k];
+}
+/* legged_gym/utils/isaacgym_utils.py:11-29 */
+static void get_euler_xyz(const float q[4], float rpy[3]) {
+    float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+    float sinr = 2.0f * (qw * qx + qy * qz);
+    float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+    rpy[0] = atan2f(sinr, cosr);
+    float sinp = 2.0f * (qw * qy - qz * qx);
+    rpy[1] = fabsf(sinp) >= 1.f ? copysignf(LGS_PI_F / 2.0f, sinp) : asinf(sinp);
+    float siny = 2.0f * (qw * qz + qx * qy);
+    float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+    rpy[2] = atan2f(siny, cosy);
+}
+/* legged_gym/utils/math.py:15-19 (torch remainder semantics) */
+static float wrap_to_pi(float a) {
+    const float tp = 2.0f * LGS_PI_F;
+    float m = fmodf(a, tp);
+    if (m != 0.f && m < 0.f) m += tp;
+    if (m > LGS_PI_F) m -= tp;
+    return m;
+}
+static float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+typedef struct {
+    float* root; float* dofs; float* cforce; float* rbs;
+} ostate;
+
+/* _resample_commands (legged_robot.py:519-538) */
+static void resample_commands(const lgs_task_params* T, float* cmd, uint64_t seed, uint32_t env, uint32_t step,
+                              uint32_t stream) {
+    cmd[0] = rand_range(T->cmd_lin_vel_x[0], T->cmd_lin_vel_x[1], orc_uniform(seed, env, step, stream, 0));
+    cmd[1] = rand_range(T->cmd_lin_vel_y[0], T->cmd_lin_vel_y[1], orc_uniform(seed, env, step, stream, 1));
+    if (T->heading_command)
+        cmd[3] = rand_range(T->cmd_heading[0], T->cmd_heading[1], orc_uniform(seed, env, step, stream, 2));
+    else
+        cmd[2] = rand_range(T->cmd_ang_vel_yaw[0], T->cmd_ang_vel_yaw[1], orc_uniform(seed, env, step, stream, 2));
+    float nrm = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+    float keep = nrm > 0.2f ? 1.f : 0.f;
+    cmd[0] *= keep; cmd[1] *= keep;
+}
+
+/* reward terms (legged_robot.py:843-939, h1_env.py:98-123) */
+static float reward_term(int id, const lgs_task_params* T, int A, const float* bl, const float* ba, const float* pg,
+                         const float* root, const float* q, const float* qd, const float* last_qd, const float* act,
+                         const float* last_act, const float* tau, const float* cf, const float* cmd,
+                         float* air, uint8_t* last_c, const float* rbs, const float* leg_phase, int reset, int timeout) {
+    float s = 0.f;
+    switch (id) {
+    case LGS_REW_LIN_VEL_Z: return bl[2] * bl[2];
+    case LGS_REW_ANG_VEL_XY: return ba[0] * ba[0] + ba[1] * ba[1];
+    case LGS_REW_ORIENTATION: return pg[0] * pg[0] + pg[1] * pg[1];
+    case LGS_REW_BASE_HEIGHT: { float d = root[2] - T->base_height_target; return d * d; }
+    case LGS_REW_TORQUES: for (int j = 0; j < A; ++j) s += tau[j] * tau[j]; return s;
+    case LGS_REW_DOF_VEL: for (int j = 0; j < A; ++j) s += qd[j] * qd[j]; return s;
+    case LGS_REW_DOF_ACC:
+        for (int j = 0; j < A; ++j) { float d = (last_qd[j] - qd[j]) / T->control_dt; s += d * d; }
+        return s;
+    case LGS_REW_ACTION_RATE:
+        for (int j = 0; j < A; ++j) { float d = last_act[j] - act[j]; s += d * d; }
+        return s;
+    case LGS_REW_COLLISION:
+        for (int i = 0; i < T->num_penalised; ++i) {
+            const float* F = cf + 3 * T->penalised_idx[i];
+            s += (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 0.1f) ? 1.f : 0.f;
+        }
+        return s;
+    case LGS_REW_DOF_POS_LIMITS:
+        for (int j = 0; j < A; ++j) {
+            float o = -fminf(q[j] - T->soft_dof_pos_lower[j], 0.f);
+            o += fmaxf(q[j] - T->soft_dof_pos_upper[j], 0.f);
+            s += o;
+        }
+        return s;
+    case LGS_REW_DOF_VEL_LIMITS:
+        for (int j = 0; j < A; ++j)
+            s += clipf(fabsf(qd[j]) - T->dof_vel_limits[j] * T->soft_dof_vel_limit, 0.f, 1.f);
+        return s;
+    case LGS_REW_TORQUE_LIMITS:
+        for (int j = 0; j < A; ++j) s += fmaxf(fabsf(tau[j]) - T->torque_limits[j] * T->soft_torque_limit, 0.f);
+        return s;
+    case LGS_REW_TRACKING_LIN_VEL: {
+        float e0 = cmd[0] - bl[0], e1 = cmd[1] - bl[1];
+        float e = e0 * e0 + e1 * e1;
+        return expf(-e / T->tracking_sigma);
+    }
+    case LGS_REW_TRACKING_ANG_VEL: {
+        float e = cmd[2] - ba[2];
+        e = e * e;
+        return expf(-e / T->tracking_sigma);
+    }
+    case LGS_REW_FEET_AIR_TIME: { /* legged_robot.py:912-923, mutates air/last_c */
+        float r = 0.f;
+        int filt[LGS_MAX_FEET];
+        for (int f = 0; f < T->num_feet; ++f) {
+            int contact = cf[3 * T->feet_idx[f] + 2] > 1.f;
+            filt[f] = contact || last_c[f];
+            last_c[f] = (uint8_t)contact;
+            float first = (air[f] > 0.f && filt[f]) ? 1.f : 0.f;
+            air[f] += T->control_dt;
+            r += (air[f] - 0.5f) * first;
+        }
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+        r *= (cn > 0.1f) ? 1.f : 0.f;
+        for (int f = 0; f < T->num_feet; ++f)
+            if (filt[f]) air[f] = 0.f; /* feet_air_time *= ~contact_filt */
+        return r;
+    }
+    case LGS_REW_FEET_STUMBLE: {
+        for (int f = 0; f < T->num_feet; ++f) {
+            const float* F = cf + 3 * T->feet_idx[f];
+            if (sqrtf(F[0] * F[0] + F[1] * F[1]) > 5.f * fabsf(F[2])) return 1.f;
+        }
+        return 0.f;
+    }
+    case LGS_REW_STAND_STILL: {
+        for (int j = 0; j < A; ++j) s += fabsf(q[j] - T->default_dof_pos[j]);
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+        return s * ((cn < 0.1f) ? 1.f : 0.f);
+    }
+    case LGS_REW_FEET_CONTACT_FORCES:
+        for (int f = 0; f < T->num_feet; ++f) {
+            const float* F = cf + 3 * T->feet_idx[f];
+            s += fmaxf(sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) - T->max_contact_force, 0.f);
+        }
+        return s;
+    case LGS_REW_ALIVE: return 1.0f;
+    case LGS_REW_CONTACT: /* h1_env.py:98-105 */
+        for (int f = 0; f < T->num_feet; ++f) {
+            int stance = leg_phase[f] < T->stance_threshold;
+            int contact = cf[3 * T->feet_idx[f] + 2] > 1.f;
+            s += (contact == stance) ? 1.f : 0.f;
+        }
+        return s;
+    case LGS_REW_FEET_SWING_HEIGHT: /* h1_env.py:107-110 */
+        for (int f = 0; f < T->num_feet; ++f) {
+            const float* F = cf + 3 * T->feet_idx[f];
+            int contact = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f;
+            float d = rbs[13 * T->feet_idx[f] + 2] - T->swing_height_target;
+            s += d * d * (contact ? 0.f : 1.f);
+        }
+        return s;
+    case LGS_REW_CONTACT_NO_VEL: /* h1_env.py:115-119 */
+        for (int f = 0; f < T->num_feet; ++f) {
+            const float* F = cf + 3 * T->feet_idx[f];
+            float c = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f ? 1.f : 0.f;
+            const float* v = rbs + 13 * T->feet_idx[f] + 7;
+            for (int k = 0; k < 3; ++k) { float x = v[k] * c; s += x * x; }
+        }
+        return s;
+    case LGS_REW_HIP_POS: /* h1_env.py:121-123 */
+        for (int i = 0; i < T->num_hip; ++i) s += q[T->hip_dofs[i]] * q[T->hip_dofs[i]];
+        return s;
+    default: return 0.f;
+    }
+    (void)reset; (void)timeout;
+}
+
+/* _compute_torques (legged_robot.py:649-671), P/V/T control */
+static void compute_torques(const lgs_task_params* T, int D, const float* act, const float* dofs,
+                            const float* last_qd, float sim_dt, float* tau) {
+    for (int j = 0; j < D; ++j) {
+        float as = act[j] * T->action_scale;
+        float q = dofs[2 * j], qd = dofs[2 * j + 1], t;
+        if (T->control_type == 0)
+            t = T->p_gains[j] * (as + T->default_dof_pos[j] - q) - T->d_gains[j] * qd;
+        else if (T->control_type == 1)
+            t = T->p_gains[j] * (as - qd) - T->d_gains[j] * (qd - last_qd[j]) / sim_dt;
+        else
+            t = as;
+        tau[j] = clipf(t, -T->torque_limits[j], T->torque_limits[j]);
+    }
+}
+
+/* post_physics_step (legged_robot.py:673-709) for env e, state already simulated.
+ * `full` = 1 runs the whole stack incl. reset/push; feet rigid states must be
+ * current in st->rbs for humanoid layouts. */
+void orc_post_physics_env(const lgs_model_desc* md, const lgs_task_params* T, int N, int e, ostate* st,
+                          const lgs_env_buffers* E, int64_t step_counter) {
+    const int D = md->num_dofs, B = md->num_bodies, A = T->num_actions;
+    const int O = T->num_obs, P = T->num_privileged_obs;
+    const uint64_t seed = T->seed;
+    const uint32_t step = (uint32_t)step_counter;
+    float* root = st->root + 13 * e;
+    float* dofs = st->dofs + 2 * D * e;
+    const float* cf = st->cforce + 3 * B * e;
+    const float* rbs = st->rbs ? st->rbs + 13 * B * e : NULL;
+    float* cmd = E->commands + 4 * e;
+    float* act = E->actions + A * e;
+    float* last_act = E->last_actions + A * e;
+    float* last_qd = E->last_dof_vel + D * e;
+    float* air = E->feet_air_time + T->num_feet * e;
+    uint8_t* lastc = E->last_contacts + T->num_feet * e;
+    int64_t* ep = E->episode_length + e;
+    float* tau = E->torques + D * e;
+
+    *ep += 1;                                                       /* :681 */
+    float bl[3], ba[3], pg[3], rpy[3];
+    const float g[3] = {0.f, 0.f, -1.f};
+    quat_rotate_inverse(root + 3, root + 7, bl);                    /* :688 */
+    quat_rotate_inverse(root + 3, root + 10, ba);                   /* :689 */
+    quat_rotate_inverse(root + 3, g, pg);                           /* :690 */
+    get_euler_xyz(root + 3, rpy);                                   /* :687 */
+    float phase = 0.f, leg_phase[2] = {0.f, 0.f};
+    if (T->obs_layout == LGS_OBS_HUMANOID) {                        /* h1_env.py:58-63 */
+        float t = (float)(*ep) * T->control_dt;
+        phase = fmodf(t, T->phase_period);
+        if (phase != 0.f && phase < 0.f) phase += T->phase_period;
+        phase = phase / T->phase_period;
+        leg_phase[0] = phase;
+        float pr = fmodf(phase + T->phase_offset, 1.0f);
+        if (pr != 0.f && pr < 0.f) pr += 1.0f;
+        leg_phase[1] = pr;
+    }
+    /* _post_physics_step_callback (:511-516) */
+    if ((*ep) % T->resample_interval == 0) resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_CMD);
+    if (T->heading_command) {
+        const float fx[3] = {1.f, 0.f, 0.f};
+        float fwd[3];
+        quat_apply(root + 3, fx, fwd);
+        float heading = atan2f(fwd[1], fwd[0]);
+        cmd[2] = clipf(0.5f * wrap_to_pi(cmd[3] - heading), -1.f, 1.f);
+    }
+    /* check_termination (:711-721) */
+    int reset = 0;
+    for (int i = 0; i < T->num_termination; ++i) {
+        const float* F = cf + 3 * T->termination_idx[i];
+        if (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f) reset = 1;
+    }
+    if (fabsf(rpy[1]) > 1.0f || fabsf(rpy[0]) > 0.8f) reset = 1;
+    int timeout = (float)(*ep) > T->max_episode_length;
+    reset |= timeout;
+    /* compute_reward (:770-787) */
+    float q[LGS_MAX_DOFS], qd[LGS_MAX_DOFS];
+    for (int j = 0; j < D; ++j) { q[j] = dofs[2 * j]; qd[j] = dofs[2 * j + 1]; }
+    float rew = 0.f;
+    for (int k = 0; k < T->num_rewards; ++k) {
+        float r = reward_term(T->reward_ids[k], T, A, bl, ba, pg, root, q, qd, last_qd, act, last_act, tau, cf, cmd,
+                              air, lastc, rbs, leg_phase, reset, timeout) * T->reward_scales[k];
+        rew += r;
+        E->episode_sums[(size_t)k * N + e] += r;
+        if (E->rew_terms) E->rew_terms[(size_t)k * N + e] = r;
+    }
+    if (T->only_positive_rewards) rew = fmaxf(rew, 0.f);
+    if (T->has_termination_reward) {
+        float r = ((reset && !timeout) ? 1.f : 0.f) * T->termination_scale;
+        rew += r;
+        E->episode_sums[(size_t)T->num_rewards * N + e] += r;
+    }
+    E->rew[e] = rew;
+    E->reset[e] = (uint8_t)reset;
+    E->time_out[e] = (uint8_t)timeout;
+    /* reset_idx (:723-768) */
+    if (reset) {
+        for (int j = 0; j < D; ++j) {                              /* _reset_dofs :566-567 */
+            dofs[2 * j] = T->default_dof_pos[j] * rand_range(0.5f, 1.5f, orc_uniform(seed, e, step, LGS_STREAM_RESET_DOF, j));
+            dofs[2 * j + 1] = 0.f;
+        }
+        for (int k = 0; k < 13; ++k) root[k] = T->base_init_state[k];  /* _reset_root_states :587-590 */
+        for (int k = 0; k < 3; ++k) root[k] += E->env_origins[3 * e + k];
+        for (int k = 0; k < 6; ++k) root[7 + k] = rand_range(-0.5f, 0.5f, orc_uniform(seed, e, step, LGS_STREAM_RESET_ROOT, k));
+        resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_RESET_CMD);
+        for (int j = 0; j < A; ++j) { act[j] = 0.f; last_act[j] = 0.f; }
+        for (int j = 0; j < D; ++j) last_qd[j] = 0.f;
+        for (int f = 0; f < T->num_feet; ++f) air[f] = 0.f;
+        *ep = 0;
+        int nsum = T->num_rewards + (T->has_termination_reward ? 1 : 0);
+        for (int k = 0; k < nsum; ++k) {
+            E->episode_acc[k] += E->episode_sums[(size_t)k * N + e];
+            E->episode_sums[(size_t)k * N + e] = 0.f;
+        }
+        E->episode_acc[nsum] += 1.f;
+    }
+    /* _push_robots (:540-555): envs with ep_len % interval == 0, incl. just-reset ones */
+    if (T->push_robots && (*ep) % T->push_interval == 0) {
+        root[7] = rand_range(-T->max_push_vel_xy, T->max_push_vel_xy, orc_uniform(seed, e, step, LGS_STREAM_PUSH, 0));
+        root[8] = rand_range(-T->max_push_vel_xy, T->max_push_vel_xy, orc_uniform(seed, e, step, LGS_STREAM_PUSH, 1));
+    }
+    /* compute_observations (:800-811 / h1_env.py:70-95); q/qd/actions/commands post-reset */
+    float* ob = E->obs + (size_t)O * e;
+    float* pr = P > 0 && E->priv_obs ? E->priv_obs + (size_t)P * e : NULL;
+    float tmp[LGS_MAX_OBS];
+    int k = 0;
+    if (T->obs_layout == LGS_OBS_QUADRUPED) {
+        for (int i = 0; i < 3; ++i) tmp[k++] = bl[i] * T->obs_scale_lin_vel;
+    }
+    for (int i = 0; i < 3; ++i) tmp[k++] = ba[i] * T->obs_scale_ang_vel;
+    for (int i = 0; i < 3; ++i) tmp[k++] = pg[i];
+    for (int i = 0; i < 3; ++i) tmp[k++] = cmd[i] * T->commands_scale[i];
+    for (int j = 0; j < D; ++j) tmp[k++] = (dofs[2 * j] - T->default_dof_pos[j]) * T->obs_scale_dof_pos;
+    for (int j = 0; j < D; ++j) tmp[k++] = dofs[2 * j + 1] * T->obs_scale_dof_vel;
+    for (int j = 0; j < A; ++j) tmp[k++] = act[j];
+    if (T->obs_layout == LGS_OBS_HUMANOID) {
+        float ph = 2.0f * LGS_PI_F * phase;
+        tmp[k++] = sinf(ph);
+        tmp[k++] = cosf(ph);
+        if (pr) {
+            for (int i = 0; i < 3; ++i) pr[i] = clipf(bl[i] * T->obs_scale_lin_vel, -T->clip_observations, T->clip_observations);
+            for (int i = 0; i < k; ++i) pr[3 + i] = clipf(tmp[i], -T->clip_observations, T->clip_observations);
+        }
+    }
+    for (int i = 0; i < O; ++i) {
+        float x = tmp[i];
+        if (T->add_noise) x += (2.f * orc_uniform(seed, e, step, LGS_STREAM_NOISE, i) - 1.f) * T->noise_vec[i];
+        ob[i] = clipf(x, -T->clip_observations, T->clip_observations);
+    }
+    /* diagnostics buffers mirrored for the python attributes */
+    for (int i = 0; i < 3; ++i) {
+        E->base_lin_vel[3 * e + i] = bl[i];
+        E->base_ang_vel[3 * e + i] = ba[i];
+        E->projected_gravity[3 * e + i] = pg[i];
+        E->rpy[3 * e + i] = rpy[i];
+    }
+    if (E->phase) E->phase[e] = phase;
+    if (E->leg_phase) { E->leg_phase[2 * e] = leg_phase[0]; E->leg_phase[2 * e + 1] = leg_phase[1]; }
+    /* bookkeeping (:707-709) */
+    for (int j = 0; j < A; ++j) last_act[j] = act[j];
+    for (int j = 0; j < D; ++j) last_qd[j] = dofs[2 * j + 1];
+    for (int i = 0; i < 6; ++i) E->last_root_vel[6 * e + i] = root[7 + i];
+}
+
+/* ====================================================== entry points === */
+
+/* one substep for all envs (lgs_simulate) */
+void orc_simulate(const lgs_model_desc* md, const lgs_sim_params* sp, int N, float* root, float* dofs,
+                  const float* tau, float* cforce, float* rbs, const float* added_mass, const float* friction) {
+    const int B = md->num_bodies, D = md->num_dofs;
+#pragma omp parallel for schedule(static)
+    for (int e = 0; e < N; ++e) {
+        orc_substep_env(md, sp, root + 13 * e, dofs + 2 * D * e, tau + D * e, cforce + 3 * B * e,
+                        added_mass ? added_mass[e] : 0.f, friction ? friction[e] : 1.f);
+        if (rbs) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
+    }
+}
+
+/* the fused control step (LeggedRobot.step, legged_robot.py:615-647) for all envs */
+void orc_step(const lgs_model_desc* md, const lgs_sim_params* sp, const lgs_task_params* T, int N, float* root,
+              float* dofs, float* cforce, float* rbs, const float* added_mass, const float* friction,
+              const lgs_env_buffers* E, int64_t step_counter) {
+    const int B = md->num_bodies, D = md->num_dofs, A = T->num_actions;
+#pragma omp parallel for schedule(static)
+    for (int e = 0; e < N; ++e) {
+        float* act = E->actions + A * e;
+        for (int j = 0; j < A; ++j) act[j] = clipf(act[j], -T->clip_actions, T->clip_actions); /* :623-624 */
+        for (int s = 0; s < T->decimation; ++s) {                      /* :627-639 */
+            compute_torques(T, D, act, dofs + 2 * D * e, E->last_dof_vel + D * e, sp->dt, E->torques + D * e);
+            orc_substep_env(md, sp, root + 13 * e, dofs + 2 * D * e, E->torques + D * e, cforce + 3 * B * e,
+                            added_mass ? added_mass[e] : 0.f, friction ? friction[e] : 1.f);
+        }
+        if (rbs) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
+        ostate st = {root, dofs, cforce, rbs};
+        orc_post_physics_env(md, T, N, e, &st, E, step_counter);
+    }
+}
+
+/* post-physics only (golden-vector tests): torques already in E->torques */
+void orc_post_physics(const lgs_model_desc* md, const lgs_task_params* T, int N, float* root, float* dofs,
+                      float* cforce, float* rbs, const lgs_env_buffers* E, int64_t step_counter) {
+    for (int e = 0; e < N; ++e) {
+        ostate st = {root, dofs, cforce, rbs};
+        orc_post_physics_env(md, T, N, e, &st, E, step_counter);
+    }
+}
+
+void orc_compute_torques(const lgs_task_params* T, int N, int D, const float* act, const float* dofs,
+                         const float* last_qd, float sim_dt, float* tau) {
+    for (int e = 0; e < N; ++e) compute_torques(T, D, act + D * e, dofs + 2 * D * e, last_qd + D * e, sim_dt, tau + D * e);
+}

@@ -1,0 +1,1415 @@
+// leggedsim.hip — MI355X (gfx950) implementation of include/leggedsim.h.
+//
+// One wavefront (a 64-thread workgroup) owns one env.  The env's articulated
+// state lives in LDS for the whole control step: `decimation` physics substeps
+// and the post-physics stack run inside ONE launch, lanes spread over bodies,
+// DOFs, constraint rows and observation entries.  HBM sees each env's state
+// once in and once out per control step (SURVEY §8d algorithmic bytes).
+//
+// Substep (same algorithm as oracle/lgs_oracle.c, part B):
+//   FK (lane per body, walks its own chain)  ->  spatial inertia / motion
+//   subspace / RNEA bias per body  ->  subtree sums (lane per body, contiguous
+//   DFS ranges)  ->  mass matrix (lane per lower-triangle entry) + bias  ->
+//   left-looking Cholesky (lane per row)  ->  free velocity  ->  joint-limit and
+//   contact rows (ballot compaction)  ->  Y = L^-1 J^T (lane per row)  ->
+//   A = Y^T Y  ->  projected Gauss-Seidel (row owner lanes, readlane
+//   broadcasts)  ->  qd' = qf + L^-T Y lambda  ->  integrate.
+// Post-physics (legged_robot.py:673-709): lane 0 runs the scalar stack in the
+// reference's order; observation/noise/reset draws are spread over lanes.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/leggedsim.h"
+
+#define MAXB LGS_MAX_BODIES
+#define MAXD LGS_MAX_DEPTH
+#define WAVE 64
+
+// ------------------------------------------------------------------ errors --
+static thread_local std::string g_err;
+static int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIP_TRY(x)                                                                        \
+    do {                                                                                  \
+        hipError_t _e = (x);                                                              \
+        if (_e != hipSuccess) return set_err(LGS_ERR_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// ------------------------------------------------------------ device math --
+struct DevModel {
+    int B, D, P;
+    const int* parent;
+    const int* dof;
+    const int* subtree_end;
+    const int* depth;
+    const int* chain;
+    const float* joint_rot;
+    const float* joint_pos;
+    const float* axis;
+    const float* mass;
+    const float* com;
+    const float* inertia;
+    const float* dof_lower;
+    const float* dof_upper;
+    const float* dof_velocity;
+    const int* pt_body;
+    const float* pt_pos;
+    const float* pt_radius;
+};
+
+struct DevSim {
+    float dt, gx, gy, gz;
+    int iters;
+    float contact_offset, rest_offset, max_depen, beta, ground_friction, armature;
+    int clamp_qd, max_contacts, max_rows;
+};
+
+struct DevState {
+    float* root;     // [N,13]
+    float* dofs;     // [N,D,2]
+    float* cforce;   // [N,B,3]
+    float* rbs;      // [N,B,13]
+    const float* friction;    // [N]
+    const float* added_mass;  // [N]
+    const float* torques_in;  // [N,D] (lgs_simulate)
+};
+
+__device__ __forceinline__ float rl(float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+__device__ __forceinline__ int rli(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
+__device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
+    float x = a[1] * b[2] - a[2] * b[1];
+    float y = a[2] * b[0] - a[0] * b[2];
+    float z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void matvec(const float* R, const float* v, float* o) {
+    float x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    float y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    float z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ void matmul(const float* A, const float* B, float* C) {
+    float T[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = T[i];
+}
+__device__ __forceinline__ void quat_to_mat(const float* q, float* R) {
+    float x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void mat_to_quat(const float* R, float* q) {
+    float tr = R[0] + R[4] + R[8];
+    if (tr > 0.f) {
+        float s = sqrtf(tr + 1.f) * 2.f;
+        q[3] = 0.25f * s; q[0] = (R[7] - R[5]) / s; q[1] = (R[2] - R[6]) / s; q[2] = (R[3] - R[1]) / s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        float s = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f;
+        q[3] = (R[7] - R[5]) / s; q[0] = 0.25f * s; q[1] = (R[1] + R[3]) / s; q[2] = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        float s = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f;
+        q[3] = (R[2] - R[6]) / s; q[0] = (R[1] + R[3]) / s; q[1] = 0.25f * s; q[2] = (R[5] + R[7]) / s;
+    } else {
+        float s = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f;
+        q[3] = (R[3] - R[1]) / s; q[0] = (R[2] + R[6]) / s; q[1] = (R[5] + R[7]) / s; q[2] = 0.25f * s;
+    }
+}
+__device__ __forceinline__ void axis_angle(const float* a, float ang, float* R) {
+    float s, c;
+    sincosf(ang, &s, &c);
+    float t = 1.f - c;
+    float x = a[0], y = a[1], z = a[2];
+    R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
+    R[3] = t * x * y + s * z; R[4] = t * y * y + c;     R[5] = t * y * z - s * x;
+    R[6] = t * x * z - s * y; R[7] = t * y * z + s * x; R[8] = t * z * z + c;
+}
+// spatial inertia (m, h, I6) applied to motion (w, v) -> force (n, f)
+__device__ __forceinline__ void sin_apply(float m, const float* h, const float* I, const float* w, const float* v,
+                                          float* n, float* f) {
+    float Iw0 = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
+    float Iw1 = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
+    float Iw2 = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
+    float hv[3], hw[3];
+    cross3(h, v, hv);
+    cross3(h, w, hw);
+    n[0] = Iw0 + hv[0]; n[1] = Iw1 + hv[1]; n[2] = Iw2 + hv[2];
+    f[0] = m * v[0] - hw[0]; f[1] = m * v[1] - hw[1]; f[2] = m * v[2] - hw[2];
+}
+
+// ----------------------------------------------------------- Philox RNG --
+__host__ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
+                                                         uint32_t c3) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return (float)(c0 >> 8) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float rand_range(float lo, float hi, float u) { return (hi - lo) * u + lo; }
+__device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// ------------------------------------------------------------ LDS layout --
+template <int D, int B, int ROWS>
+struct Smem {
+    static constexpr int n = 6 + D;
+    static constexpr int NP = (n % 2 == 0) ? n + 1 : n;     // odd row stride: conflict-free columns
+    static constexpr int AS = (ROWS % 2 == 0) ? ROWS + 1 : ROWS;
+    float root[16];
+    float q[D], qd[D], tau[D], act[D];
+    float R[B][9], p[B][3], aw[B][3], cw[B][3];
+    union {
+        struct {
+            float Sw[B][3], Sv[B][3];
+            float m[B], h[B][3], I[B][6];
+            float fn[B][3], ff[B][3];
+            float cm[B], ch[B][3], cI[B][6];
+            float Fn[B][3], Ff[B][3];
+        } dyn;
+        struct {
+            float Y[ROWS][NP];
+            float A[ROWS][AS];
+        } con;
+    } u;
+    float M[n][NP];
+    float qf[n];
+    float tgt[ROWS];
+    int kind[ROWS];
+    int c_body[ROWS / 3];
+    float c_pt[ROWS / 3][3];
+    float c_sep[ROWS / 3];
+    float cf[B][3];
+    // post-physics scratch
+    float obs_tmp[LGS_MAX_OBS];
+    float misc[32];
+    int flags[8];
+};
+
+// -------------------------------------------------------------- substep --
+// One physics substep of this block's env.  Preconditions: s.root/q/qd/tau hold
+// the state and the torques.  Postcondition: state integrated, s.cf = contact
+// forces of this substep.  All 64 lanes must call it.
+template <int D, int B, int ROWS>
+__device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& sp, float added_mass, float shape_mu) {
+    constexpr int n = 6 + D;
+    constexpr int NP = Smem<D, B, ROWS>::NP;
+    constexpr int AS = Smem<D, B, ROWS>::AS;
+    const int lane = threadIdx.x;
+    const float dt = sp.dt;
+
+    // ---- 1. forward kinematics: lane b walks root..b
+    if (lane < B) {
+        float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
+        quat_to_mat(s.root + 3, R);
+        p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
+        const int d = md.depth[lane];
+        for (int l = 1; l <= d; ++l) {
+            const int a = md.chain[lane * MAXD + l];
+            float Rj[9], t[3];
+            matmul(R, md.joint_rot + 9 * a, Rj);
+            matvec(R, md.joint_pos + 3 * a, t);
+            p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
+            const int j = md.dof[a];
+            if (j >= 0) {
+                if (l == d) matvec(Rj, md.axis + 3 * a, aw);
+                float Ra[9];
+                axis_angle(md.axis + 3 * a, s.q[j], Ra);
+                matmul(Rj, Ra, R);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) R[k] = Rj[k];
+            }
+        }
+        float c[3];
+        matvec(R, md.com + 3 * lane, c);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            s.p[lane][k] = p[k];
+            s.aw[lane][k] = aw[k];
+            s.cw[lane][k] = p[k] + c[k];
+        }
+    }
+    __syncthreads();
+    const float O[3] = {s.p[0][0], s.p[0][1], s.p[0][2]};
+    float w0[3] = {s.root[10], s.root[11], s.root[12]};
+    float vO[3];
+    {
+        float rc[3] = {s.cw[0][0] - O[0], s.cw[0][1] - O[1], s.cw[0][2] - O[2]}, wxr[3];
+        cross3(w0, rc, wxr);
+        vO[0] = s.root[7] - wxr[0]; vO[1] = s.root[8] - wxr[1]; vO[2] = s.root[9] - wxr[2];
+    }
+    // ---- 2. per-body spatial inertia at O and motion subspace
+    if (lane < B) {
+        float m = md.mass[lane], scale = 1.f;
+        if (lane == 0 && added_mass != 0.f && m > 0.f) { scale = (m + added_mass) / m; m = m + added_mass; }
+        const float* Il = md.inertia + 6 * lane;
+        float IL[9] = {Il[0] * scale, Il[3] * scale, Il[4] * scale, Il[3] * scale, Il[1] * scale,
+                       Il[5] * scale, Il[4] * scale, Il[5] * scale, Il[2] * scale};
+        float R[9], Rt[9], T[9], Iw[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = s.R[lane][k];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Rt[3 * i + j] = R[3 * j + i];
+        matmul(R, IL, T);
+        matmul(T, Rt, Iw);
+        float r[3] = {s.cw[lane][0] - O[0], s.cw[lane][1] - O[1], s.cw[lane][2] - O[2]};
+        float rr = dot3(r, r);
+        s.u.dyn.m[lane] = m;
+        s.u.dyn.h[lane][0] = m * r[0]; s.u.dyn.h[lane][1] = m * r[1]; s.u.dyn.h[lane][2] = m * r[2];
+        s.u.dyn.I[lane][0] = Iw[0] + m * (rr - r[0] * r[0]);
+        s.u.dyn.I[lane][1] = Iw[4] + m * (rr - r[1] * r[1]);
+        s.u.dyn.I[lane][2] = Iw[8] + m * (rr - r[2] * r[2]);
+        s.u.dyn.I[lane][3] = Iw[1] - m * r[0] * r[1];
+        s.u.dyn.I[lane][4] = Iw[2] - m * r[0] * r[2];
+        s.u.dyn.I[lane][5] = Iw[5] - m * r[1] * r[2];
+        float rp[3] = {s.p[lane][0] - O[0], s.p[lane][1] - O[1], s.p[lane][2] - O[2]}, sv[3];
+        float a[3] = {s.aw[lane][0], s.aw[lane][1], s.aw[lane][2]};
+        cross3(rp, a, sv);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { s.u.dyn.Sw[lane][k] = a[k]; s.u.dyn.Sv[lane][k] = sv[k]; }
+    }
+    __syncthreads();
+    // ---- 3. velocity + bias acceleration down the chain, bias force per body
+    if (lane < B) {
+        float Vw[3] = {w0[0], w0[1], w0[2]}, Vv[3] = {vO[0], vO[1], vO[2]};
+        float Aw[3] = {0.f, 0.f, 0.f}, Av[3] = {-sp.gx, -sp.gy, -sp.gz};
+        const int d = md.depth[lane];
+        for (int l = 1; l <= d; ++l) {
+            const int a = md.chain[lane * MAXD + l];
+            const int j = md.dof[a];
+            if (j < 0) continue;
+            const float qd = s.qd[j];
+            float sw[3] = {s.u.dyn.Sw[a][0] * qd, s.u.dyn.Sw[a][1] * qd, s.u.dyn.Sw[a][2] * qd};
+            float sv[3] = {s.u.dyn.Sv[a][0] * qd, s.u.dyn.Sv[a][1] * qd, s.u.dyn.Sv[a][2] * qd};
+            float t1[3], t2[3], t3[3];
+            cross3(Vw, sw, t1);
+            cross3(Vw, sv, t2);
+            cross3(Vv, sw, t3);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                Aw[k] += t1[k];
+                Av[k] += t2[k] + t3[k];
+                Vw[k] += sw[k];
+                Vv[k] += sv[k];
+            }
+        }
+        const float m = s.u.dyn.m[lane];
+        float h[3] = {s.u.dyn.h[lane][0], s.u.dyn.h[lane][1], s.u.dyn.h[lane][2]};
+        float I[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) I[k] = s.u.dyn.I[lane][k];
+        float IAn[3], IAf[3], IVn[3], IVf[3], a1[3], a2[3], a3[3];
+        sin_apply(m, h, I, Aw, Av, IAn, IAf);
+        sin_apply(m, h, I, Vw, Vv, IVn, IVf);
+        cross3(Vw, IVn, a1);
+        cross3(Vv, IVf, a2);
+        cross3(Vw, IVf, a3);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            s.u.dyn.fn[lane][k] = IAn[k] + a1[k] + a2[k];
+            s.u.dyn.ff[lane][k] = IAf[k] + a3[k];
+        }
+    }
+    __syncthreads();
+    // ---- 4. subtree (composite) sums: lane b adds the contiguous DFS range.
+    // Summation order mirrors the oracle's leaf-to-root accumulation.
+    if (lane < B) {
+        // oracle: for b = B-1..1: Ic[parent] += Ic[b]  -> per node the children are
+        // added in descending child order, each child's value already complete.
+        // A descending scan of the subtree with a per-node stack reproduces that;
+        // for simplicity we recompute composite values with the same recursion
+        // bottom-up per lane (trees here are <= 32 nodes).
+        const int end = md.subtree_end[lane];
+        float cm = 0.f, ch[3] = {0.f, 0.f, 0.f}, cI[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float Fn[3] = {0.f, 0.f, 0.f}, Ff[3] = {0.f, 0.f, 0.f};
+        for (int k = end - 1; k >= lane; --k) {
+            cm += s.u.dyn.m[k];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) { ch[t] += s.u.dyn.h[k][t]; Fn[t] += s.u.dyn.fn[k][t]; Ff[t] += s.u.dyn.ff[k][t]; }
+#pragma unroll
+            for (int t = 0; t < 6; ++t) cI[t] += s.u.dyn.I[k][t];
+        }
+        s.u.dyn.cm[lane] = cm;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) { s.u.dyn.ch[lane][t] = ch[t]; s.u.dyn.Fn[lane][t] = Fn[t]; s.u.dyn.Ff[lane][t] = Ff[t]; }
+#pragma unroll
+        for (int t = 0; t < 6; ++t) s.u.dyn.cI[lane][t] = cI[t];
+    }
+    __syncthreads();
+    // ---- 5. mass matrix (lower triangle) and rhs = tau - C
+    for (int idx = lane; idx < n * (n + 1) / 2; idx += WAVE) {
+        int r = (int)((sqrtf(8.f * idx + 1.f) - 1.f) * 0.5f);
+        while ((r + 1) * (r + 2) / 2 <= idx) ++r;
+        while (r * (r + 1) / 2 > idx) --r;
+        const int c = idx - r * (r + 1) / 2;  // r >= c
+        float val;
+        if (r < 6) {  // base-base block of the root composite
+            const float* I = s.u.dyn.cI[0];
+            const float* h = s.u.dyn.ch[0];
+            if (r < 3) {  // c < 3
+                const int m3[9] = {0, 3, 4, 3, 1, 5, 4, 5, 2};
+                val = I[m3[3 * r + c]];
+            } else if (c < 3) {  // row 3+i, col c : [h]x^T (i, c) = [h]x (c, i)
+                const int i = r - 3;
+                const float H[9] = {0, -h[2], h[1], h[2], 0, -h[0], -h[1], h[0], 0};
+                val = H[3 * c + i];
+            } else {
+                val = (r == c) ? s.u.dyn.cm[0] : 0.f;
+            }
+        } else {
+            const int j = r - 6;
+            int bj = -1;
+            for (int b = 1; b < B; ++b) if (md.dof[b] == j) bj = b;
+            float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
+            float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
+            float cn[3], cf[3];
+            sin_apply(s.u.dyn.cm[bj], s.u.dyn.ch[bj], s.u.dyn.cI[bj], Sw, Sv, cn, cf);
+            if (c < 3) val = cn[c];
+            else if (c < 6) val = cf[c - 3];
+            else {
+                const int i = c - 6;  // i <= j
+                int bi = -1;
+                for (int b = 1; b < B; ++b) if (md.dof[b] == i) bi = b;
+                if (bj >= bi && bj < md.subtree_end[bi]) {
+                    float Si_w[3] = {s.u.dyn.Sw[bi][0], s.u.dyn.Sw[bi][1], s.u.dyn.Sw[bi][2]};
+                    float Si_v[3] = {s.u.dyn.Sv[bi][0], s.u.dyn.Sv[bi][1], s.u.dyn.Sv[bi][2]};
+                    val = dot3(Si_w, cn) + dot3(Si_v, cf);
+                    if (i == j) val += sp.armature;
+                } else {
+                    val = 0.f;
+                }
+            }
+        }
+        s.M[r][c] = val;
+    }
+    // rhs in lanes 0..n-1 (registers), C from the composites
+    float x = 0.f;
+    if (lane < 6) {
+        x = -(lane < 3 ? s.u.dyn.Fn[0][lane] : s.u.dyn.Ff[0][lane - 3]);
+    } else if (lane < n) {
+        const int j = lane - 6;
+        int bj = -1;
+        for (int b = 1; b < B; ++b) if (md.dof[b] == j) bj = b;
+        float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
+        float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
+        float Fn[3] = {s.u.dyn.Fn[bj][0], s.u.dyn.Fn[bj][1], s.u.dyn.Fn[bj][2]};
+        float Ff[3] = {s.u.dyn.Ff[bj][0], s.u.dyn.Ff[bj][1], s.u.dyn.Ff[bj][2]};
+        float C = dot3(Sw, Fn) + dot3(Sv, Ff);
+        x = s.tau[j] - C;
+    }
+    __syncthreads();
+    // ---- 6. Cholesky (left-looking, in place, lane per row)
+    for (int k = 0; k < n; ++k) {
+        if (lane >= k && lane < n) {
+            float d = s.M[k][k];
+            for (int t = 0; t < k; ++t) d -= s.M[k][t] * s.M[k][t];
+            d = sqrtf(fmaxf(d, 1e-12f));
+            if (lane == k) {
+                s.M[k][k] = d;
+            } else {
+                float v = s.M[lane][k];
+                for (int t = 0; t < k; ++t) v -= s.M[lane][t] * s.M[k][t];
+                s.M[lane][k] = v / d;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- 7. qdd = M^-1 rhs by column sweeps (lane i owns x_i)
+    for (int i = 0; i < n; ++i) {
+        if (lane == i) x = x / s.M[i][i];
+        const float xi = rl(x, i);
+        if (lane > i && lane < n) x -= s.M[lane][i] * xi;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        if (lane == i) x = x / s.M[i][i];
+        const float xi = rl(x, i);
+        if (lane < i) x -= s.M[i][lane] * xi;
+    }
+    // free velocity (classical velocity of the root origin after dt)
+    {
+        float wxv[3];
+        cross3(w0, vO, wxv);
+        const int c = lane % 3;
+        const float wl = c == 0 ? w0[0] : (c == 1 ? w0[1] : w0[2]);
+        const float vl = c == 0 ? vO[0] : (c == 1 ? vO[1] : vO[2]);
+        const float cl = c == 0 ? wxv[0] : (c == 1 ? wxv[1] : wxv[2]);
+        if (lane < 3) s.qf[lane] = wl + dt * x;
+        else if (lane < 6) s.qf[lane] = vl + dt * (x + cl);
+        else if (lane < n) s.qf[lane] = s.qd[lane - 6] + dt * x;
+    }
+    __syncthreads();
+    // ---- 8. constraint rows.  Joint limits first (DOF order), then contacts.
+    const float beta = sp.beta;
+    int nlimit;
+    {
+        bool lo_act = false, hi_act = false;
+        float gap = 0.f;
+        if (lane < D) {
+            const float qj = s.q[lane], lo = md.dof_lower[lane], hi = md.dof_upper[lane];
+            const float qn = qj + dt * s.qf[6 + lane];
+            if (qn < lo) { lo_act = true; gap = qj - lo; }
+            else if (qn > hi) { hi_act = true; gap = hi - qj; }
+        }
+        const bool act = lo_act || hi_act;
+        const uint64_t mask = __ballot(act);
+        const int slot = __popcll(mask & ((1ull << lane) - 1ull));
+        const int max_limit = sp.max_rows - 3 * sp.max_contacts;
+        nlimit = __popcll(mask);
+        if (nlimit > max_limit) nlimit = max_limit;
+        if (act && slot < max_limit) {
+            float* row = s.u.con.Y[slot];
+            for (int i = 0; i < n; ++i) row[i] = 0.f;
+            row[6 + lane] = lo_act ? 1.f : -1.f;
+            s.tgt[slot] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            s.kind[slot] = 0;
+        }
+    }
+    int nc = 0;
+    {
+        const int maxc0 = (sp.max_rows - nlimit) / 3;
+        const int maxc = maxc0 < sp.max_contacts ? maxc0 : sp.max_contacts;
+        for (int base = 0; base < md.P && nc < maxc; base += WAVE) {
+            const int k = base + lane;
+            bool act = false;
+            float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f;
+            int b = 0;
+            if (k < md.P) {
+                b = md.pt_body[k];
+                float R[9];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) R[t] = s.R[b][t];
+                matvec(R, md.pt_pos + 3 * k, c);
+                c[0] += s.p[b][0]; c[1] += s.p[b][1]; c[2] += s.p[b][2];
+                rad = md.pt_radius[k];
+                sep = c[2] - rad - sp.rest_offset;
+                act = sep < sp.contact_offset;
+            }
+            const uint64_t mask = __ballot(act);
+            const int slot = nc + __popcll(mask & ((1ull << lane) - 1ull));
+            if (act && slot < maxc) {
+                s.c_body[slot] = b;
+                s.c_pt[slot][0] = c[0]; s.c_pt[slot][1] = c[1]; s.c_pt[slot][2] = c[2] - rad;
+                s.c_sep[slot] = sep;
+            }
+            nc += __popcll(mask);
+            if (nc > maxc) nc = maxc;
+        }
+    }
+    const int nrows = nlimit + 3 * nc;
+    __syncthreads();
+    // contact rows (lane per row): J row into Y[r]
+    if (lane >= nlimit && lane < nrows) {
+        const int cc = (lane - nlimit) / 3, dd = (lane - nlimit) % 3;
+        const float d[3] = {dd == 1 ? 1.f : 0.f, dd == 2 ? 1.f : 0.f, dd == 0 ? 1.f : 0.f};
+        const int b = s.c_body[cc];
+        float pc[3] = {s.c_pt[cc][0], s.c_pt[cc][1], s.c_pt[cc][2]};
+        float r[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]}, rxd[3];
+        cross3(r, d, rxd);
+        float* row = s.u.con.Y[lane];
+        for (int i = 0; i < n; ++i) row[i] = 0.f;
+        row[0] = rxd[0]; row[1] = rxd[1]; row[2] = rxd[2];
+        row[3] = d[0]; row[4] = d[1]; row[5] = d[2];
+        const int dep = md.depth[b];
+        for (int l = 1; l <= dep; ++l) {
+            const int a = md.chain[b * MAXD + l];
+            const int j = md.dof[a];
+            if (j < 0) continue;
+            float rp[3] = {pc[0] - s.p[a][0], pc[1] - s.p[a][1], pc[2] - s.p[a][2]}, t[3];
+            float aw[3] = {s.aw[a][0], s.aw[a][1], s.aw[a][2]};
+            cross3(aw, rp, t);
+            row[6 + j] = dot3(d, t);
+        }
+        if (dd == 0) {
+            const float sep = s.c_sep[cc];
+            s.tgt[lane] = sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp.max_depen);
+            s.kind[lane] = 0;
+        } else {
+            s.tgt[lane] = 0.f;
+            s.kind[lane] = dd;  // 1 = friction head, 2 = tail
+        }
+    }
+    __syncthreads();
+    // ---- 9. v = J qf ; Y = L^-1 J^T (lane r, registers)
+    float y[n];
+    float v = 0.f, lam = 0.f;
+    if (lane < nrows) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) y[i] = s.u.con.Y[lane][i];
+#pragma unroll
+        for (int i = 0; i < n; ++i) v += y[i] * s.qf[i];
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            float t = y[i];
+#pragma unroll
+            for (int k = 0; k < i; ++k) t -= s.M[i][k] * y[k];
+            y[i] = t / s.M[i][i];
+        }
+#pragma unroll
+        for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = y[i];
+    }
+    __syncthreads();
+    // ---- 10. A = Y^T Y (lane r computes row r)
+    float diag = 1.f;
+    if (lane < nrows) {
+        for (int t = 0; t < nrows; ++t) {
+            float a = 0.f;
+#pragma unroll
+            for (int i = 0; i < n; ++i) a += y[i] * s.u.con.Y[t][i];
+            s.u.con.A[lane][t] = a;
+            if (t == lane) diag = a;
+        }
+    }
+    __syncthreads();
+    // ---- 11. projected Gauss-Seidel
+    const float mu = 0.5f * (sp.ground_friction + shape_mu);
+    const float tg = (lane < nrows) ? s.tgt[lane] : 0.f;
+    for (int it = 0; it < sp.iters; ++it) {
+        for (int r = 0; r < nrows; ++r) {
+            const int kd = s.kind[r];
+            if (kd == 0) {
+                const float vr = rl(v, r), lr = rl(lam, r), ar = rl(diag, r), tr = rl(tg, r);
+                const float ln = fmaxf(0.f, lr + (tr - vr) / (ar + 1e-9f));
+                const float dl = ln - lr;
+                if (lane == r) lam = ln;
+                if (dl != 0.f && lane < nrows) v += s.u.con.A[r][lane] * dl;
+            } else if (kd == 1) {
+                const float lim = mu * rl(lam, r - 1);
+                const float l1o = rl(lam, r), l2o = rl(lam, r + 1);
+                float l1 = l1o - rl(v, r) / (rl(diag, r) + 1e-9f);
+                float l2 = l2o - rl(v, r + 1) / (rl(diag, r + 1) + 1e-9f);
+                const float nrm = sqrtf(l1 * l1 + l2 * l2);
+                if (nrm > lim) {
+                    const float sc = nrm > 0.f ? lim / nrm : 0.f;
+                    l1 *= sc; l2 *= sc;
+                }
+                const float d1 = l1 - l1o, d2 = l2 - l2o;
+                if (lane == r) lam = l1;
+                if (lane == r + 1) lam = l2;
+                if (lane < nrows) v += s.u.con.A[r][lane] * d1 + s.u.con.A[r + 1][lane] * d2;
+            }
+        }
+    }
+    // ---- 12. z = Y^T lambda ; dq = L^-T z ; qd' = qf + dq
+    float z = 0.f;
+    for (int r = 0; r < nrows; ++r) {
+        const float lr = rl(lam, r);
+        if (lane < n) z += s.u.con.Y[r][lane] * lr;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        if (lane == i) z = z / s.M[i][i];
+        const float zi = rl(z, i);
+        if (lane < i) z -= s.M[i][lane] * zi;
+    }
+    float qn = (lane < n) ? s.qf[lane] + z : 0.f;
+    if (sp.clamp_qd && lane >= 6 && lane < n) {
+        const float lim = md.dof_velocity[lane - 6];
+        if (lim > 0.f) qn = fminf(fmaxf(qn, -lim), lim);
+    }
+    // contact forces of this substep
+    {
+        float F[3] = {0.f, 0.f, 0.f};
+        for (int c = 0; c < nc; ++c) {
+            const int r = nlimit + 3 * c;
+            const float ln = rl(lam, r), l1 = rl(lam, r + 1), l2 = rl(lam, r + 2);
+            if (s.c_body[c] == lane) { F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt; }
+        }
+        if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
+    }
+    // ---- 13. integrate
+    const float qw0 = rl(qn, 0), qw1 = rl(qn, 1), qw2 = rl(qn, 2);
+    const float qv0 = rl(qn, 3), qv1 = rl(qn, 4), qv2 = rl(qn, 5);
+    __syncthreads();
+    if (lane >= 6 && lane < n) {
+        const int j = lane - 6;
+        s.qd[j] = qn;
+        s.q[j] = s.q[j] + dt * qn;
+    }
+    if (lane == 0) {
+        float* rt = s.root;
+        rt[0] += dt * qv0; rt[1] += dt * qv1; rt[2] += dt * qv2;
+        float* q = rt + 3;
+        const float w[3] = {qw0, qw1, qw2};
+        float dq[4];
+        dq[0] = 0.5f * dt * (q[3] * w[0] + (w[1] * q[2] - w[2] * q[1]));
+        dq[1] = 0.5f * dt * (q[3] * w[1] + (w[2] * q[0] - w[0] * q[2]));
+        dq[2] = 0.5f * dt * (q[3] * w[2] + (w[0] * q[1] - w[1] * q[0]));
+        dq[3] = 0.5f * dt * (-(w[0] * q[0] + w[1] * q[1] + w[2] * q[2]));
+        float nn = 0.f;
+        for (int k = 0; k < 4; ++k) { q[k] += dq[k]; nn += q[k] * q[k]; }
+        nn = 1.f / sqrtf(nn);
+        for (int k = 0; k < 4; ++k) q[k] *= nn;
+        float R[9], c[3], wc[3];
+        quat_to_mat(q, R);
+        matvec(R, md.com, c);
+        cross3(w, c, wc);
+        rt[10] = w[0]; rt[11] = w[1]; rt[12] = w[2];
+        rt[7] = qv0 + wc[0]; rt[8] = qv1 + wc[1]; rt[9] = qv2 + wc[2];
+    }
+    __syncthreads();
+}
+
+// rigid body states [B][13] of the block's env into global memory
+template <int D, int B, int ROWS>
+__device__ void body_states(Smem<D, B, ROWS>& s, const DevModel& md, float* rbs_out) {
+    const int lane = threadIdx.x;
+    if (lane < B) {
+        float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
+        quat_to_mat(s.root + 3, R);
+        p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
+        const float O[3] = {p[0], p[1], p[2]};
+        float c0[3];
+        matvec(R, md.com, c0);
+        float w[3] = {s.root[10], s.root[11], s.root[12]}, t[3];
+        cross3(w, c0, t);
+        float Vw[3] = {w[0], w[1], w[2]};
+        float Vv[3] = {s.root[7] - t[0], s.root[8] - t[1], s.root[9] - t[2]};
+        const int d = md.depth[lane];
+        for (int l = 1; l <= d; ++l) {
+            const int a = md.chain[lane * MAXD + l];
+            float Rj[9], tp[3];
+            matmul(R, md.joint_rot + 9 * a, Rj);
+            matvec(R, md.joint_pos + 3 * a, tp);
+            p[0] += tp[0]; p[1] += tp[1]; p[2] += tp[2];
+            const int j = md.dof[a];
+            if (j >= 0) {
+                matvec(Rj, md.axis + 3 * a, aw);
+                float Ra[9];
+                axis_angle(md.axis + 3 * a, s.q[j], Ra);
+                matmul(Rj, Ra, R);
+                const float qd = s.qd[j];
+                float rp[3] = {p[0] - O[0], p[1] - O[1], p[2] - O[2]}, sv[3];
+                cross3(rp, aw, sv);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { Vw[k] += aw[k] * qd; Vv[k] += sv[k] * qd; }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) R[k] = Rj[k];
+            }
+        }
+        float c[3];
+        matvec(R, md.com + 3 * lane, c);
+        float r[3] = {p[0] + c[0] - O[0], p[1] + c[1] - O[1], p[2] + c[2] - O[2]}, wr[3];
+        cross3(Vw, r, wr);
+        float* o = rbs_out + 13 * lane;
+        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+        float qq[4];
+        mat_to_quat(R, qq);
+        o[3] = qq[0]; o[4] = qq[1]; o[5] = qq[2]; o[6] = qq[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { o[7 + k] = Vv[k] + wr[k]; o[10 + k] = Vw[k]; }
+    }
+}
+
+template <int D, int B, int ROWS>
+__device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
+    const int lane = threadIdx.x;
+    if (lane < 13) s.root[lane] = st.root[13 * e + lane];
+    if (lane < 2 * D) {
+        const float v = st.dofs[(size_t)2 * D * e + lane];
+        if (lane & 1) s.qd[lane >> 1] = v; else s.q[lane >> 1] = v;
+    }
+}
+template <int D, int B, int ROWS>
+__device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
+    const int lane = threadIdx.x;
+    if (lane < 13) st.root[13 * e + lane] = s.root[lane];
+    if (lane < 2 * D) st.dofs[(size_t)2 * D * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
+    for (int i = lane; i < 3 * B; i += WAVE) st.cforce[(size_t)3 * B * e + i] = (&s.cf[0][0])[i];
+}
+
+// ---------------------------------------------------------- kernels --------
+template <int D, int B, int ROWS>
+__global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevState st, int N) {
+    __shared__ Smem<D, B, ROWS> s;
+    const int e = blockIdx.x;
+    if (e >= N) return;
+    load_state(s, st, e);
+    if (threadIdx.x < D) s.tau[threadIdx.x] = st.torques_in[(size_t)D * e + threadIdx.x];
+    __syncthreads();
+    substep(s, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
+    store_state(s, st, e);
+    if (st.rbs) body_states(s, md, st.rbs + (size_t)13 * B * e);
+}
+
+template <int D, int B, int ROWS>
+__global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
+    __shared__ Smem<D, B, ROWS> s;
+    const int e = blockIdx.x;
+    if (e >= N) return;
+    load_state(s, st, e);
+    __syncthreads();
+    body_states(s, md, st.rbs + (size_t)13 * B * e);
+}
+
+struct DevEnv {
+    lgs_env_buffers b;
+};
+
+// torch.remainder-style modulo for positive divisor
+__device__ __forceinline__ float fmod_pos(float a, float b) {
+    float m = fmodf(a, b);
+    if (m != 0.f && m < 0.f) m += b;
+    return m;
+}
+
+__device__ __forceinline__ void quat_rotate_inverse(const float* q, const float* v, float* o) {
+    float w = q[3];
+    float s = 2.0f * w * w - 1.0f;
+    float c[3];
+    cross3(q, v, c);
+    float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = v[k] * s - c[k] * w * 2.0f + q[k] * d * 2.0f;
+}
+
+__device__ __forceinline__ void resample_commands(const lgs_task_params& T, float* cmd, uint64_t seed, uint32_t env,
+                                                  uint32_t step, uint32_t stream) {
+    cmd[0] = rand_range(T.cmd_lin_vel_x[0], T.cmd_lin_vel_x[1], philox_uniform(seed, env, step, stream, 0));
+    cmd[1] = rand_range(T.cmd_lin_vel_y[0], T.cmd_lin_vel_y[1], philox_uniform(seed, env, step, stream, 1));
+    if (T.heading_command)
+        cmd[3] = rand_range(T.cmd_heading[0], T.cmd_heading[1], philox_uniform(seed, env, step, stream, 2));
+    else
+        cmd[2] = rand_range(T.cmd_ang_vel_yaw[0], T.cmd_ang_vel_yaw[1], philox_uniform(seed, env, step, stream, 2));
+    float nrm = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+    float keep = nrm > 0.2f ? 1.f : 0.f;
+    cmd[0] *= keep; cmd[1] *= keep;
+}
+
+// ------------------------------------------------ post-physics (lane 0) ----
+// legged_robot.py:673-709 with _post_physics_step_callback, check_termination,
+// compute_reward; humanoid variants h1_env.py / g1_env.py.  Everything up to
+// the reset decision; returns reset flag in s.flags[0].
+template <int D, int B, int ROWS>
+__device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
+                                    const float* rbs, int N, int e, uint32_t step) {
+    const int A = T.num_actions;
+    float* root = s.root;
+    float* cmd = E.commands + 4 * e;
+    const float* act = s.act;
+    const float* last_act = E.last_actions + A * e;
+    const float* last_qd = E.last_dof_vel + D * e;
+    float* air = E.feet_air_time + T.num_feet * e;
+    uint8_t* lastc = E.last_contacts + T.num_feet * e;
+    int64_t* ep = E.episode_length + e;
+    const float* tau = s.tau;
+
+    *ep += 1;
+    float bl[3], ba[3], pg[3], rpy[3];
+    const float g[3] = {0.f, 0.f, -1.f};
+    quat_rotate_inverse(root + 3, root + 7, bl);
+    quat_rotate_inverse(root + 3, root + 10, ba);
+    quat_rotate_inverse(root + 3, g, pg);
+    {
+        const float* q = root + 3;
+        float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+        float sinr = 2.0f * (qw * qx + qy * qz);
+        float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+        rpy[0] = atan2f(sinr, cosr);
+        float sinp = 2.0f * (qw * qy - qz * qx);
+        rpy[1] = fabsf(sinp) >= 1.f ? copysignf(3.14159265358979323846f / 2.0f, sinp) : asinf(sinp);
+        float siny = 2.0f * (qw * qz + qx * qy);
+        float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+        rpy[2] = atan2f(siny, cosy);
+    }
+    float phase = 0.f, leg_phase[2] = {0.f, 0.f};
+    if (T.obs_layout == LGS_OBS_HUMANOID) {
+        float t = (float)(*ep) * T.control_dt;
+        phase = fmod_pos(t, T.phase_period) / T.phase_period;
+        leg_phase[0] = phase;
+        leg_phase[1] = fmod_pos(phase + T.phase_offset, 1.0f);
+    }
+    const uint64_t seed = T.seed;
+    if ((*ep) % T.resample_interval == 0) resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_CMD);
+    if (T.heading_command) {
+        const float* q = root + 3;
+        const float fx[3] = {1.f, 0.f, 0.f};
+        float t[3], u[3];
+        cross3(q, fx, t);
+        t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
+        cross3(q, t, u);
+        float fwd0 = fx[0] + q[3] * t[0] + u[0];
+        float fwd1 = fx[1] + q[3] * t[1] + u[1];
+        float heading = atan2f(fwd1, fwd0);
+        const float tp = 2.0f * 3.14159265358979323846f;
+        float wv = fmod_pos(cmd[3] - heading, tp);
+        if (wv > 3.14159265358979323846f) wv -= tp;
+        cmd[2] = clipf(0.5f * wv, -1.f, 1.f);
+    }
+    int reset = 0;
+    for (int i = 0; i < T.num_termination; ++i) {
+        const float* F = s.cf[T.termination_idx[i]];
+        if (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f) reset = 1;
+    }
+    if (fabsf(rpy[1]) > 1.0f || fabsf(rpy[0]) > 0.8f) reset = 1;
+    const int timeout = (float)(*ep) > T.max_episode_length;
+    reset |= timeout;
+    // rewards, active terms in alphabetical order
+    float rew = 0.f;
+    for (int k = 0; k < T.num_rewards; ++k) {
+        float sum = 0.f, r;
+        switch (T.reward_ids[k]) {
+        case LGS_REW_LIN_VEL_Z: r = bl[2] * bl[2]; break;
+        case LGS_REW_ANG_VEL_XY: r = ba[0] * ba[0] + ba[1] * ba[1]; break;
+        case LGS_REW_ORIENTATION: r = pg[0] * pg[0] + pg[1] * pg[1]; break;
+        case LGS_REW_BASE_HEIGHT: { float d = root[2] - T.base_height_target; r = d * d; } break;
+        case LGS_REW_TORQUES: for (int j = 0; j < A; ++j) sum += tau[j] * tau[j]; r = sum; break;
+        case LGS_REW_DOF_VEL: for (int j = 0; j < A; ++j) sum += s.qd[j] * s.qd[j]; r = sum; break;
+        case LGS_REW_DOF_ACC:
+            for (int j = 0; j < A; ++j) { float d = (last_qd[j] - s.qd[j]) / T.control_dt; sum += d * d; }
+            r = sum; break;
+        case LGS_REW_ACTION_RATE:
+            for (int j = 0; j < A; ++j) { float d = last_act[j] - act[j]; sum += d * d; }
+            r = sum; break;
+        case LGS_REW_COLLISION:
+            for (int i = 0; i < T.num_penalised; ++i) {
+                const float* F = s.cf[T.penalised_idx[i]];
+                sum += (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 0.1f) ? 1.f : 0.f;
+            }
+            r = sum; break;
+        case LGS_REW_DOF_POS_LIMITS:
+            for (int j = 0; j < A; ++j) {
+                float o = -fminf(s.q[j] - T.soft_dof_pos_lower[j], 0.f);
+                o += fmaxf(s.q[j] - T.soft_dof_pos_upper[j], 0.f);
+                sum += o;
+            }
+            r = sum; break;
+        case LGS_REW_DOF_VEL_LIMITS:
+            for (int j = 0; j < A; ++j) sum += clipf(fabsf(s.qd[j]) - T.dof_vel_limits[j] * T.soft_dof_vel_limit, 0.f, 1.f);
+            r = sum; break;
+        case LGS_REW_TORQUE_LIMITS:
+            for (int j = 0; j < A; ++j) sum += fmaxf(fabsf(tau[j]) - T.torque_limits[j] * T.soft_torque_limit, 0.f);
+            r = sum; break;
+        case LGS_REW_TRACKING_LIN_VEL: {
+            float e0 = cmd[0] - bl[0], e1 = cmd[1] - bl[1];
+            r = expf(-(e0 * e0 + e1 * e1) / T.tracking_sigma);
+        } break;
+        case LGS_REW_TRACKING_ANG_VEL: {
+            float d = cmd[2] - ba[2];
+            r = expf(-(d * d) / T.tracking_sigma);
+        } break;
+        case LGS_REW_FEET_AIR_TIME: {
+            int filt[LGS_MAX_FEET];
+            for (int f = 0; f < T.num_feet; ++f) {
+                int contact = s.cf[T.feet_idx[f]][2] > 1.f;
+                filt[f] = contact || lastc[f];
+                lastc[f] = (uint8_t)contact;
+                float first = (air[f] > 0.f && filt[f]) ? 1.f : 0.f;
+                air[f] += T.control_dt;
+                sum += (air[f] - 0.5f) * first;
+            }
+            float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+            sum *= (cn > 0.1f) ? 1.f : 0.f;
+            for (int f = 0; f < T.num_feet; ++f)
+                if (filt[f]) air[f] = 0.f;
+            r = sum;
+        } break;
+        case LGS_REW_FEET_STUMBLE: {
+            r = 0.f;
+            for (int f = 0; f < T.num_feet; ++f) {
+                const float* F = s.cf[T.feet_idx[f]];
+                if (sqrtf(F[0] * F[0] + F[1] * F[1]) > 5.f * fabsf(F[2])) r = 1.f;
+            }
+        } break;
+        case LGS_REW_STAND_STILL: {
+            for (int j = 0; j < A; ++j) sum += fabsf(s.q[j] - T.default_dof_pos[j]);
+            float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+            r = sum * ((cn < 0.1f) ? 1.f : 0.f);
+        } break;
+        case LGS_REW_FEET_CONTACT_FORCES:
+            for (int f = 0; f < T.num_feet; ++f) {
+                const float* F = s.cf[T.feet_idx[f]];
+                sum += fmaxf(sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) - T.max_contact_force, 0.f);
+            }
+            r = sum; break;
+        case LGS_REW_ALIVE: r = 1.0f; break;
+        case LGS_REW_CONTACT:
+            for (int f = 0; f < T.num_feet; ++f) {
+                int stance = leg_phase[f] < T.stance_threshold;
+                int contact = s.cf[T.feet_idx[f]][2] > 1.f;
+                sum += (contact == stance) ? 1.f : 0.f;
+            }
+            r = sum; break;
+        case LGS_REW_FEET_SWING_HEIGHT:
+            for (int f = 0; f < T.num_feet; ++f) {
+                const float* F = s.cf[T.feet_idx[f]];
+                int contact = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f;
+                float d = rbs[13 * T.feet_idx[f] + 2] - T.swing_height_target;
+                sum += d * d * (contact ? 0.f : 1.f);
+            }
+            r = sum; break;
+        case LGS_REW_CONTACT_NO_VEL:
+            for (int f = 0; f < T.num_feet; ++f) {
+                const float* F = s.cf[T.feet_idx[f]];
+                float c = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f ? 1.f : 0.f;
+                const float* vv = rbs + 13 * T.feet_idx[f] + 7;
+                for (int k2 = 0; k2 < 3; ++k2) { float xx = vv[k2] * c; sum += xx * xx; }
+            }
+            r = sum; break;
+        case LGS_REW_HIP_POS:
+            for (int i = 0; i < T.num_hip; ++i) sum += s.q[T.hip_dofs[i]] * s.q[T.hip_dofs[i]];
+            r = sum; break;
+        default: r = 0.f;
+        }
+        r = r * T.reward_scales[k];
+        rew += r;
+        E.episode_sums[(size_t)k * N + e] += r;
+        if (E.rew_terms) E.rew_terms[(size_t)k * N + e] = r;
+    }
+    if (T.only_positive_rewards) rew = fmaxf(rew, 0.f);
+    if (T.has_termination_reward) {
+        float r = ((reset && !timeout) ? 1.f : 0.f) * T.termination_scale;
+        rew += r;
+        E.episode_sums[(size_t)T.num_rewards * N + e] += r;
+    }
+    E.rew[e] = rew;
+    E.reset[e] = (uint8_t)reset;
+    E.time_out[e] = (uint8_t)timeout;
+    for (int i = 0; i < 3; ++i) {
+        E.base_lin_vel[3 * e + i] = bl[i];
+        E.base_ang_vel[3 * e + i] = ba[i];
+        E.projected_gravity[3 * e + i] = pg[i];
+        E.rpy[3 * e + i] = rpy[i];
+        s.misc[i] = bl[i]; s.misc[3 + i] = ba[i]; s.misc[6 + i] = pg[i];
+    }
+    s.misc[9] = phase;
+    if (E.phase) E.phase[e] = phase;
+    if (E.leg_phase) { E.leg_phase[2 * e] = leg_phase[0]; E.leg_phase[2 * e + 1] = leg_phase[1]; }
+    s.flags[0] = reset;
+}
+
+template <int D, int B, int ROWS>
+__device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
+                             const float* rbs, int N, int e, uint32_t step, bool force_reset) {
+    const int lane = threadIdx.x;
+    const int A = T.num_actions;
+    const uint64_t seed = T.seed;
+    if (!force_reset) {
+        if (lane == 0) post_physics_scalar(s, T, E, rbs, N, e, step);
+    } else {
+        if (lane == 0) s.flags[0] = 1;
+    }
+    __syncthreads();
+    const int reset = s.flags[0];
+    float* act = s.act;
+    if (reset) {  // reset_idx (legged_robot.py:723-768)
+        if (lane < D) {
+            s.q[lane] = T.default_dof_pos[lane] *
+                        rand_range(0.5f, 1.5f, philox_uniform(seed, e, step, LGS_STREAM_RESET_DOF, lane));
+            s.qd[lane] = 0.f;
+            E.last_dof_vel[D * e + lane] = 0.f;
+        }
+        if (lane < A) { act[lane] = 0.f; E.actions[A * e + lane] = 0.f; E.last_actions[A * e + lane] = 0.f; }
+        if (lane < T.num_feet) E.feet_air_time[T.num_feet * e + lane] = 0.f;
+        float rv = (lane < 6) ? rand_range(-0.5f, 0.5f, philox_uniform(seed, e, step, LGS_STREAM_RESET_ROOT, lane)) : 0.f;
+        __syncthreads();
+        if (lane < 13) {
+            float x = T.base_init_state[lane];
+            if (lane < 3) x += E.env_origins[3 * e + lane];
+            s.root[lane] = x;
+        }
+        __syncthreads();
+        if (lane < 6) s.root[7 + lane] = rv;
+        if (!force_reset) {
+            const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+            if (lane < nsum) {
+                atomicAdd(E.episode_acc + lane, E.episode_sums[(size_t)lane * N + e]);
+                E.episode_sums[(size_t)lane * N + e] = 0.f;
+            }
+            if (lane == 0) atomicAdd(E.episode_acc + nsum, 1.f);
+        } else {
+            const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+            if (lane < nsum) E.episode_sums[(size_t)lane * N + e] = 0.f;
+        }
+        if (lane == 0) {
+            resample_commands(T, E.commands + 4 * e, seed, (uint32_t)e, step, LGS_STREAM_RESET_CMD);
+            E.episode_length[e] = 0;
+        }
+        __syncthreads();
+    }
+    if (force_reset) return;  // BaseTask.reset: the following step() builds obs
+    // _push_robots (legged_robot.py:540-555)
+    if (lane == 0 && T.push_robots && E.episode_length[e] % T.push_interval == 0) {
+        s.root[7] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy, philox_uniform(seed, e, step, LGS_STREAM_PUSH, 0));
+        s.root[8] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy, philox_uniform(seed, e, step, LGS_STREAM_PUSH, 1));
+    }
+    // compute_observations
+    if (lane == 0) {
+        const float* cmd = E.commands + 4 * e;
+        // quadruped obs = tmp[0:O]; humanoid priv = tmp[0:P], obs = tmp[3:3+O]
+        float* tmp = s.obs_tmp;
+        tmp[0] = s.misc[0] * T.obs_scale_lin_vel;
+        tmp[1] = s.misc[1] * T.obs_scale_lin_vel;
+        tmp[2] = s.misc[2] * T.obs_scale_lin_vel;
+        int k = 3;
+        for (int i = 0; i < 3; ++i) tmp[k++] = s.misc[3 + i] * T.obs_scale_ang_vel;
+        for (int i = 0; i < 3; ++i) tmp[k++] = s.misc[6 + i];
+        for (int i = 0; i < 3; ++i) tmp[k++] = cmd[i] * T.commands_scale[i];
+        for (int j = 0; j < D; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
+        for (int j = 0; j < D; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
+        for (int j = 0; j < A; ++j) tmp[k++] = act[j];
+        if (T.obs_layout == LGS_OBS_HUMANOID) {
+            float ph = 2.0f * 3.14159265358979323846f * s.misc[9];
+            tmp[k++] = sinf(ph);
+            tmp[k++] = cosf(ph);
+        }
+    }
+    __syncthreads();
+    const int O = T.num_obs, P = T.num_privileged_obs;
+    const int off = (T.obs_layout == LGS_OBS_HUMANOID) ? 3 : 0;
+    for (int i = lane; i < O; i += WAVE) {
+        float x = s.obs_tmp[off + i];
+        if (T.add_noise) x += (2.f * philox_uniform(seed, e, step, LGS_STREAM_NOISE, i) - 1.f) * T.noise_vec[i];
+        E.obs[(size_t)O * e + i] = clipf(x, -T.clip_observations, T.clip_observations);
+    }
+    if (P > 0 && E.priv_obs && T.obs_layout == LGS_OBS_HUMANOID)
+        for (int i = lane; i < P; i += WAVE)
+            E.priv_obs[(size_t)P * e + i] = clipf(s.obs_tmp[i], -T.clip_observations, T.clip_observations);
+    // bookkeeping (:707-709)
+    if (lane < A) E.last_actions[A * e + lane] = act[lane];
+    if (lane < D) E.last_dof_vel[D * e + lane] = s.qd[lane];
+    if (lane < 6) E.last_root_vel[6 * e + lane] = s.root[7 + lane];
+}
+
+template <int D, int B, int ROWS>
+__global__ __launch_bounds__(WAVE) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
+                                               lgs_env_buffers E, int N, uint32_t step) {
+    __shared__ Smem<D, B, ROWS> s;
+    const int e = blockIdx.x;
+    if (e >= N) return;
+    const lgs_task_params& T = *Tp;
+    const int lane = threadIdx.x;
+    load_state(s, st, e);
+    const int A = T.num_actions;
+    float a = 0.f;
+    if (lane < A) {
+        a = clipf(E.actions[A * e + lane], -T.clip_actions, T.clip_actions);  // :623-624
+        E.actions[A * e + lane] = a;
+        s.act[lane] = a;
+    }
+    const float lqd = (lane < D) ? E.last_dof_vel[D * e + lane] : 0.f;
+    const float am = st.added_mass ? st.added_mass[e] : 0.f;
+    const float mu = st.friction ? st.friction[e] : 1.f;
+    __syncthreads();
+    for (int it = 0; it < T.decimation; ++it) {  // :627-639
+        if (lane < D) {  // _compute_torques :649-671
+            const float as = a * T.action_scale;
+            const float q = s.q[lane], qd = s.qd[lane];
+            float t;
+            if (T.control_type == 0) t = T.p_gains[lane] * (as + T.default_dof_pos[lane] - q) - T.d_gains[lane] * qd;
+            else if (T.control_type == 1) t = T.p_gains[lane] * (as - qd) - T.d_gains[lane] * (qd - lqd) / sp.dt;
+            else t = as;
+            s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
+        }
+        __syncthreads();
+        substep(s, md, sp, am, mu);
+    }
+    if (lane < D) E.torques[D * e + lane] = s.tau[lane];
+    float* rbs = st.rbs + (size_t)13 * B * e;
+    body_states(s, md, rbs);  // refresh_rigid_body_state (h1_env.py:49)
+    __syncthreads();
+    post_physics(s, T, E, rbs, N, e, step, false);
+    __syncthreads();
+    store_state(s, st, e);
+}
+
+template <int D, int B, int ROWS>
+__global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
+                                                    lgs_env_buffers E, int N, uint32_t step) {
+    __shared__ Smem<D, B, ROWS> s;
+    const int e = blockIdx.x;
+    if (e >= N) return;
+    load_state(s, st, e);
+    if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
+    __syncthreads();
+    post_physics(s, *Tp, E, nullptr, N, e, step, true);
+    __syncthreads();
+    store_state(s, st, e);
+    if (st.rbs) body_states(s, md, st.rbs + (size_t)13 * B * e);
+}
+
+__global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, int n, int width) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = i / width, col = i % width;
+    if (row >= n) return;
+    const size_t r = (size_t)ids[row];
+    dst[r * width + col] = src[r * width + col];
+}
+
+// ------------------------------------------------------------ host side ----
+struct lgs_sim {
+    int N, B, D, P;
+    int device;
+    hipStream_t stream = nullptr;
+    DevModel md{};
+    DevSim sp{};
+    void* model_mem = nullptr;
+    float* friction = nullptr;
+    float* added_mass = nullptr;
+    float* root = nullptr;
+    float* dofs = nullptr;
+    float* cforce = nullptr;
+    float* rbs = nullptr;
+    const float* torques = nullptr;
+    lgs_task_params* task_dev = nullptr;
+    int has_task = 0;
+    int rows = 32;
+};
+
+enum Variant { V_12_19, V_12_13, V_10_11, V_NONE };
+
+static Variant pick(const lgs_sim* s) {
+    if (s->D == 12 && s->B <= 19) return V_12_19;
+    if (s->D == 12 && s->B <= 13) return V_12_13;
+    if (s->D == 10 && s->B <= 11) return V_10_11;
+    return V_NONE;
+}
+
+#define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
+    switch (pick(sim)) {                                                                                  \
+    case V_12_19: hipLaunchKernelGGL((KERNEL<12, 19, 32>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
+    case V_12_13: hipLaunchKernelGGL((KERNEL<12, 13, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
+    case V_10_11: hipLaunchKernelGGL((KERNEL<10, 11, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
+    default: return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");                                 \
+    }
+
+static DevState state_of(lgs_sim* s) {
+    DevState st;
+    st.root = s->root; st.dofs = s->dofs; st.cforce = s->cforce; st.rbs = s->rbs;
+    st.friction = s->friction; st.added_mass = s->added_mass; st.torques_in = s->torques;
+    return st;
+}
+
+extern "C" {
+
+LGS_API const char* lgs_last_error(void) { return g_err.c_str(); }
+LGS_API int lgs_version(void) { return 1; }
+
+LGS_API float lgs_uniform(uint64_t seed, uint32_t env, uint32_t step, uint32_t stream, uint32_t index) {
+    return philox_uniform(seed, env, step, stream, index);
+}
+
+LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int32_t num_envs, int32_t device_id,
+                           lgs_sim** out) {
+    if (!m || !p || !out || num_envs <= 0) return set_err(LGS_ERR_ARG, "lgs_create_sim: null argument or num_envs <= 0");
+    if (m->num_bodies < 1 || m->num_bodies > LGS_MAX_BODIES || m->num_dofs < 0 || m->num_dofs > LGS_MAX_DOFS)
+        return set_err(LGS_ERR_ARG, "lgs_create_sim: model exceeds LGS_MAX_BODIES/LGS_MAX_DOFS");
+    for (int b = 0; b < m->num_bodies; ++b)
+        if (m->depth[b] >= LGS_MAX_DEPTH) return set_err(LGS_ERR_ARG, "lgs_create_sim: tree deeper than LGS_MAX_DEPTH");
+    HIP_TRY(hipSetDevice(device_id));
+    lgs_sim* s = new lgs_sim();
+    s->N = num_envs; s->B = m->num_bodies; s->D = m->num_dofs; s->P = m->num_points; s->device = device_id;
+    if (pick(s) == V_NONE) {
+        delete s;
+        return set_err(LGS_ERR_ARG, "lgs_create_sim: no kernel instantiation for this (dofs, bodies)");
+    }
+    {
+        const int cap = pick(s) == V_12_19 ? 32 : 48;
+        if (p->max_rows > cap || p->max_rows < 3 * p->max_contacts || p->max_contacts < 0) {
+            delete s;
+            return set_err(LGS_ERR_ARG, "lgs_create_sim: need 3*max_contacts <= max_rows <= " + std::to_string(cap));
+        }
+    }
+    const int B = s->B, D = s->D, P = s->P;
+    // pack the model into one device allocation
+    size_t ints = (size_t)B * (4 + LGS_MAX_DEPTH) + (size_t)P;
+    size_t floats = (size_t)B * (9 + 3 + 3 + 1 + 3 + 6) + (size_t)D * 3 + (size_t)P * 4;
+    size_t bytes = ints * 4 + floats * 4 + 256;
+    HIP_TRY(hipMalloc(&s->model_mem, bytes));
+    char* host = (char*)calloc(1, bytes);
+    size_t off = 0;
+    auto put = [&](const void* src, size_t n) -> size_t {
+        size_t o = off;
+        if (n) memcpy(host + off, src, n);
+        off += (n + 15) & ~size_t(15);
+        return o;
+    };
+    size_t o_parent = put(m->parent, 4 * B), o_dof = put(m->dof, 4 * B), o_se = put(m->subtree_end, 4 * B);
+    size_t o_depth = put(m->depth, 4 * B), o_chain = put(m->chain, 4 * B * LGS_MAX_DEPTH);
+    size_t o_jr = put(m->joint_rot, 36 * B), o_jp = put(m->joint_pos, 12 * B), o_ax = put(m->axis, 12 * B);
+    size_t o_mass = put(m->mass, 4 * B), o_com = put(m->com, 12 * B), o_in = put(m->inertia, 24 * B);
+    size_t o_lo = put(m->dof_lower, 4 * D), o_hi = put(m->dof_upper, 4 * D), o_vel = put(m->dof_velocity, 4 * D);
+    size_t o_pb = put(m->pt_body, 4 * P), o_pp = put(m->pt_pos, 12 * P), o_pr = put(m->pt_radius, 4 * P);
+    if (off > bytes) { free(host); return set_err(LGS_ERR_STATE, "model packing overflow"); }
+    HIP_TRY(hipMemcpy(s->model_mem, host, off, hipMemcpyHostToDevice));
+    free(host);
+    char* d = (char*)s->model_mem;
+    DevModel& md = s->md;
+    md.B = B; md.D = D; md.P = P;
+    md.parent = (const int*)(d + o_parent); md.dof = (const int*)(d + o_dof); md.subtree_end = (const int*)(d + o_se);
+    md.depth = (const int*)(d + o_depth); md.chain = (const int*)(d + o_chain);
+    md.joint_rot = (const float*)(d + o_jr); md.joint_pos = (const float*)(d + o_jp); md.axis = (const float*)(d + o_ax);
+    md.mass = (const float*)(d + o_mass); md.com = (const float*)(d + o_com); md.inertia = (const float*)(d + o_in);
+    md.dof_lower = (const float*)(d + o_lo); md.dof_upper = (const float*)(d + o_hi); md.dof_velocity = (const float*)(d + o_vel);
+    md.pt_body = (const int*)(d + o_pb); md.pt_pos = (const float*)(d + o_pp); md.pt_radius = (const float*)(d + o_pr);
+    DevSim& sp = s->sp;
+    sp.dt = p->dt; sp.gx = p->gravity[0]; sp.gy = p->gravity[1]; sp.gz = p->gravity[2];
+    sp.iters = p->solver_iterations; sp.contact_offset = p->contact_offset; sp.rest_offset = p->rest_offset;
+    sp.max_depen = p->max_depenetration_velocity; sp.beta = p->baumgarte; sp.ground_friction = p->ground_friction;
+    sp.armature = p->armature; sp.clamp_qd = p->clamp_joint_velocity; sp.max_contacts = p->max_contacts;
+    sp.max_rows = p->max_rows;
+    HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
+    HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
+    HIP_TRY(hipMemset(s->added_mass, 0, sizeof(float) * num_envs));
+    {
+        float* ones = (float*)malloc(sizeof(float) * num_envs);
+        for (int i = 0; i < num_envs; ++i) ones[i] = p->ground_friction;
+        HIP_TRY(hipMemcpy(s->friction, ones, sizeof(float) * num_envs, hipMemcpyHostToDevice));
+        free(ones);
+    }
+    HIP_TRY(hipMalloc(&s->task_dev, sizeof(lgs_task_params)));
+    *out = s;
+    return LGS_OK;
+}
+
+LGS_API int lgs_destroy_sim(lgs_sim* s) {
+    if (!s) return LGS_OK;
+    (void)hipFree(s->model_mem);
+    (void)hipFree(s->friction);
+    (void)hipFree(s->added_mass);
+    (void)hipFree(s->task_dev);
+    delete s;
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_stream(lgs_sim* s, void* stream) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    s->stream = (hipStream_t)stream;
+    return LGS_OK;
+}
+
+LGS_API int lgs_synchronize(lgs_sim* s) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_env_properties(lgs_sim* s, const float* friction, const float* added_mass) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    if (friction) HIP_TRY(hipMemcpy(s->friction, friction, sizeof(float) * s->N, hipMemcpyHostToDevice));
+    if (added_mass) HIP_TRY(hipMemcpy(s->added_mass, added_mass, sizeof(float) * s->N, hipMemcpyHostToDevice));
+    return LGS_OK;
+}
+
+LGS_API int lgs_bind_state(lgs_sim* s, float* root, float* dofs, float* cforce, float* rbs) {
+    if (!s || !root || !dofs || !cforce || !rbs) return set_err(LGS_ERR_ARG, "lgs_bind_state: null pointer");
+    s->root = root; s->dofs = dofs; s->cforce = cforce; s->rbs = rbs;
+    return LGS_OK;
+}
+
+LGS_API int lgs_refresh(lgs_sim* s) { return s ? LGS_OK : set_err(LGS_ERR_ARG, "null sim"); }
+
+LGS_API int lgs_set_dof_actuation_force(lgs_sim* s, const float* tau) {
+    if (!s || !tau) return set_err(LGS_ERR_ARG, "null argument");
+    s->torques = tau;
+    return LGS_OK;
+}
+
+LGS_API int lgs_simulate(lgs_sim* s) {
+    if (!s || !s->root) return set_err(LGS_ERR_STATE, "lgs_simulate: state not bound");
+    if (!s->torques) return set_err(LGS_ERR_STATE, "lgs_simulate: no actuation force set");
+    DevState st = state_of(s);
+    LGS_DISPATCH(s, k_simulate, s->md, s->sp, st, s->N);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_forward_kinematics(lgs_sim* s) {
+    if (!s || !s->root) return set_err(LGS_ERR_STATE, "state not bound");
+    DevState st = state_of(s);
+    LGS_DISPATCH(s, k_fk, s->md, st, s->N);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_actor_root_state_indexed(lgs_sim* s, const float* src, const int32_t* ids, int32_t n) {
+    if (!s || !src || (!ids && n > 0)) return set_err(LGS_ERR_ARG, "null argument");
+    if (src == s->root || n == 0) return LGS_OK;
+    const int total = n * 13;
+    hipLaunchKernelGGL(k_copy_rows, dim3((total + 255) / 256), dim3(256), 0, s->stream, s->root, src, ids, n, 13);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_dof_state_indexed(lgs_sim* s, const float* src, const int32_t* ids, int32_t n) {
+    if (!s || !src || (!ids && n > 0)) return set_err(LGS_ERR_ARG, "null argument");
+    if (src == s->dofs || n == 0) return LGS_OK;
+    const int w = 2 * s->D, total = n * w;
+    hipLaunchKernelGGL(k_copy_rows, dim3((total + 255) / 256), dim3(256), 0, s->stream, s->dofs, src, ids, n, w);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_task(lgs_sim* s, const lgs_task_params* t) {
+    if (!s || !t) return set_err(LGS_ERR_ARG, "null argument");
+    if (t->num_actions != s->D) return set_err(LGS_ERR_ARG, "lgs_set_task: num_actions must equal num_dofs");
+    if (t->num_obs > LGS_MAX_OBS || t->num_privileged_obs > LGS_MAX_OBS || t->num_rewards > LGS_MAX_REWARDS)
+        return set_err(LGS_ERR_ARG, "lgs_set_task: obs/reward counts exceed limits");
+    if (t->num_feet > LGS_MAX_FEET || t->resample_interval <= 0 || t->push_interval <= 0 || t->decimation <= 0)
+        return set_err(LGS_ERR_ARG, "lgs_set_task: invalid feet count / intervals / decimation");
+    for (int i = 0; i < t->num_feet; ++i)
+        if (t->feet_idx[i] < 0 || t->feet_idx[i] >= s->B) return set_err(LGS_ERR_ARG, "feet index out of range");
+    for (int i = 0; i < t->num_penalised; ++i)
+        if (t->penalised_idx[i] < 0 || t->penalised_idx[i] >= s->B) return set_err(LGS_ERR_ARG, "penalised index out of range");
+    for (int i = 0; i < t->num_termination; ++i)
+        if (t->termination_idx[i] < 0 || t->termination_idx[i] >= s->B) return set_err(LGS_ERR_ARG, "termination index out of range");
+    for (int i = 0; i < t->num_hip; ++i)
+        if (t->hip_dofs[i] < 0 || t->hip_dofs[i] >= s->D) return set_err(LGS_ERR_ARG, "hip dof out of range");
+    HIP_TRY(hipMemcpy(s->task_dev, t, sizeof(lgs_task_params), hipMemcpyHostToDevice));
+    s->has_task = 1;
+    return LGS_OK;
+}
+
+LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    if (!s || !env) return set_err(LGS_ERR_ARG, "null argument");
+    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_step: state not bound or task not set");
+    DevState st = state_of(s);
+    LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    if (!s || !env) return set_err(LGS_ERR_ARG, "null argument");
+    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_reset_all: state not bound or task not set");
+    DevState st = state_of(s);
+    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_get_counts(lgs_sim* s, int32_t* n, int32_t* b, int32_t* d) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    if (n) *n = s->N;
+    if (b) *b = s->B;
+    if (d) *d = s->D;
+    return LGS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,360 @@
+"""LeggedRobot on the MI355X-native simulator.
+
+Drop-in for the reference's ``legged_gym/envs/base/legged_robot.py`` (class
+``LeggedRobot``, :21-941): same constructor signature, same VecEnv attributes
+and buffers, same cfg semantics.  The difference is where the work happens:
+
+* ``step()`` (:615-647) is ONE launch of ``lgs_step`` — PD torques, the
+  decimation physics substeps and the whole ``post_physics_step`` (:673-709:
+  commands, termination, rewards, reset, push, observations) run in a HIP
+  kernel with one wavefront per env.  There are no per-term PyTorch ops and no
+  device->host syncs (the reference's ``nonzero()`` at :511, :545, :697 are
+  in-kernel masks).
+* ``create_sim`` builds the articulated model from the URDF (IsaacGym asset
+  semantics, :294-407) and hands it to ``libleggedsim``.
+
+Buffers that the caller keeps across a step (obs, privileged obs, resets,
+time-outs) are double-buffered, because the reference returns fresh tensors
+each step and rsl_rl holds references to them across the next ``step()``.
+"""
+import os
+
+import numpy as np
+import torch
+
+from isaacgym.torch_utils import get_axis_params, to_torch, torch_rand_float
+from legged_gym import LEGGED_GYM_ROOT_DIR
+from legged_gym.envs.base.base_task import BaseTask
+from legged_gym.utils.helpers import class_to_dict
+from leggedsim import cabi, native
+from leggedsim.model import load_model
+from leggedsim.task import build_task_params
+
+from .legged_robot_config import LeggedRobotCfg
+
+
+class LeggedRobot(BaseTask):
+    obs_layout = cabi.OBS_QUADRUPED
+    hip_dof_indices = ()
+    max_contacts = 8
+    max_rows = 32
+
+    def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
+        self.cfg = cfg
+        self.sim_params = sim_params
+        self.height_samples = None
+        self.debug_viz = False
+        self.init_done = False
+        self._parse_cfg(self.cfg)
+        super().__init__(self.cfg, sim_params, physics_engine, sim_device, headless)
+        self._init_buffers()
+        self._prepare_reward_function()
+        self._build_task()
+        self.init_done = True
+
+    # ------------------------------------------------------------ config ----
+    def _parse_cfg(self, cfg):
+        """legged_robot.py:52-67"""
+        self.dt = self.cfg.control.decimation * self.sim_params.dt
+        self.obs_scales = self.cfg.normalization.obs_scales
+        self.reward_scales = class_to_dict(self.cfg.rewards.scales)
+        self.command_ranges = class_to_dict(self.cfg.commands.ranges)
+        self.max_episode_length_s = self.cfg.env.episode_length_s
+        self.max_episode_length = np.ceil(self.max_episode_length_s / self.dt)
+        self.cfg.domain_rand.push_interval = np.ceil(self.cfg.domain_rand.push_interval_s / self.dt)
+
+    # ------------------------------------------------------------- sim ------
+    def create_sim(self):
+        """Model + native sim creation (legged_robot.py:223-242, 281-407, 412-483)."""
+        self.up_axis_idx = 2
+        asset_path = self.cfg.asset.file.format(LEGGED_GYM_ROOT_DIR=LEGGED_GYM_ROOT_DIR)
+        if not os.path.exists(asset_path) and os.environ.get("LEGGED_GYM_RESOURCES"):
+            rel = asset_path.split("resources/", 1)[-1]
+            asset_path = os.path.join(os.environ["LEGGED_GYM_RESOURCES"], rel)
+        model = load_model(asset_path, collapse_fixed_joints=self.cfg.asset.collapse_fixed_joints)
+        self.num_dof = model.num_dofs
+        self.num_bodies = model.num_bodies
+        self.dof_names = list(model.dof_names)
+        self.num_dofs = len(self.dof_names)
+        body_names = list(model.body_names)
+        self.body_names = body_names
+        feet_names = [s for s in body_names if self.cfg.asset.foot_name in s]
+        penalized = []
+        for name in self.cfg.asset.penalize_contacts_on:
+            penalized.extend([s for s in body_names if name in s])
+        termination = []
+        for name in self.cfg.asset.terminate_after_contacts_on:
+            termination.extend([s for s in body_names if name in s])
+        self.feet_indices = torch.tensor([body_names.index(n) for n in feet_names], dtype=torch.long, device=self.device)
+        self.penalised_contact_indices = torch.tensor([body_names.index(n) for n in penalized], dtype=torch.long,
+                                                      device=self.device)
+        self.termination_contact_indices = torch.tensor([body_names.index(n) for n in termination], dtype=torch.long,
+                                                        device=self.device)
+        model.reorder_points({body_names.index(n) for n in feet_names})
+        self.model = model
+
+        init = self.cfg.init_state
+        self.base_init_state = to_torch(init.pos + init.rot + init.lin_vel + init.ang_vel, device=self.device)
+        self._get_env_origins()
+
+        # DOF props (_process_dof_props, :456-469)
+        lo, hi = model.dof_lower.astype(np.float64), model.dof_upper.astype(np.float64)
+        self.dof_pos_limits = torch.zeros(self.num_dof, 2, dtype=torch.float, device=self.device)
+        m = (lo + hi) / 2
+        r = hi - lo
+        self.dof_pos_limits[:, 0] = torch.tensor(m - 0.5 * r * self.cfg.rewards.soft_dof_pos_limit)
+        self.dof_pos_limits[:, 1] = torch.tensor(m + 0.5 * r * self.cfg.rewards.soft_dof_pos_limit)
+        self.dof_vel_limits = torch.tensor(model.dof_velocity, dtype=torch.float, device=self.device)
+        self.torque_limits = torch.tensor(model.dof_effort, dtype=torch.float, device=self.device)
+
+        # shape friction buckets (_process_rigid_shape_props, :429-439): torch CPU RNG as the reference
+        friction = np.full(self.num_envs, self.cfg.terrain.static_friction, dtype=np.float32)
+        if self.cfg.domain_rand.randomize_friction:
+            fr = self.cfg.domain_rand.friction_range
+            bucket_ids = torch.randint(0, 64, (self.num_envs, 1))
+            buckets = torch_rand_float(fr[0], fr[1], (64, 1), device="cpu")
+            self.friction_coeffs = buckets[bucket_ids]
+            friction = self.friction_coeffs.view(-1).numpy().astype(np.float32)
+        # base mass (_process_rigid_body_props, :480-482)
+        added_mass = np.zeros(self.num_envs, dtype=np.float32)
+        if self.cfg.domain_rand.randomize_base_mass:
+            rng = self.cfg.domain_rand.added_mass_range
+            added_mass = np.array([np.random.uniform(rng[0], rng[1]) for _ in range(self.num_envs)], dtype=np.float32)
+        self.added_base_mass = added_mass
+
+        sp = cabi.sim_params_from_cfg(self.cfg.sim, self.cfg.asset, max_contacts=self.max_contacts,
+                                      max_rows=self.max_rows, ground_friction=float(self.cfg.terrain.static_friction))
+        self._lgs_params = sp
+        self.sim = native.Sim(model, sp, self.num_envs, self.sim_device_id)
+        self.sim.set_env_properties(friction, added_mass)
+        self.shape_friction = friction
+
+    def _create_ground_plane(self):
+        """The plane is the z = 0 half-space inside the contact kernel."""
+
+    def _get_env_origins(self):
+        """Grid of env origins (legged_robot.py:258-272)."""
+        self.custom_origins = False
+        self.env_origins = torch.zeros(self.num_envs, 3, device=self.device, requires_grad=False)
+        num_cols = np.floor(np.sqrt(self.num_envs))
+        num_rows = np.ceil(self.num_envs / num_cols)
+        xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
+        spacing = self.cfg.env.env_spacing
+        self.env_origins[:, 0] = spacing * xx.flatten()[: self.num_envs]
+        self.env_origins[:, 1] = spacing * yy.flatten()[: self.num_envs]
+        self.env_origins[:, 2] = 0.0
+
+    # --------------------------------------------------------- buffers ------
+    def _init_buffers(self):
+        """State tensors bound to the simulator + the env's working buffers (:69-186)."""
+        N, D, B, dev = self.num_envs, self.num_dof, self.num_bodies, self.device
+        self.root_states = torch.zeros(N, 13, dtype=torch.float, device=dev)
+        self.dof_state = torch.zeros(N * D, 2, dtype=torch.float, device=dev)
+        self._contact_forces = torch.zeros(N * B, 3, dtype=torch.float, device=dev)
+        self.rigid_body_states = torch.zeros(N * B, 13, dtype=torch.float, device=dev)
+        # initial placement: base_init_state at the origin with +-1 m xy jitter (:364-370)
+        self.root_states[:] = self.base_init_state
+        self.root_states[:, :3] += self.env_origins
+        self.root_states[:, :2] += torch_rand_float(-1.0, 1.0, (N, 2), device=dev)
+        self.dof_pos = self.dof_state.view(N, D, 2)[..., 0]
+        self.dof_vel = self.dof_state.view(N, D, 2)[..., 1]
+        self.base_quat = self.root_states[:, 3:7]
+        self.base_pos = self.root_states[:N, 0:3]
+        self.contact_forces = self._contact_forces.view(N, -1, 3)
+        self.rigid_body_states_view = self.rigid_body_states.view(N, -1, 13)
+        self.sim.bind(self.root_states, self.dof_state, self._contact_forces, self.rigid_body_states)
+        self._stream = None
+        self._sync_stream()
+
+        self.common_step_counter = 0
+        self.extras = {}
+        self.gravity_vec = to_torch(get_axis_params(-1.0, self.up_axis_idx), device=dev).repeat((N, 1))
+        self.forward_vec = to_torch([1.0, 0.0, 0.0], device=dev).repeat((N, 1))
+        self.torques = torch.zeros(N, self.num_actions, dtype=torch.float, device=dev)
+        self.p_gains = torch.zeros(self.num_actions, dtype=torch.float, device=dev)
+        self.d_gains = torch.zeros(self.num_actions, dtype=torch.float, device=dev)
+        self.actions = torch.zeros(N, self.num_actions, dtype=torch.float, device=dev)
+        self.last_actions = torch.zeros(N, self.num_actions, dtype=torch.float, device=dev)
+        self.last_dof_vel = torch.zeros(N, D, dtype=torch.float, device=dev)
+        self.last_root_vel = torch.zeros(N, 6, dtype=torch.float, device=dev)
+        self.commands = torch.zeros(N, self.cfg.commands.num_commands, dtype=torch.float, device=dev)
+        if self.commands.shape[1] != 4:
+            raise ValueError("the native step expects commands.num_commands == 4")
+        self.commands_scale = torch.tensor([self.obs_scales.lin_vel, self.obs_scales.lin_vel, self.obs_scales.ang_vel],
+                                           device=dev)
+        nf = len(self.feet_indices)
+        self.feet_air_time = torch.zeros(N, nf, dtype=torch.float, device=dev)
+        self.last_contacts = torch.zeros(N, nf, dtype=torch.bool, device=dev)
+        self.base_lin_vel = torch.zeros(N, 3, dtype=torch.float, device=dev)
+        self.base_ang_vel = torch.zeros(N, 3, dtype=torch.float, device=dev)
+        self.projected_gravity = torch.zeros(N, 3, dtype=torch.float, device=dev)
+        self.rpy = torch.zeros(N, 3, dtype=torch.float, device=dev)
+        self._episode_length = torch.zeros(N, dtype=torch.long, device=dev)
+        self.phase = torch.zeros(N, dtype=torch.float, device=dev)
+        self.leg_phase = torch.zeros(N, 2, dtype=torch.float, device=dev)
+        # double-buffered step outputs
+        P = self.num_privileged_obs
+        self._obs_bufs = [torch.zeros(N, self.num_obs, dtype=torch.float, device=dev) for _ in range(2)]
+        self._priv_bufs = [torch.zeros(N, P, dtype=torch.float, device=dev) for _ in range(2)] if P else [None, None]
+        self._reset_bufs = [torch.ones(N, dtype=torch.bool, device=dev) for _ in range(2)]
+        self._timeout_bufs = [torch.zeros(N, dtype=torch.bool, device=dev) for _ in range(2)]
+        self._buf_idx = 0
+        self.obs_buf = self._obs_bufs[0]
+        self.privileged_obs_buf = self._priv_bufs[0]
+        self.reset_buf = torch.ones(N, dtype=torch.long, device=dev)  # long at init, bool after a step (base_task.py:43)
+        self.time_out_buf = self._timeout_bufs[0]
+        self.rew_buf = torch.zeros(N, dtype=torch.float, device=dev)
+        self.noise_scale_vec = self._get_noise_scale_vec(self.cfg)
+
+        # default joint angles and PD gains by name substring, last match wins (:168-186)
+        self.default_dof_pos = torch.zeros(self.num_dof, dtype=torch.float, device=dev)
+        for i, name in enumerate(self.dof_names):
+            self.default_dof_pos[i] = self.cfg.init_state.default_joint_angles[name]
+            found = False
+            for key in self.cfg.control.stiffness.keys():
+                if key in name:
+                    self.p_gains[i] = self.cfg.control.stiffness[key]
+                    self.d_gains[i] = self.cfg.control.damping[key]
+                    found = True
+            if not found:
+                self.p_gains[i] = 0.0
+                self.d_gains[i] = 0.0
+                if self.cfg.control.control_type in ["P", "V"]:
+                    print(f"PD gain of joint {name} were not defined, setting them to zero")
+        self.default_dof_pos = self.default_dof_pos.unsqueeze(0)
+        self.dof_pos[:] = self.default_dof_pos
+
+    @property
+    def episode_length_buf(self):
+        return self._episode_length
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value):
+        # rsl_rl rebinds this attribute (randint_like) before learning; keep the
+        # kernel's buffer and copy the values in.
+        self._episode_length.copy_(value.to(device=self.device, dtype=torch.long))
+
+    def _get_noise_scale_vec(self, cfg):
+        """Quadruped layout (legged_robot.py:188-219)."""
+        noise_vec = torch.zeros_like(self.obs_buf[0])
+        self.add_noise = self.cfg.noise.add_noise
+        ns = self.cfg.noise.noise_scales
+        lvl = self.cfg.noise.noise_level
+        A = self.num_actions
+        noise_vec[:3] = ns.lin_vel * lvl * self.obs_scales.lin_vel
+        noise_vec[3:6] = ns.ang_vel * lvl * self.obs_scales.ang_vel
+        noise_vec[6:9] = ns.gravity * lvl
+        noise_vec[9:12] = 0.0
+        noise_vec[12:12 + A] = ns.dof_pos * lvl * self.obs_scales.dof_pos
+        noise_vec[12 + A:12 + 2 * A] = ns.dof_vel * lvl * self.obs_scales.dof_vel
+        noise_vec[12 + 2 * A:12 + 3 * A] = 0.0
+        return noise_vec
+
+    def _prepare_reward_function(self):
+        """Drop zero scales, multiply the rest by dt; dict order = alphabetical (:817-840)."""
+        for key in list(self.reward_scales.keys()):
+            if self.reward_scales[key] == 0:
+                self.reward_scales.pop(key)
+            else:
+                self.reward_scales[key] *= self.dt
+        self.reward_names = [n for n in self.reward_scales if n != "termination"]
+        for n in self.reward_names:
+            rid = cabi.REWARD_ALIASES.get(n, n)
+            if rid not in cabi.REWARD_ID:
+                raise AttributeError(f"'{type(self).__name__}' has no native reward term '_reward_{n}'")
+        self._sum_names = list(self.reward_names) + (["termination"] if "termination" in self.reward_scales else [])
+        nsum = len(self._sum_names)
+        self._episode_sums = torch.zeros(nsum, self.num_envs, dtype=torch.float, device=self.device)
+        self.episode_sums = {name: self._episode_sums[i] for i, name in enumerate(self._sum_names)}
+        self._episode_acc = torch.zeros(nsum + 1, dtype=torch.float, device=self.device)
+        self._ep_means = torch.zeros(nsum, dtype=torch.float, device=self.device)
+
+    # ------------------------------------------------------ native task -----
+    def _build_task(self):
+        self.task_params = build_task_params(self)
+        self.sim.set_task(self.task_params)
+        self._env_structs = [self._make_env_struct(i) for i in range(2)]
+
+    def _make_env_struct(self, i):
+        E = cabi.EnvBuffers()
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        E.actions = p(self.actions)
+        E.last_actions = p(self.last_actions)
+        E.last_dof_vel = p(self.last_dof_vel)
+        E.last_root_vel = p(self.last_root_vel)
+        E.torques = p(self.torques)
+        E.commands = p(self.commands)
+        E.feet_air_time = p(self.feet_air_time)
+        E.last_contacts = p(self.last_contacts)
+        E.episode_length = p(self._episode_length)
+        E.obs = p(self._obs_bufs[i])
+        E.priv_obs = p(self._priv_bufs[i])
+        E.rew = p(self.rew_buf)
+        E.reset = p(self._reset_bufs[i])
+        E.time_out = p(self._timeout_bufs[i])
+        E.episode_sums = p(self._episode_sums)
+        E.episode_acc = p(self._episode_acc)
+        E.base_lin_vel = p(self.base_lin_vel)
+        E.base_ang_vel = p(self.base_ang_vel)
+        E.projected_gravity = p(self.projected_gravity)
+        E.rpy = p(self.rpy)
+        E.env_origins = p(self.env_origins)
+        E.phase = p(self.phase)
+        E.leg_phase = p(self.leg_phase)
+        E.rew_terms = None
+        return E
+
+    def _sync_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream:
+            self.sim.set_stream(s)
+            self._stream = s
+
+    # ------------------------------------------------------------ step ------
+    def step(self, actions):
+        """Apply actions, simulate `decimation` substeps, post-physics; one launch."""
+        self._sync_stream()
+        self._buf_idx ^= 1
+        i = self._buf_idx
+        self.actions.copy_(actions)
+        self._episode_acc.zero_()
+        self.sim.step(self._env_structs[i], self.common_step_counter)
+        self.common_step_counter += 1
+        self.obs_buf = self._obs_bufs[i]
+        self.privileged_obs_buf = self._priv_bufs[i]
+        self.reset_buf = self._reset_bufs[i]
+        self.time_out_buf = self._timeout_bufs[i]
+        self._update_extras()
+        return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    def _update_extras(self):
+        """extras["episode"] / ["time_outs"] refresh only when >= 1 env reset (:742-768)."""
+        nsum = len(self._sum_names)
+        cnt = self._episode_acc[nsum]
+        any_reset = cnt > 0
+        means = self._episode_acc[:nsum] / cnt.clamp(min=1.0) / self.max_episode_length_s
+        self._ep_means = torch.where(any_reset, means, self._ep_means)
+        self.extras["episode"] = {"rew_" + k: self._ep_means[i] for i, k in enumerate(self._sum_names)}
+        if self.cfg.env.send_timeouts:
+            prev = self.extras.get("time_outs", self.time_out_buf)
+            self.extras["time_outs"] = torch.where(any_reset, self.time_out_buf, prev)
+
+    def reset_idx(self, env_ids):
+        """Reset the given envs.  The native kernel resets every env of the batch
+        (BaseTask.reset's use); arbitrary subsets go through reset_buf masks in step()."""
+        if len(env_ids) == 0:
+            return
+        if len(env_ids) != self.num_envs:
+            raise NotImplementedError("reset_idx of a subset: resets happen inside step() from reset_buf")
+        self._sync_stream()
+        self.sim.reset_all(self._env_structs[self._buf_idx], self.common_step_counter)
+        self.extras["episode"] = {"rew_" + k: self._ep_means[i] for i, k in enumerate(self._sum_names)}
+        if self.cfg.env.send_timeouts:
+            self.extras["time_outs"] = self.time_out_buf
+
+    def post_physics_step(self):
+        raise RuntimeError("post_physics_step runs inside the fused native step()")
+
+    # -------------------------------------------------------- utilities -----
+    def close(self):
+        self.sim.close()

@@ -1,0 +1,40 @@
+"""Roll out / export a trained policy (reference scripts/play.py:15-51; same CLI)."""
+import os
+
+import isaacgym  # noqa: F401
+from legged_gym import LEGGED_GYM_ROOT_DIR
+from legged_gym.envs import *  # noqa: F401,F403
+from legged_gym.utils import export_policy_as_jit, get_args, task_registry
+
+EXPORT_POLICY = True
+
+
+def play(args, num_steps=None):
+    env_cfg, train_cfg = task_registry.get_cfgs(name=args.task)
+    env_cfg.env.num_envs = min(env_cfg.env.num_envs, 100)
+    env_cfg.terrain.num_rows = 5
+    env_cfg.terrain.num_cols = 5
+    env_cfg.terrain.curriculum = False
+    env_cfg.noise.add_noise = False
+    env_cfg.domain_rand.randomize_friction = False
+    env_cfg.domain_rand.push_robots = False
+    env_cfg.env.test = True
+
+    env, _ = task_registry.make_env(name=args.task, args=args, env_cfg=env_cfg)
+    obs = env.get_observations()
+    train_cfg.runner.resume = True
+    ppo_runner, train_cfg = task_registry.make_alg_runner(env=env, name=args.task, args=args, train_cfg=train_cfg)
+    policy = ppo_runner.get_inference_policy(device=env.device)
+    if EXPORT_POLICY:
+        path = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name, "exported", "policies")
+        export_policy_as_jit(ppo_runner.alg.actor_critic, path)
+        print("Exported policy as jit script to: ", path)
+    steps = num_steps if num_steps is not None else 10 * int(env.max_episode_length)
+    for _ in range(steps):
+        actions = policy(obs.detach())
+        obs, _, rews, dones, infos = env.step(actions.detach())
+    return env
+
+
+if __name__ == "__main__":
+    play(get_args())

@@ -1,0 +1,155 @@
+"""Loader for the HIP simulator ``libleggedsim.so`` (the product path).
+
+There is deliberately no CPU fallback: if the library or a GPU is missing the
+env raises.  Build with ``make -C unitree-rl-gym_amd/csrc`` or
+``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import cabi
+
+_LIB = None
+LIB_NAME = "libleggedsim.so"
+
+
+def lib_path():
+    env = os.environ.get("LEGGEDSIM_LIB")
+    if env:
+        return env
+    here = os.path.dirname(os.path.abspath(__file__))
+    return os.path.join(os.path.dirname(here), "csrc", "build", LIB_NAME)
+
+
+class LeggedSimError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libleggedsim.so.  torch must be imported first so that the library
+    binds to the same HIP runtime (same SONAME) torch already loaded."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (HIP runtime first, see docstring)
+
+    p = lib_path()
+    if not os.path.exists(p):
+        raise LeggedSimError(
+            f"HIP simulator library not found at {p}; build it with `make -C unitree-rl-gym_amd/csrc` "
+            "(no CPU fallback exists for the product path)")
+    lib = C.CDLL(p)
+    vp = C.c_void_p
+    lib.lgs_last_error.restype = C.c_char_p
+    lib.lgs_version.restype = C.c_int
+    lib.lgs_uniform.restype = C.c_float
+    lib.lgs_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.lgs_create_sim.argtypes = [C.POINTER(cabi.ModelDesc), C.POINTER(cabi.SimParams), C.c_int32, C.c_int32,
+                                   C.POINTER(vp)]
+    lib.lgs_destroy_sim.argtypes = [vp]
+    lib.lgs_set_stream.argtypes = [vp, vp]
+    lib.lgs_synchronize.argtypes = [vp]
+    lib.lgs_set_env_properties.argtypes = [vp, vp, vp]
+    lib.lgs_bind_state.argtypes = [vp, vp, vp, vp, vp]
+    lib.lgs_refresh.argtypes = [vp]
+    lib.lgs_set_dof_actuation_force.argtypes = [vp, vp]
+    lib.lgs_simulate.argtypes = [vp]
+    lib.lgs_forward_kinematics.argtypes = [vp]
+    lib.lgs_set_actor_root_state_indexed.argtypes = [vp, vp, vp, C.c_int32]
+    lib.lgs_set_dof_state_indexed.argtypes = [vp, vp, vp, C.c_int32]
+    lib.lgs_set_task.argtypes = [vp, C.POINTER(cabi.TaskParams)]
+    lib.lgs_step.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_reset_all.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
+                 "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
+                 "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
+                 "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts"):
+        getattr(lib, name).restype = C.c_int
+    _LIB = lib
+    return lib
+
+
+def check(lib, status, what):
+    if status != 0:
+        raise LeggedSimError(f"{what} failed ({status}): {lib.lgs_last_error().decode(errors='replace')}")
+
+
+EXPORTED_SYMBOLS = [
+    "lgs_last_error", "lgs_version", "lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize",
+    "lgs_set_env_properties", "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
+    "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
+    "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform",
+]
+
+
+class Sim:
+    """Thin owner of an ``lgs_sim*`` bound to caller-owned torch state tensors."""
+
+    def __init__(self, model, sim_params: cabi.SimParams, num_envs: int, device_id: int):
+        self.lib = load()
+        self.model = model
+        self._mh = cabi.ModelHandle(model)
+        self._sp = sim_params
+        h = C.c_void_p()
+        check(self.lib, self.lib.lgs_create_sim(C.byref(self._mh.desc), C.byref(sim_params), num_envs, device_id,
+                                                C.byref(h)), "lgs_create_sim")
+        self.handle = h
+        self.num_envs = num_envs
+
+    def set_stream(self, stream_ptr):
+        check(self.lib, self.lib.lgs_set_stream(self.handle, C.c_void_p(stream_ptr)), "lgs_set_stream")
+
+    def set_env_properties(self, friction=None, added_mass=None):
+        import numpy as np
+        f = None if friction is None else np.ascontiguousarray(friction, dtype=np.float32)
+        m = None if added_mass is None else np.ascontiguousarray(added_mass, dtype=np.float32)
+        check(self.lib, self.lib.lgs_set_env_properties(
+            self.handle, None if f is None else f.ctypes.data, None if m is None else m.ctypes.data),
+            "lgs_set_env_properties")
+
+    def bind(self, root, dofs, cforce, rbs):
+        for t in (root, dofs, cforce, rbs):
+            assert t.is_cuda and t.is_contiguous() and str(t.dtype) == "torch.float32"
+        self._bound = (root, dofs, cforce, rbs)
+        check(self.lib, self.lib.lgs_bind_state(self.handle, root.data_ptr(), dofs.data_ptr(), cforce.data_ptr(),
+                                                rbs.data_ptr()), "lgs_bind_state")
+
+    def set_task(self, task: cabi.TaskParams):
+        self._task = task
+        check(self.lib, self.lib.lgs_set_task(self.handle, C.byref(task)), "lgs_set_task")
+
+    def step(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_step(self.handle, C.byref(env_bufs), step_counter), "lgs_step")
+
+    def reset_all(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_reset_all(self.handle, C.byref(env_bufs), step_counter), "lgs_reset_all")
+
+    def simulate(self, torques):
+        self._tau = torques
+        check(self.lib, self.lib.lgs_set_dof_actuation_force(self.handle, torques.data_ptr()), "set_dof_actuation_force")
+        check(self.lib, self.lib.lgs_simulate(self.handle), "lgs_simulate")
+
+    def forward_kinematics(self):
+        check(self.lib, self.lib.lgs_forward_kinematics(self.handle), "lgs_forward_kinematics")
+
+    def set_root_indexed(self, src, ids_i32, n):
+        check(self.lib, self.lib.lgs_set_actor_root_state_indexed(self.handle, src.data_ptr(), ids_i32.data_ptr(), n),
+              "set_actor_root_state_indexed")
+
+    def set_dof_indexed(self, src, ids_i32, n):
+        check(self.lib, self.lib.lgs_set_dof_state_indexed(self.handle, src.data_ptr(), ids_i32.data_ptr(), n),
+              "set_dof_state_indexed")
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.lgs_destroy_sim(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,196 @@
+"""PPO with clipped surrogate / clipped value loss / adaptive-KL learning rate
+(rsl_rl v1.0.2 semantics).
+
+ROCm-specific changes that do not change the maths:
+* the adaptive learning rate lives in a device tensor consumed by Adam, so the
+  KL test costs no host sync per mini-batch (the reference does 1 + 2 .item()s);
+* losses are accumulated on the device and read once per update;
+* with torch.distributed initialised (one process per GPU, RCCL), the gradient
+  is flattened into ONE bucket and all-reduced (mean) per optimizer step, the
+  mini-batch KL is averaged across ranks before the LR decision, and advantages
+  are normalised with global statistics — so N ranks behave like one batch of
+  N x num_envs envs.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.optim as optim
+
+from rsl_rl.modules import ActorCritic
+from rsl_rl.storage import RolloutStorage
+
+
+def _dist_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
+class PPO:
+    actor_critic: ActorCritic
+
+    def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998, lam=0.95,
+                 value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+        self.device = device
+        self.desired_kl = desired_kl
+        self.schedule = schedule
+        self.actor_critic = actor_critic
+        self.actor_critic.to(self.device)
+        self.storage = None
+        self._lr = torch.tensor(float(learning_rate), device=self.device)
+        params = list(self.actor_critic.parameters())
+        on_gpu = str(self.device).startswith("cuda")
+        try:
+            self.optimizer = optim.Adam(params, lr=self._lr if on_gpu else float(learning_rate),
+                                        fused=True if on_gpu else None)
+        except (RuntimeError, TypeError, ValueError):
+            self.optimizer = optim.Adam(params, lr=float(learning_rate))
+        self._lr_is_tensor = torch.is_tensor(self.optimizer.param_groups[0]["lr"])
+        self.transition = RolloutStorage.Transition()
+        self.clip_param = clip_param
+        self.num_learning_epochs = num_learning_epochs
+        self.num_mini_batches = num_mini_batches
+        self.value_loss_coef = value_loss_coef
+        self.entropy_coef = entropy_coef
+        self.gamma = gamma
+        self.lam = lam
+        self.max_grad_norm = max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.world_size = _dist_world()
+        if self.world_size > 1:
+            for p in params:  # identical initial policy on every rank
+                dist.broadcast(p.data, src=0)
+
+    # learning_rate is read by the runner's logger (rsl_rl attribute)
+    @property
+    def learning_rate(self):
+        return float(self._lr)
+
+    @learning_rate.setter
+    def learning_rate(self, v):
+        self._lr.fill_(float(v))
+        if not self._lr_is_tensor:
+            for g in self.optimizer.param_groups:
+                g["lr"] = float(v)
+
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                                      action_shape, self.device)
+
+    def test_mode(self):
+        self.actor_critic.eval()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def act(self, obs, critic_obs):
+        if self.actor_critic.is_recurrent:
+            self.transition.hidden_states = self.actor_critic.get_hidden_states()
+        self.transition.actions = self.actor_critic.act(obs).detach()
+        self.transition.values = self.actor_critic.evaluate(critic_obs).detach()
+        self.transition.actions_log_prob = self.actor_critic.get_actions_log_prob(self.transition.actions).detach()
+        self.transition.action_mean = self.actor_critic.action_mean.detach()
+        self.transition.action_sigma = self.actor_critic.action_std.detach()
+        self.transition.observations = obs
+        self.transition.critic_observations = critic_obs
+        return self.transition.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        self.transition.rewards = rewards.clone()
+        self.transition.dones = dones
+        if "time_outs" in infos:  # bootstrap on time-outs
+            self.transition.rewards += self.gamma * torch.squeeze(
+                self.transition.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(self.transition)
+        self.transition.clear()
+        self.actor_critic.reset(dones)
+
+    def _global_adv_stats(self, adv):
+        n = torch.tensor(float(adv.numel()), device=adv.device)
+        s = torch.stack([adv.sum(), (adv * adv).sum(), n])
+        dist.all_reduce(s)
+        mean = s[0] / s[2]
+        var = (s[1] - s[2] * mean * mean) / (s[2] - 1.0)
+        return mean, torch.sqrt(var.clamp(min=0.0))
+
+    def compute_returns(self, last_critic_obs):
+        last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        stats = self._global_adv_stats if self.world_size > 1 else None
+        self.storage.compute_returns(last_values, self.gamma, self.lam, adv_stats=stats)
+
+    def _allreduce_grads(self):
+        grads = [p.grad for p in self.actor_critic.parameters() if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat)
+        flat /= self.world_size
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+    def update(self):
+        dev = self.device
+        sum_value_loss = torch.zeros((), device=dev)
+        sum_surrogate_loss = torch.zeros((), device=dev)
+        if self.actor_critic.is_recurrent:
+            generator = self.storage.reccurent_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        else:
+            generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
+             old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
+            self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+            actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
+            value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch,
+                                                     hidden_states=hid_states_batch[1])
+            mu_batch = self.actor_critic.action_mean
+            sigma_batch = self.actor_critic.action_std
+            entropy_batch = self.actor_critic.entropy
+
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                with torch.inference_mode():
+                    kl = torch.sum(torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
+                                   + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
+                                   / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
+                    kl_mean = torch.mean(kl)
+                    if self.world_size > 1:
+                        dist.all_reduce(kl_mean)
+                        kl_mean /= self.world_size
+                    lr = self._lr
+                    new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
+                                         torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
+                                                     torch.clamp(lr * 1.5, max=1e-2), lr))
+                self._lr.copy_(new_lr)
+                if not self._lr_is_tensor:
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = float(self._lr)
+
+            ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
+            surrogate = -torch.squeeze(advantages_batch) * ratio
+            surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
+                                                                               1.0 + self.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            if self.use_clipped_value_loss:
+                value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
+                                                                                                self.clip_param)
+                value_losses = (value_batch - returns_batch).pow(2)
+                value_losses_clipped = (value_clipped - returns_batch).pow(2)
+                value_loss = torch.max(value_losses, value_losses_clipped).mean()
+            else:
+                value_loss = (returns_batch - value_batch).pow(2).mean()
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+
+            self.optimizer.zero_grad()
+            loss.backward()
+            if self.world_size > 1:
+                self._allreduce_grads()
+            nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
+            self.optimizer.step()
+            sum_value_loss += value_loss.detach()
+            sum_surrogate_loss += surrogate_loss.detach()
+
+        num_updates = self.num_learning_epochs * self.num_mini_batches
+        means = (torch.stack([sum_value_loss, sum_surrogate_loss]) / num_updates).tolist()
+        self.storage.clear()
+        return means[0], means[1]

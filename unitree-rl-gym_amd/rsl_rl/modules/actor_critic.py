@@ -1,0 +1,95 @@
+import torch
+import torch.nn as nn
+from torch.distributions import Normal
+
+
+def get_activation(name):
+    table = {"elu": nn.ELU(), "selu": nn.SELU(), "relu": nn.ReLU(), "crelu": nn.ReLU(), "lrelu": nn.LeakyReLU(),
+             "tanh": nn.Tanh(), "sigmoid": nn.Sigmoid()}
+    if name not in table:
+        print("invalid activation function!")
+        return None
+    return table[name]
+
+
+def mlp(in_dim, hidden, out_dim, activation):
+    layers = [nn.Linear(in_dim, hidden[0]), activation]
+    for i in range(len(hidden)):
+        if i == len(hidden) - 1:
+            layers.append(nn.Linear(hidden[i], out_dim))
+        else:
+            layers.append(nn.Linear(hidden[i], hidden[i + 1]))
+            layers.append(activation)
+    return nn.Sequential(*layers)
+
+
+class ActorCritic(nn.Module):
+    """Gaussian MLP actor + MLP critic (rsl_rl v1.0.2 ActorCritic).
+
+    ``mixed_precision=True`` runs the Linear layers under bf16 autocast (MFMA
+    GEMMs on MI355X) while parameters, the distribution and all losses stay fp32.
+    """
+    is_recurrent = False
+
+    def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=[256, 256, 256],
+                 critic_hidden_dims=[256, 256, 256], activation="elu", init_noise_std=1.0, mixed_precision=True,
+                 **kwargs):
+        if kwargs:
+            print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str([k for k in kwargs]))
+        super().__init__()
+        act = get_activation(activation)
+        self.actor = mlp(num_actor_obs, actor_hidden_dims, num_actions, act)
+        self.critic = mlp(num_critic_obs, critic_hidden_dims, 1, act)
+        print(f"Actor MLP: {self.actor}")
+        print(f"Critic MLP: {self.critic}")
+        self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
+        self.distribution = None
+        self.mixed_precision = mixed_precision
+        Normal.set_default_validate_args = False
+
+    def _run(self, net, x):
+        if self.mixed_precision and x.is_cuda:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = net(x)
+            return y.float()
+        return net(x)
+
+    @staticmethod
+    def init_weights(sequential, scales):
+        [torch.nn.init.orthogonal_(module.weight, gain=scales[idx]) for idx, module in
+         enumerate(mod for mod in sequential if isinstance(mod, nn.Linear))]
+
+    def reset(self, dones=None):
+        pass
+
+    def forward(self):
+        raise NotImplementedError
+
+    @property
+    def action_mean(self):
+        return self.distribution.mean
+
+    @property
+    def action_std(self):
+        return self.distribution.stddev
+
+    @property
+    def entropy(self):
+        return self.distribution.entropy().sum(dim=-1)
+
+    def update_distribution(self, observations):
+        mean = self._run(self.actor, observations)
+        self.distribution = Normal(mean, mean * 0.0 + self.std)
+
+    def act(self, observations, **kwargs):
+        self.update_distribution(observations)
+        return self.distribution.sample()
+
+    def get_actions_log_prob(self, actions):
+        return self.distribution.log_prob(actions).sum(dim=-1)
+
+    def act_inference(self, observations):
+        return self._run(self.actor, observations)
+
+    def evaluate(self, critic_observations, **kwargs):
+        return self._run(self.critic, critic_observations)

@@ -1,0 +1,196 @@
+"""OnPolicyRunner (rsl_rl v1.0.2 API; call sites task_registry.py:119,126,
+train.py:14, play.py:34,39).  Checkpoint dict keys and log tags are the same."""
+import json
+import os
+import statistics
+import time
+from collections import deque
+
+import torch
+import torch.distributed as dist
+
+from rsl_rl.algorithms import PPO  # noqa: F401  (eval'd by name)
+from rsl_rl.env import VecEnv
+from rsl_rl.modules import ActorCritic, ActorCriticRecurrent  # noqa: F401  (eval'd by name)
+
+
+class _JsonlWriter:
+    """Fallback when tensorboard is not installed: one JSON line per scalar."""
+
+    def __init__(self, log_dir, flush_secs=10):
+        os.makedirs(log_dir, exist_ok=True)
+        self._f = open(os.path.join(log_dir, "scalars.jsonl"), "a")
+
+    def add_scalar(self, tag, value, step):
+        self._f.write(json.dumps({"tag": tag, "value": float(value), "step": int(step)}) + "\n")
+
+    def flush(self):
+        self._f.flush()
+
+    def close(self):
+        self._f.close()
+
+
+def _make_writer(log_dir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(log_dir=log_dir, flush_secs=10)
+    except Exception:
+        return _JsonlWriter(log_dir)
+
+
+class OnPolicyRunner:
+    def __init__(self, env: VecEnv, train_cfg, log_dir=None, device="cpu"):
+        self.cfg = train_cfg["runner"]
+        self.alg_cfg = train_cfg["algorithm"]
+        self.policy_cfg = train_cfg["policy"]
+        self.device = device
+        self.env = env
+        num_critic_obs = self.env.num_privileged_obs if self.env.num_privileged_obs is not None else self.env.num_obs
+        actor_critic_class = eval(self.cfg["policy_class_name"])
+        actor_critic = actor_critic_class(self.env.num_obs, num_critic_obs, self.env.num_actions,
+                                          **self.policy_cfg).to(self.device)
+        alg_class = eval(self.cfg["algorithm_class_name"])
+        self.alg: PPO = alg_class(actor_critic, device=self.device, **self.alg_cfg)
+        self.num_steps_per_env = self.cfg["num_steps_per_env"]
+        self.save_interval = self.cfg["save_interval"]
+        self.alg.init_storage(self.env.num_envs, self.num_steps_per_env, [self.env.num_obs],
+                              [self.env.num_privileged_obs], [self.env.num_actions])
+        self.is_main = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+        self.log_dir = log_dir if self.is_main else None
+        self.writer = None
+        self.tot_timesteps = 0
+        self.tot_time = 0
+        self.current_learning_iteration = 0
+        _, _ = self.env.reset()
+
+    def learn(self, num_learning_iterations, init_at_random_ep_len=False):
+        if self.log_dir is not None and self.writer is None:
+            self.writer = _make_writer(self.log_dir)
+        if init_at_random_ep_len:
+            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
+                                                             high=int(self.env.max_episode_length))
+        obs = self.env.get_observations()
+        privileged_obs = self.env.get_privileged_observations()
+        critic_obs = privileged_obs if privileged_obs is not None else obs
+        obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+        self.alg.actor_critic.train()
+
+        ep_infos = []
+        rewbuffer = deque(maxlen=100)
+        lenbuffer = deque(maxlen=100)
+        cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        sync = (lambda: torch.cuda.synchronize(self.device)) if str(self.device).startswith("cuda") else (lambda: None)
+
+        tot_iter = self.current_learning_iteration + num_learning_iterations
+        for it in range(self.current_learning_iteration, tot_iter):
+            start = time.time()
+            with torch.inference_mode():
+                for _ in range(self.num_steps_per_env):
+                    actions = self.alg.act(obs, critic_obs)
+                    obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
+                    critic_obs = privileged_obs if privileged_obs is not None else obs
+                    obs, critic_obs, rewards, dones = (obs.to(self.device), critic_obs.to(self.device),
+                                                       rewards.to(self.device), dones.to(self.device))
+                    self.alg.process_env_step(rewards, dones, infos)
+                    if self.log_dir is not None:
+                        if "episode" in infos:
+                            ep_infos.append(infos["episode"])
+                        cur_reward_sum += rewards
+                        cur_episode_length += 1
+                        new_ids = (dones > 0).nonzero(as_tuple=False)
+                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                        cur_reward_sum[new_ids] = 0
+                        cur_episode_length[new_ids] = 0
+                sync()
+                stop = time.time()
+                collection_time = stop - start
+                start = stop
+                self.alg.compute_returns(critic_obs)
+            mean_value_loss, mean_surrogate_loss = self.alg.update()
+            sync()
+            stop = time.time()
+            learn_time = stop - start
+            if self.log_dir is not None:
+                self.log(locals())
+                if it % self.save_interval == 0:
+                    self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
+            ep_infos.clear()
+            self.last_iteration_times = (collection_time, learn_time)
+        self.current_learning_iteration += num_learning_iterations
+        if self.log_dir is not None:
+            self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))
+
+    def log(self, locs, width=80, pad=35):
+        ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.tot_timesteps += self.num_steps_per_env * self.env.num_envs * ws
+        self.tot_time += locs["collection_time"] + locs["learn_time"]
+        iteration_time = locs["collection_time"] + locs["learn_time"]
+        it = locs["it"]
+        ep_string = ""
+        if locs["ep_infos"]:
+            for key in locs["ep_infos"][0]:
+                infotensor = torch.tensor([], device=self.device)
+                for ep_info in locs["ep_infos"]:
+                    v = ep_info[key]
+                    if not isinstance(v, torch.Tensor):
+                        v = torch.Tensor([v])
+                    if len(v.shape) == 0:
+                        v = v.unsqueeze(0)
+                    infotensor = torch.cat((infotensor, v.to(self.device)))
+                value = torch.mean(infotensor)
+                self.writer.add_scalar("Episode/" + key, value, it)
+                ep_string += f"""{f'Mean episode {key}:':>{pad}} {value:.4f}\n"""
+        mean_std = self.alg.actor_critic.std.mean()
+        fps = int(self.num_steps_per_env * self.env.num_envs * ws / iteration_time)
+        self.writer.add_scalar("Loss/value_function", locs["mean_value_loss"], it)
+        self.writer.add_scalar("Loss/surrogate", locs["mean_surrogate_loss"], it)
+        self.writer.add_scalar("Loss/learning_rate", self.alg.learning_rate, it)
+        self.writer.add_scalar("Policy/mean_noise_std", mean_std.item(), it)
+        self.writer.add_scalar("Perf/total_fps", fps, it)
+        self.writer.add_scalar("Perf/collection time", locs["collection_time"], it)
+        self.writer.add_scalar("Perf/learning_time", locs["learn_time"], it)
+        if len(locs["rewbuffer"]) > 0:
+            self.writer.add_scalar("Train/mean_reward", statistics.mean(locs["rewbuffer"]), it)
+            self.writer.add_scalar("Train/mean_episode_length", statistics.mean(locs["lenbuffer"]), it)
+            self.writer.add_scalar("Train/mean_reward/time", statistics.mean(locs["rewbuffer"]), self.tot_time)
+            self.writer.add_scalar("Train/mean_episode_length/time", statistics.mean(locs["lenbuffer"]), self.tot_time)
+        head = f" \033[1m Learning iteration {it}/{locs['tot_iter']} \033[0m "
+        lines = [
+            "#" * width, head.center(width, " "), "",
+            f"""{'Computation:':>{pad}} {fps:.0f} steps/s (collection: {locs['collection_time']:.3f}s, learning {locs['learn_time']:.3f}s)""",
+            f"""{'Value function loss:':>{pad}} {locs['mean_value_loss']:.4f}""",
+            f"""{'Surrogate loss:':>{pad}} {locs['mean_surrogate_loss']:.4f}""",
+            f"""{'Mean action noise std:':>{pad}} {mean_std.item():.2f}""",
+        ]
+        if len(locs["rewbuffer"]) > 0:
+            lines += [f"""{'Mean reward:':>{pad}} {statistics.mean(locs['rewbuffer']):.2f}""",
+                      f"""{'Mean episode length:':>{pad}} {statistics.mean(locs['lenbuffer']):.2f}"""]
+        lines += [ep_string.rstrip("\n"), "-" * width,
+                  f"""{'Total timesteps:':>{pad}} {self.tot_timesteps}""",
+                  f"""{'Iteration time:':>{pad}} {iteration_time:.2f}s""",
+                  f"""{'Total time:':>{pad}} {self.tot_time:.2f}s""",
+                  f"""{'ETA:':>{pad}} {self.tot_time / (it + 1) * (locs['num_learning_iterations'] - it):.1f}s"""]
+        print("\n".join(lines))
+
+    def save(self, path, infos=None):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        torch.save({"model_state_dict": self.alg.actor_critic.state_dict(),
+                    "optimizer_state_dict": self.alg.optimizer.state_dict(),
+                    "iter": self.current_learning_iteration, "infos": infos}, path)
+
+    def load(self, path, load_optimizer=True):
+        loaded = torch.load(path, map_location=self.device, weights_only=True)
+        self.alg.actor_critic.load_state_dict(loaded["model_state_dict"])
+        if load_optimizer:
+            self.alg.optimizer.load_state_dict(loaded["optimizer_state_dict"])
+        self.current_learning_iteration = loaded["iter"]
+        return loaded["infos"]
+
+    def get_inference_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_inference
