@@ -3,8 +3,6 @@
 privileged obs = [base lin vel, obs], feet rigid-body state, and the five extra
 reward terms.  All of it is computed inside the native step; this class only
 selects the humanoid layout and exposes the same attributes."""
-import torch
-
 from leggedsim import cabi
 
 from .legged_robot import LeggedRobot
@@ -14,22 +12,6 @@ class HumanoidRobot(LeggedRobot):
     obs_layout = cabi.OBS_HUMANOID
     max_contacts = 12
     max_rows = 48
-
-    def _get_noise_scale_vec(self, cfg):
-        """h1_env.py:10-31"""
-        noise_vec = torch.zeros_like(self.obs_buf[0])
-        self.add_noise = self.cfg.noise.add_noise
-        ns = self.cfg.noise.noise_scales
-        lvl = self.cfg.noise.noise_level
-        A = self.num_actions
-        noise_vec[:3] = ns.ang_vel * lvl * self.obs_scales.ang_vel
-        noise_vec[3:6] = ns.gravity * lvl
-        noise_vec[6:9] = 0.0
-        noise_vec[9:9 + A] = ns.dof_pos * lvl * self.obs_scales.dof_pos
-        noise_vec[9 + A:9 + 2 * A] = ns.dof_vel * lvl * self.obs_scales.dof_vel
-        noise_vec[9 + 2 * A:9 + 3 * A] = 0.0
-        noise_vec[9 + 3 * A:9 + 3 * A + 2] = 0.0
-        return noise_vec
 
     def _init_buffers(self):
         super()._init_buffers()

@@ -30,6 +30,7 @@ from leggedsim import cabi, native
 from leggedsim.model import load_model
 from leggedsim.task import build_task_params
 
+from .env_spec import derive_env_spec
 from .legged_robot_config import LeggedRobotCfg
 
 
@@ -72,40 +73,25 @@ class LeggedRobot(BaseTask):
             rel = asset_path.split("resources/", 1)[-1]
             asset_path = os.path.join(os.environ["LEGGED_GYM_RESOURCES"], rel)
         model = load_model(asset_path, collapse_fixed_joints=self.cfg.asset.collapse_fixed_joints)
-        self.num_dof = model.num_dofs
-        self.num_bodies = model.num_bodies
-        self.dof_names = list(model.dof_names)
-        self.num_dofs = len(self.dof_names)
-        body_names = list(model.body_names)
-        self.body_names = body_names
-        feet_names = [s for s in body_names if self.cfg.asset.foot_name in s]
-        penalized = []
-        for name in self.cfg.asset.penalize_contacts_on:
-            penalized.extend([s for s in body_names if name in s])
-        termination = []
-        for name in self.cfg.asset.terminate_after_contacts_on:
-            termination.extend([s for s in body_names if name in s])
-        self.feet_indices = torch.tensor([body_names.index(n) for n in feet_names], dtype=torch.long, device=self.device)
-        self.penalised_contact_indices = torch.tensor([body_names.index(n) for n in penalized], dtype=torch.long,
-                                                      device=self.device)
-        self.termination_contact_indices = torch.tensor([body_names.index(n) for n in termination], dtype=torch.long,
-                                                        device=self.device)
-        model.reorder_points({body_names.index(n) for n in feet_names})
+        model_feet = {model.body_names.index(n) for n in model.body_names if self.cfg.asset.foot_name in n}
+        model.reorder_points(model_feet)
         self.model = model
-
-        init = self.cfg.init_state
-        self.base_init_state = to_torch(init.pos + init.rot + init.lin_vel + init.ang_vel, device=self.device)
+        spec = derive_env_spec(self.cfg, model, self.sim_params.dt, self.obs_layout, self.hip_dof_indices)
+        self.spec = spec
+        dev = self.device
+        self.num_dof = spec.num_dof
+        self.num_bodies = spec.num_bodies
+        self.dof_names = spec.dof_names
+        self.num_dofs = len(self.dof_names)
+        self.body_names = spec.body_names
+        self.feet_indices = torch.tensor(spec.feet_indices, dtype=torch.long, device=dev)
+        self.penalised_contact_indices = torch.tensor(spec.penalised_contact_indices, dtype=torch.long, device=dev)
+        self.termination_contact_indices = torch.tensor(spec.termination_contact_indices, dtype=torch.long, device=dev)
+        self.base_init_state = torch.tensor(spec.base_init_state, device=dev)
         self._get_env_origins()
-
-        # DOF props (_process_dof_props, :456-469)
-        lo, hi = model.dof_lower.astype(np.float64), model.dof_upper.astype(np.float64)
-        self.dof_pos_limits = torch.zeros(self.num_dof, 2, dtype=torch.float, device=self.device)
-        m = (lo + hi) / 2
-        r = hi - lo
-        self.dof_pos_limits[:, 0] = torch.tensor(m - 0.5 * r * self.cfg.rewards.soft_dof_pos_limit)
-        self.dof_pos_limits[:, 1] = torch.tensor(m + 0.5 * r * self.cfg.rewards.soft_dof_pos_limit)
-        self.dof_vel_limits = torch.tensor(model.dof_velocity, dtype=torch.float, device=self.device)
-        self.torque_limits = torch.tensor(model.dof_effort, dtype=torch.float, device=self.device)
+        self.dof_pos_limits = torch.tensor(spec.dof_pos_limits, device=dev)
+        self.dof_vel_limits = torch.tensor(spec.dof_vel_limits, device=dev)
+        self.torque_limits = torch.tensor(spec.torque_limits, device=dev)
 
         # shape friction buckets (_process_rigid_shape_props, :429-439): torch CPU RNG as the reference
         friction = np.full(self.num_envs, self.cfg.terrain.static_friction, dtype=np.float32)
@@ -207,21 +193,9 @@ class LeggedRobot(BaseTask):
         self.noise_scale_vec = self._get_noise_scale_vec(self.cfg)
 
         # default joint angles and PD gains by name substring, last match wins (:168-186)
-        self.default_dof_pos = torch.zeros(self.num_dof, dtype=torch.float, device=dev)
-        for i, name in enumerate(self.dof_names):
-            self.default_dof_pos[i] = self.cfg.init_state.default_joint_angles[name]
-            found = False
-            for key in self.cfg.control.stiffness.keys():
-                if key in name:
-                    self.p_gains[i] = self.cfg.control.stiffness[key]
-                    self.d_gains[i] = self.cfg.control.damping[key]
-                    found = True
-            if not found:
-                self.p_gains[i] = 0.0
-                self.d_gains[i] = 0.0
-                if self.cfg.control.control_type in ["P", "V"]:
-                    print(f"PD gain of joint {name} were not defined, setting them to zero")
-        self.default_dof_pos = self.default_dof_pos.unsqueeze(0)
+        self.default_dof_pos = torch.tensor(self.spec.default_dof_pos, device=dev)
+        self.p_gains[:] = torch.tensor(self.spec.p_gains, device=dev)
+        self.d_gains[:] = torch.tensor(self.spec.d_gains, device=dev)
         self.dof_pos[:] = self.default_dof_pos
 
     @property
@@ -235,34 +209,19 @@ class LeggedRobot(BaseTask):
         self._episode_length.copy_(value.to(device=self.device, dtype=torch.long))
 
     def _get_noise_scale_vec(self, cfg):
-        """Quadruped layout (legged_robot.py:188-219)."""
-        noise_vec = torch.zeros_like(self.obs_buf[0])
+        """legged_robot.py:188-219 (quadruped) / h1_env.py:10-31 (humanoid layout)."""
         self.add_noise = self.cfg.noise.add_noise
-        ns = self.cfg.noise.noise_scales
-        lvl = self.cfg.noise.noise_level
-        A = self.num_actions
-        noise_vec[:3] = ns.lin_vel * lvl * self.obs_scales.lin_vel
-        noise_vec[3:6] = ns.ang_vel * lvl * self.obs_scales.ang_vel
-        noise_vec[6:9] = ns.gravity * lvl
-        noise_vec[9:12] = 0.0
-        noise_vec[12:12 + A] = ns.dof_pos * lvl * self.obs_scales.dof_pos
-        noise_vec[12 + A:12 + 2 * A] = ns.dof_vel * lvl * self.obs_scales.dof_vel
-        noise_vec[12 + 2 * A:12 + 3 * A] = 0.0
-        return noise_vec
+        return torch.tensor(self.spec.noise_scale_vec, device=self.device)
 
     def _prepare_reward_function(self):
         """Drop zero scales, multiply the rest by dt; dict order = alphabetical (:817-840)."""
-        for key in list(self.reward_scales.keys()):
-            if self.reward_scales[key] == 0:
-                self.reward_scales.pop(key)
-            else:
-                self.reward_scales[key] *= self.dt
-        self.reward_names = [n for n in self.reward_scales if n != "termination"]
+        self.reward_scales = dict(self.spec.reward_scales)
+        self.reward_names = list(self.spec.reward_names)
         for n in self.reward_names:
             rid = cabi.REWARD_ALIASES.get(n, n)
             if rid not in cabi.REWARD_ID:
                 raise AttributeError(f"'{type(self).__name__}' has no native reward term '_reward_{n}'")
-        self._sum_names = list(self.reward_names) + (["termination"] if "termination" in self.reward_scales else [])
+        self._sum_names = list(self.spec.sum_names)
         nsum = len(self._sum_names)
         self._episode_sums = torch.zeros(nsum, self.num_envs, dtype=torch.float, device=self.device)
         self.episode_sums = {name: self._episode_sums[i] for i, name in enumerate(self._sum_names)}
