@@ -1,0 +1,214 @@
+"""Benchmark: env-steps/s + PPO-iteration wall time, Go2, 4096 envs per GPU.
+
+A bench "step" is one rsl_rl PPO iteration (BASELINE.json metric): 24 control
+steps of the 4096-env Go2 task (policy inference + the fused HIP env step) and
+the PPO update (5 epochs x 4 mini-batches), exactly what OnPolicyRunner.learn
+does per iteration.  value = env-steps/s over the whole job
+(= n_gpus * 4096 * 24 * K / max-over-ranks wall time); ms_per_step = the
+PPO-iteration wall time.
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; envs are
+sharded (4096 per rank, weak scaling) and PPO all-reduces one flat gradient
+bucket per optimizer step over RCCL.
+
+Extra fields: env-only and rollout throughput, the live-timed fused env-step
+kernel against the HBM roofline (algorithmic bytes), and the CPU
+oracle baseline (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "unitree-rl-gym_amd"))
+
+NUM_ENVS = 4096
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# algorithmic bytes per Go2 env-step (state read+write, obs, rewards, ...)
+GO2_BYTES_PER_ENV_STEP = 1154
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10, help="timed PPO iterations")
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--num_envs", type=int, default=NUM_ENVS)
+    p.add_argument("--env_steps", type=int, default=200, help="timed control steps of the env-only leg")
+    p.add_argument("--cpu_seconds", type=float, default=12.0, help="budget of the CPU oracle baseline")
+    p.add_argument("--no_cpu_baseline", action="store_true")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return world, rank, local
+
+
+def barrier(world):
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch of the env-step kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_k_step.json, written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(env, seconds):
+    """The CPU oracle (oracle/lgs_oracle.c, OpenMP over envs) on the same Go2 workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bridge
+    lib = bridge.ensure_built()
+    snap = bridge.snapshot(env)
+    n_envs = env.num_envs
+    rng = np.random.default_rng(0)
+    acts = [rng.normal(0, 0.5, (n_envs, env.num_actions)).astype(np.float32) for _ in range(4)]
+    b = {k: (None if v is None else v.copy()) for k, v in snap.items()}
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    steps, t0 = 0, time.time()
+    while True:
+        b["actions"][:] = acts[steps % 4]
+        b["episode_acc"][:] = 0
+        bridge.step_raw(env.model, env._lgs_params, env.task_params, n_envs, b, 10_000 + steps, lib)
+        steps += 1
+        el = time.time() - t0
+        if el >= seconds and steps >= 2:
+            break
+    return {"value": n_envs * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"Go2 {n_envs} envs x {steps} fused control steps (PD + 4 physics substeps + post-physics), "
+                      f"oracle/lgs_oracle.c with OpenMP over envs, no policy; {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    world, rank, local = setup_dist(args)
+    import isaacgym  # noqa: F401
+    from legged_gym.envs import task_registry  # noqa: F401
+    from legged_gym.utils import get_args
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+
+    dev = f"cuda:{local}"
+    gargs = get_args(["--task", "go2", "--num_envs", str(args.num_envs), "--headless", "--sim_device", dev,
+                      "--rl_device", dev])
+    env, env_cfg = task_registry.make_env(name="go2", args=gargs)
+    _, train_cfg = task_registry.get_cfgs("go2")
+    runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device=dev)
+    T = runner.num_steps_per_env
+    N = env.num_envs
+
+    # ---- env-only leg: the fused step kernel, timed with HIP events on its stream
+    g = torch.Generator(device=dev).manual_seed(rank)
+    acts = [0.5 * torch.randn(N, env.num_actions, device=dev, generator=g) for _ in range(8)]
+    for i in range(20):
+        env.step(acts[i % 8])
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.env_steps)]
+    torch.cuda.synchronize(dev)
+    t0 = time.time()
+    for i in range(args.env_steps):
+        env._sync_stream()
+        env._buf_idx ^= 1
+        env.actions.copy_(acts[i % 8])
+        ev[i][0].record(stream)
+        env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
+        ev[i][1].record(stream)
+        env.common_step_counter += 1
+    torch.cuda.synchronize(dev)
+    env_wall = time.time() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.env_steps
+    env_only = N * args.env_steps / env_wall
+
+    # ---- rollout leg: policy inference + env.step (no update)
+    with torch.inference_mode():
+        obs = env.get_observations()
+        for _ in range(10):
+            obs, _, _, _, _ = env.step(runner.alg.actor_critic.act(obs))
+        torch.cuda.synchronize(dev)
+        t0 = time.time()
+        for _ in range(2 * T):
+            obs, _, _, _, _ = env.step(runner.alg.actor_critic.act(obs))
+        torch.cuda.synchronize(dev)
+    rollout = N * 2 * T / (time.time() - t0)
+
+    # ---- full PPO iterations (the metric)
+    runner.learn(num_learning_iterations=args.warmup, init_at_random_ep_len=True)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    t0 = time.time()
+    runner.learn(num_learning_iterations=args.steps)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    elapsed = max_over_ranks(time.time() - t0, world)
+    ms_per_iter = elapsed / args.steps * 1e3
+    value = world * N * T * args.steps / elapsed
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    bytes_per_launch = GO2_BYTES_PER_ENV_STEP * N
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    line = {
+        "metric": "env-steps/sec + PPO-iter wall-time, Go2 4096 envs/GPU at 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_iter, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 env step; bf16-autocast policy GEMMs",
+        "data": "synthetic (random-init policy, simulated Go2 on flat ground)",
+        "config": {"workload": "Go2 flat terrain, 4096 envs/GPU, MLP actor-critic 512-256-128, PPO 24 steps x 5 epochs x 4 mini-batches",
+                   "num_envs_per_gpu": N, "decimation": env_cfg.control.decimation,
+                   "parallelism": f"dp{world}"},
+        "ppo_iter_ms": round(ms_per_iter, 3),
+        "env_only_env_steps_per_s": round(env_only, 1),
+        "rollout_env_steps_per_s": round(rollout, 1),
+        "env_step_kernel_ms": round(kernel_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc_traffic(),
+                     "kernel": "k_step<12,19,32> (fused Go2 control step)",
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(env, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
