@@ -925,3 +925,14 @@ void orc_compute_torques(const lgs_task_params* T, int N, int D, const float* ac
                          const float* last_qd, float sim_dt, float* tau) {
     for (int e = 0; e < N; ++e) compute_torques(T, D, act + D * e, dofs + 2 * D * e, last_qd + D * e, sim_dt, tau + D * e);
 }
+
+/* ABI self-description for the ctypes mirror test */
+long orc_sizeof(int which) {
+    switch (which) {
+    case 0: return (long)sizeof(lgs_model_desc);
+    case 1: return (long)sizeof(lgs_sim_params);
+    case 2: return (long)sizeof(lgs_task_params);
+    case 3: return (long)sizeof(lgs_env_buffers);
+    default: return -1;
+    }
+}

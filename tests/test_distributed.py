@@ -1,0 +1,72 @@
+"""Data-parallel PPO over torch.distributed (gloo here; RCCL on the GPU box):
+one flat-bucket gradient all-reduce per optimizer step gives every rank the
+mean gradient and identical parameters."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(here, "..", "unitree-rl-gym_amd"), here]
+    from fake_env import FakeEnv
+    from rsl_rl.algorithms import PPO
+    from rsl_rl.modules import ActorCritic
+    torch.manual_seed(100 + rank)  # different init: PPO must broadcast rank 0's
+    ac = ActorCritic(6, 6, 3, [16], [16])
+    ppo = PPO(ac, num_learning_epochs=1, num_mini_batches=1)
+    # gradient all-reduce == mean of per-rank gradients
+    x = torch.randn(5, 6, generator=torch.Generator().manual_seed(rank))
+    ac.zero_grad()
+    ac.actor(x).pow(2).sum().backward()
+    local = torch.cat([p.grad.reshape(-1) for p in ac.parameters() if p.grad is not None]).clone()
+    gathered = [torch.zeros_like(local) for _ in range(world)]
+    dist.all_gather(gathered, local)
+    ppo._allreduce_grads()
+    reduced = torch.cat([p.grad.reshape(-1) for p in ac.parameters() if p.grad is not None])
+    ok_mean = torch.allclose(reduced, torch.stack(gathered).mean(0), atol=1e-6)
+    # a full PPO update keeps the ranks identical
+    env = FakeEnv(num_envs=8)
+    env.g.manual_seed(rank)
+    ppo.init_storage(8, 6, [6], [None], [3])
+    obs, _ = env.reset()
+    for _ in range(6):
+        a = ppo.act(obs, obs)
+        obs, _, r, d, info = env.step(a)
+        ppo.process_env_step(r, d, info)
+    ppo.compute_returns(obs)
+    ppo.update()
+    flat = torch.cat([p.detach().reshape(-1) for p in ac.parameters()])
+    allp = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(allp, flat)
+    same = all(torch.equal(allp[0], t) for t in allp)
+    q.put((rank, ok_mean, same))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gradient_allreduce_and_identical_params():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(same for _, _, same in res), res

@@ -1,0 +1,187 @@
+"""HIP product path vs the CPU oracle, through the C ABI (the env calls lgs_step).
+
+Parity bar: the post-physics outputs (obs, rewards, resets, time-outs,
+commands, episode bookkeeping) within 1e-4 (fp32; SURVEY §7 / north star); the
+physics state within 1e-3.  One control step is compared from identical
+states; a contact that is within fp32 rounding of the 1 cm activation
+threshold can legitimately flip between the two implementations, so up to 1 %
+of envs may exceed the physics tolerance (never the reset/episode logic).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import isaacgym  # noqa: F401,E402
+from legged_gym.envs import task_registry  # noqa: E402
+from legged_gym.utils import get_args  # noqa: E402
+import bridge  # noqa: E402
+
+TASKS = ["go2", "h1", "g1", "h1_2"]
+
+
+def make(task, n, **edits):
+    args = get_args(["--task", task, "--num_envs", str(n), "--headless"])
+    env_cfg, _ = task_registry.get_cfgs(task)
+    import copy
+    cfg = copy.deepcopy(env_cfg)
+    for k, v in edits.items():
+        sec, attr = k.split("__")
+        setattr(getattr(cfg, sec), attr, v)
+    env, _ = task_registry.make_env(name=task, args=args, env_cfg=cfg)
+    return env
+
+
+def compare(env, ref, keys, atol, frac_ok=0.0):
+    n = env.num_envs
+    got = {"root": env.root_states, "dofs": env.dof_state, "cforce": env._contact_forces, "obs": env.obs_buf,
+           "priv_obs": env.privileged_obs_buf, "rew": env.rew_buf, "reset": env.reset_buf,
+           "time_out": env.time_out_buf, "commands": env.commands, "episode_length": env._episode_length,
+           "feet_air_time": env.feet_air_time, "last_contacts": env.last_contacts, "torques": env.torques,
+           "episode_sums": env._episode_sums.T, "rbs": env.rigid_body_states}
+    for k in keys:
+        g = got[k].detach().cpu().numpy()
+        r = ref[k]
+        if k == "episode_sums":
+            r = r.T
+        if g.dtype == np.bool_:
+            g = g.astype(np.uint8)
+        bad = ~np.isclose(g.astype(np.float64), r.astype(np.float64), rtol=atol, atol=atol)
+        frac = bad.reshape(n, -1).any(axis=1).mean()
+        assert np.isfinite(g).all(), k
+        assert frac <= frac_ok, f"{k}: {frac:.2%} of envs outside {atol} (max |d| {np.abs(g - r).max():.3e})"
+
+
+@pytest.mark.parametrize("task", TASKS)
+def test_fused_step_matches_oracle(task):
+    env = make(task, 512)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(30):
+        env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
+    for _ in range(3):
+        snap = bridge.snapshot(env)
+        a = 0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g)
+        ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
+        env.step(a)
+        torch.cuda.synchronize()
+        compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
+        compare(env, ref, ["obs", "rew", "commands", "feet_air_time", "last_contacts", "episode_sums"] +
+                (["priv_obs"] if env.num_privileged_obs else []), 1e-4, frac_ok=0.01)
+        compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=0.01)
+
+
+@pytest.mark.parametrize("task", ["go2", "h1"])
+def test_timeouts_reset_push_match_oracle_exactly(task):
+    """Every env times out at once: the reset/push/resample draws (Philox) and the
+    post-reset state must equal the oracle's; semantics of legged_robot.py:723-768."""
+    env = make(task, 256)
+    env.reset()
+    env.step(torch.zeros(env.num_envs, env.num_actions, device="cuda"))
+    env.episode_length_buf = torch.full_like(env.episode_length_buf, int(env.max_episode_length))
+    snap = bridge.snapshot(env)
+    a = torch.zeros(env.num_envs, env.num_actions, device="cuda")
+    ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
+    env.step(a)
+    torch.cuda.synchronize()
+    assert env.reset_buf.all() and env.time_out_buf.all()
+    assert (env.episode_length_buf == 0).all()
+    compare(env, ref, ["reset", "time_out", "episode_length", "commands"], 0.0)
+    compare(env, ref, ["root", "dofs", "episode_sums"], 1e-5)
+    compare(env, ref, ["obs"], 1e-4, frac_ok=0.01)
+    q = env.dof_pos / env.default_dof_pos
+    m = env.default_dof_pos.abs().expand_as(q) > 1e-6
+    assert ((q[m] >= 0.5 - 1e-6) & (q[m] <= 1.5 + 1e-6)).all()
+    assert (env.dof_vel == 0).all()
+    init = env.base_init_state
+    torch.testing.assert_close(env.root_states[:, :3], init[:3] + env.env_origins)
+    assert (env.root_states[:, 9:13].abs() <= 0.5).all()          # reset vel U[-0.5,0.5] (z, ang)
+    v = env.cfg.domain_rand.max_push_vel_xy
+    assert (env.root_states[:, 7:9].abs() <= v).all()              # pushed at ep_len 0
+    ep = env.extras["episode"]
+    assert set(ep) == {"rew_" + k for k in env._sum_names}
+    assert env.extras["time_outs"].all()
+
+
+def test_drop_in_semantics():
+    env = make("go2", 64)
+    obs, priv = env.reset()
+    assert priv is None and obs.shape == (64, 48)
+    assert env.num_obs == 48 and env.num_privileged_obs is None and env.num_actions == 12
+    assert env.max_episode_length == 1000
+    # rsl_rl rebinds episode_length_buf: values reach the kernel's buffer
+    env.episode_length_buf = torch.randint_like(env.episode_length_buf, high=int(env.max_episode_length))
+    lens = env.episode_length_buf.clone()
+    o1, _, r1, d1, x1 = env.step(torch.zeros(64, 12, device="cuda"))
+    assert torch.equal(env.episode_length_buf[~d1], lens[~d1] + 1)
+    kept = o1.clone()
+    o2, _, r2, d2, x2 = env.step(torch.zeros(64, 12, device="cuda"))
+    assert o2.data_ptr() != o1.data_ptr() and torch.equal(o1, kept)  # previous obs not overwritten
+    assert d2.dtype == torch.bool and r2.dtype == torch.float32
+    assert "time_outs" in x2 and "episode" in x2
+    # stale extras when no env resets (legged_robot.py:742-743)
+    env.episode_length_buf = torch.zeros_like(env.episode_length_buf)
+    env.extras["time_outs"][:] = True
+    prev = env.extras["time_outs"]
+    _, _, _, d3, x3 = env.step(torch.zeros(64, 12, device="cuda"))
+    if not d3.any():
+        assert torch.equal(x3["time_outs"], prev)
+
+
+def test_gymapi_style_substep_matches_oracle():
+    """lgs_simulate (one substep with caller torques) == orc_simulate."""
+    import ctypes as C
+    from leggedsim import cabi
+    env = make("go2", 128)
+    env.reset()
+    for _ in range(10):
+        env.step(0.3 * torch.randn(128, 12, device="cuda"))
+    tau = (5.0 * torch.randn(128, 12, device="cuda")).contiguous()
+    snap = bridge.snapshot(env)
+    env.sim.simulate(tau)
+    torch.cuda.synchronize()
+    lib = bridge.ensure_built()
+    mh = cabi.ModelHandle(env.model)
+    root, dofs = snap["root"].copy(), snap["dofs"].copy()
+    cf, rbs = snap["cforce"].copy(), snap["rbs"].copy()
+    t = tau.cpu().numpy()
+    p = lambda a: a.ctypes.data  # noqa: E731
+    lib.orc_simulate(C.byref(mh.desc), C.byref(env._lgs_params), 128, p(root), p(dofs), p(t), p(cf), p(rbs),
+                     p(snap["added_mass"]), p(snap["friction"]))
+    np.testing.assert_allclose(env.root_states.cpu().numpy(), root, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(env.dof_state.cpu().numpy(), dofs, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("task", TASKS)
+def test_long_rollout_stays_finite(task):
+    env = make(task, 256)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(300):
+        env.step(torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
+    torch.cuda.synchronize()
+    for t in (env.root_states, env.dof_state, env.obs_buf, env.rew_buf):
+        assert torch.isfinite(t).all()
+
+
+def test_ppo_training_smoke():
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    env = make("go2", 512)
+    _, train_cfg = task_registry.get_cfgs("go2")
+    runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device="cuda:0")
+    runner.learn(2, init_at_random_ep_len=True)
+    for p in runner.alg.actor_critic.parameters():
+        assert torch.isfinite(p).all()
+
+
+def test_recurrent_humanoid_training_smoke():
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    env = make("h1", 256)
+    _, train_cfg = task_registry.get_cfgs("h1")
+    runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device="cuda:0")
+    runner.learn(1, init_at_random_ep_len=True)
+    for p in runner.alg.actor_critic.parameters():
+        assert torch.isfinite(p).all()

@@ -1,0 +1,160 @@
+"""rsl_rl v1.0.2 API semantics on CPU (the library is absent from the reference
+tree, so PPO parity is unpinned; these pin the restated algorithm instead)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from fake_env import FakeEnv
+from rsl_rl.algorithms import PPO
+from rsl_rl.modules import ActorCritic, ActorCriticRecurrent
+from rsl_rl.runners import OnPolicyRunner
+from rsl_rl.storage import RolloutStorage
+from rsl_rl.utils import split_and_pad_trajectories, unpad_trajectories
+
+
+def test_actor_critic_shapes_and_distribution():
+    ac = ActorCritic(48, 48, 12, [512, 256, 128], [512, 256, 128], init_noise_std=1.0)
+    obs = torch.randn(32, 48)
+    a = ac.act(obs)
+    assert a.shape == (32, 12)
+    lp = ac.get_actions_log_prob(a)
+    ref = torch.distributions.Normal(ac.actor(obs), ac.std).log_prob(a).sum(-1)
+    torch.testing.assert_close(lp, ref)
+    assert ac.evaluate(obs).shape == (32, 1)
+    assert torch.allclose(ac.action_std, torch.ones(32, 12))
+    n_params = sum(p.numel() for p in ac.parameters())
+    assert n_params == 380313  # Go2 MLP bucket = 1.52 MB fp32
+
+
+def test_gae_matches_naive_recursion():
+    T, N, g, lam = 6, 5, 0.99, 0.95
+    st = RolloutStorage(N, T, [3], [None], [2])
+    rng = np.random.default_rng(0)
+    rew = rng.normal(size=(T, N, 1)).astype(np.float32)
+    val = rng.normal(size=(T, N, 1)).astype(np.float32)
+    done = (rng.uniform(size=(T, N, 1)) < 0.2)
+    st.rewards[:] = torch.from_numpy(rew)
+    st.values[:] = torch.from_numpy(val)
+    st.dones[:] = torch.from_numpy(done.astype(np.uint8))
+    last = rng.normal(size=(N, 1)).astype(np.float32)
+    st.compute_returns(torch.from_numpy(last), g, lam)
+    ret = np.zeros_like(rew)
+    adv = np.zeros((N, 1), np.float32)
+    for t in reversed(range(T)):
+        nv = last if t == T - 1 else val[t + 1]
+        nt = 1.0 - done[t].astype(np.float32)
+        delta = rew[t] + nt * g * nv - val[t]
+        adv = delta + nt * g * lam * adv
+        ret[t] = adv + val[t]
+    np.testing.assert_allclose(st.returns.numpy(), ret, rtol=1e-5, atol=1e-5)
+    a = ret - val
+    np.testing.assert_allclose(st.advantages.numpy(), (a - a.mean()) / (a.std(ddof=1) + 1e-8), rtol=1e-4, atol=1e-4)
+
+
+def test_split_and_pad_roundtrip():
+    T, N = 5, 3
+    x = torch.arange(T * N * 2, dtype=torch.float).view(T, N, 2)
+    dones = torch.zeros(T, N, 1, dtype=torch.uint8)
+    dones[1, 0] = 1
+    dones[3, 2] = 1
+    padded, masks = split_and_pad_trajectories(x, dones)
+    assert padded.shape[0] == T and masks.shape == (T, padded.shape[1])
+    assert padded.shape[1] == 5  # env0: 2 trajs, env1: 1, env2: 2
+    back = unpad_trajectories(padded, masks)
+    torch.testing.assert_close(back, x)
+
+
+def test_ppo_update_changes_params_and_adapts_lr():
+    torch.manual_seed(0)
+    env = FakeEnv(num_envs=32)
+    ac = ActorCritic(env.num_obs, env.num_obs, env.num_actions, [32], [32])
+    ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3, schedule="adaptive", desired_kl=0.01)
+    ppo.init_storage(env.num_envs, 8, [env.num_obs], [None], [env.num_actions])
+    obs, _ = env.reset()
+    before = [p.detach().clone() for p in ac.parameters()]
+    for _ in range(8):
+        a = ppo.act(obs, obs)
+        obs, _, r, d, info = env.step(a)
+        ppo.process_env_step(r, d, info)
+    ppo.compute_returns(obs)
+    vl, sl = ppo.update()
+    assert np.isfinite(vl) and np.isfinite(sl)
+    assert any(not torch.equal(b, p) for b, p in zip(before, ac.parameters()))
+    assert ppo.learning_rate != 1e-3  # KL-adaptive schedule moved it
+    assert 1e-5 <= ppo.learning_rate <= 1e-2
+
+
+def test_time_out_bootstrap_adds_gamma_value():
+    env = FakeEnv(num_envs=4)
+    ac = ActorCritic(env.num_obs, env.num_obs, env.num_actions, [8], [8])
+    ppo = PPO(ac, gamma=0.9)
+    ppo.init_storage(4, 2, [env.num_obs], [None], [env.num_actions])
+    obs, _ = env.reset()
+    ppo.act(obs, obs)
+    v = ppo.transition.values.clone()
+    r = torch.ones(4)
+    to = torch.tensor([True, False, True, False])
+    ppo.process_env_step(r, to, {"time_outs": to})
+    torch.testing.assert_close(ppo.storage.rewards[0, :, 0], r + 0.9 * v[:, 0] * to)
+
+
+def test_runner_learn_save_load(tmp_path):
+    env = FakeEnv(num_envs=16, num_privileged_obs=9)
+    cfg = {"runner": {"policy_class_name": "ActorCritic", "algorithm_class_name": "PPO", "num_steps_per_env": 8,
+                      "save_interval": 1},
+           "algorithm": {"num_learning_epochs": 1, "num_mini_batches": 2, "learning_rate": 1e-3},
+           "policy": {"actor_hidden_dims": [16], "critic_hidden_dims": [16], "activation": "elu", "init_noise_std": 1.0}}
+    runner = OnPolicyRunner(env, cfg, log_dir=str(tmp_path), device="cpu")
+    runner.learn(2, init_at_random_ep_len=True)
+    assert (tmp_path / "model_0.pt").exists() and (tmp_path / "model_2.pt").exists()
+    ck = torch.load(tmp_path / "model_2.pt", weights_only=True)
+    assert set(ck) == {"model_state_dict", "optimizer_state_dict", "iter", "infos"} and ck["iter"] == 2
+    r2 = OnPolicyRunner(env, cfg, log_dir=None, device="cpu")
+    r2.load(str(tmp_path / "model_2.pt"))
+    assert r2.current_learning_iteration == 2
+    pol = r2.get_inference_policy()
+    assert pol(env.get_observations()).shape == (16, env.num_actions)
+
+
+def test_recurrent_runner_learns(tmp_path):
+    env = FakeEnv(num_envs=8, num_privileged_obs=9, ep_len=5)
+    cfg = {"runner": {"policy_class_name": "ActorCriticRecurrent", "algorithm_class_name": "PPO",
+                      "num_steps_per_env": 12, "save_interval": 50},
+           "algorithm": {"num_learning_epochs": 2, "num_mini_batches": 2},
+           "policy": {"actor_hidden_dims": [16], "critic_hidden_dims": [16], "activation": "elu",
+                      "rnn_type": "lstm", "rnn_hidden_size": 8, "rnn_num_layers": 1, "init_noise_std": 0.8}}
+    runner = OnPolicyRunner(env, cfg, log_dir=None, device="cpu")
+    runner.learn(2)
+    assert runner.alg.actor_critic.is_recurrent
+
+
+@pytest.mark.parametrize("robot", ["g1", "h1", "h1_2"])
+def test_lstm_export_matches_pretrained_policy(robot, tmp_path):
+    """Golden: deploy/pre_train/<robot>/motion.pt (the reference's own exported
+    PolicyExporterLSTM).  Our ActorCriticRecurrent + PolicyExporterLSTM with the
+    same weights must reproduce its outputs and its reset_memory semantics."""
+    from legged_gym.utils.helpers import export_policy_as_jit
+    g = np.load(os.path.join(GOLDEN, f"lstm_policy_{robot}.npz"))
+    n_in = g["w.memory.weight_ih_l0"].shape[1]
+    n_act = g["w.actor.2.weight"].shape[0]
+    ac = ActorCriticRecurrent(n_in, n_in + 3, n_act, actor_hidden_dims=[32], critic_hidden_dims=[32],
+                              rnn_type="lstm", rnn_hidden_size=64, rnn_num_layers=1, init_noise_std=0.8)
+    sd = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w.")}
+    ac.actor.load_state_dict({k[len("actor."):]: v for k, v in sd.items() if k.startswith("actor.")})
+    ac.memory_a.rnn.load_state_dict({k[len("memory."):]: v for k, v in sd.items() if k.startswith("memory.")})
+    export_policy_as_jit(ac, str(tmp_path))
+    m = torch.jit.load(str(tmp_path / "policy_lstm_1.pt"))
+    m.reset_memory()
+    ys = np.stack([m(torch.from_numpy(x[None])).detach().numpy()[0] for x in g["inputs"]])
+    np.testing.assert_allclose(ys, g["outputs"], rtol=1e-5, atol=1e-5)
+    m.reset_memory()
+    ys2 = np.stack([m(torch.from_numpy(x[None])).detach().numpy()[0] for x in g["inputs"][:5]])
+    np.testing.assert_allclose(ys2, g["outputs_after_reset"], rtol=1e-5, atol=1e-5)
+    # the training-time module computes the same recurrent forward
+    ac.eval()
+    ac.memory_a.hidden_states = None
+    ys3 = np.stack([ac.act_inference(torch.from_numpy(x[None])).detach().numpy()[0] for x in g["inputs"]])
+    np.testing.assert_allclose(ys3, g["outputs"], rtol=1e-5, atol=1e-5)
