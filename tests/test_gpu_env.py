@@ -87,7 +87,8 @@ def test_timeouts_reset_push_match_oracle_exactly(task):
     torch.cuda.synchronize()
     assert env.reset_buf.all() and env.time_out_buf.all()
     assert (env.episode_length_buf == 0).all()
-    compare(env, ref, ["reset", "time_out", "episode_length", "commands"], 0.0)
+    compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
+    compare(env, ref, ["commands"], 1e-6)  # FMA contraction of (hi-lo)*u+lo on the GPU
     compare(env, ref, ["root", "dofs", "episode_sums"], 1e-5)
     compare(env, ref, ["obs"], 1e-4, frac_ok=0.01)
     q = env.dof_pos / env.default_dof_pos

@@ -1182,20 +1182,25 @@ struct lgs_sim {
     int rows = 32;
 };
 
-enum Variant { V_12_19, V_12_13, V_10_11, V_NONE };
+// Compiled (dofs, max bodies, constraint-row capacity) variants.  The row
+// capacity sets the LDS footprint (Y, A): the 32-row variant is the Go2 one.
+enum Variant { V_12_19, V_12_13, V_10_11, V_12_19_48, V_NONE };
 
 static Variant pick(const lgs_sim* s) {
-    if (s->D == 12 && s->B <= 19) return V_12_19;
+    if (s->D == 12 && s->B <= 19 && s->rows <= 32) return V_12_19;
     if (s->D == 12 && s->B <= 13) return V_12_13;
+    if (s->D == 12 && s->B <= 19) return V_12_19_48;
     if (s->D == 10 && s->B <= 11) return V_10_11;
     return V_NONE;
 }
+static int variant_rows(Variant v) { return v == V_12_19 ? 32 : 48; }
 
 #define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
     switch (pick(sim)) {                                                                                  \
     case V_12_19: hipLaunchKernelGGL((KERNEL<12, 19, 32>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
     case V_12_13: hipLaunchKernelGGL((KERNEL<12, 13, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
     case V_10_11: hipLaunchKernelGGL((KERNEL<10, 11, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
+    case V_12_19_48: hipLaunchKernelGGL((KERNEL<12, 19, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
     default: return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");                                 \
     }
 
@@ -1225,12 +1230,13 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     HIP_TRY(hipSetDevice(device_id));
     lgs_sim* s = new lgs_sim();
     s->N = num_envs; s->B = m->num_bodies; s->D = m->num_dofs; s->P = m->num_points; s->device = device_id;
+    s->rows = p->max_rows;
     if (pick(s) == V_NONE) {
         delete s;
         return set_err(LGS_ERR_ARG, "lgs_create_sim: no kernel instantiation for this (dofs, bodies)");
     }
     {
-        const int cap = pick(s) == V_12_19 ? 32 : 48;
+        const int cap = variant_rows(pick(s));
         if (p->max_rows > cap || p->max_rows < 3 * p->max_contacts || p->max_contacts < 0) {
             delete s;
             return set_err(LGS_ERR_ARG, "lgs_create_sim: need 3*max_contacts <= max_rows <= " + std::to_string(cap));
