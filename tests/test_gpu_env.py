@@ -186,3 +186,47 @@ def test_recurrent_humanoid_training_smoke():
     runner.learn(1, init_at_random_ep_len=True)
     for p in runner.alg.actor_critic.parameters():
         assert torch.isfinite(p).all()
+
+
+def test_ppo_update_graph_matches_eager():
+    """The whole-update HIP graph performs the same optimizer steps as the eager loop."""
+    import copy
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    env = make("go2", 256)
+    _, train_cfg = task_registry.get_cfgs("go2")
+    runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device="cuda:0")
+    runner.learn(2)  # eager warm-up update, then the captured graph
+    alg = runner.alg
+    assert alg.use_graph and alg._graph is not None
+    # identical storage + params + optimizer state, one update each way
+    runner.learn(1)
+    with torch.inference_mode():
+        obs = env.get_observations()
+        for _ in range(alg.storage.num_transitions_per_env):
+            a = alg.act(obs, obs)
+            obs, _, r, d, info = env.step(a)
+            alg.process_env_step(r, d, info)
+        alg.compute_returns(obs)
+    saved = {k: v.clone() for k, v in alg.storage.__dict__.items() if torch.is_tensor(v)}
+    p0 = copy.deepcopy(alg.actor_critic.state_dict())
+    o0 = copy.deepcopy(alg.optimizer.state_dict())
+    lr0 = alg._lr.clone()
+    torch.manual_seed(5)
+    perm_seed_state = torch.cuda.get_rng_state()
+    alg.update()  # graphed
+    p_graph = {k: v.clone() for k, v in alg.actor_critic.state_dict().items()}
+    # rewind and run the eager loop with the same permutation
+    alg.actor_critic.load_state_dict(p0)
+    alg.optimizer.load_state_dict(o0)
+    alg._lr.copy_(lr0)
+    for k, v in saved.items():
+        getattr(alg.storage, k).copy_(v)
+    alg.storage.step = alg.storage.num_transitions_per_env
+    torch.cuda.set_rng_state(perm_seed_state)
+    use = alg.use_graph
+    alg.use_graph = False
+    alg.update()
+    alg.use_graph = use
+    for k, v in alg.actor_critic.state_dict().items():
+        torch.testing.assert_close(v, p_graph[k], rtol=2e-3, atol=2e-4)

@@ -41,10 +41,15 @@ class PPO:
         self._lr = torch.tensor(float(learning_rate), device=self.device)
         params = list(self.actor_critic.parameters())
         on_gpu = str(self.device).startswith("cuda")
-        try:
-            self.optimizer = optim.Adam(params, lr=self._lr if on_gpu else float(learning_rate),
-                                        fused=True if on_gpu else None)
-        except (RuntimeError, TypeError, ValueError):
+        self.optimizer = None
+        if on_gpu:
+            for kw in (dict(fused=True, capturable=True), dict(foreach=True, capturable=True)):
+                try:
+                    self.optimizer = optim.Adam(params, lr=self._lr, **kw)
+                    break
+                except (RuntimeError, TypeError, ValueError):
+                    continue
+        if self.optimizer is None:
             self.optimizer = optim.Adam(params, lr=float(learning_rate))
         self._lr_is_tensor = torch.is_tensor(self.optimizer.param_groups[0]["lr"])
         self.transition = RolloutStorage.Transition()
@@ -58,6 +63,12 @@ class PPO:
         self.max_grad_norm = max_grad_norm
         self.use_clipped_value_loss = use_clipped_value_loss
         self.world_size = _dist_world()
+        # whole-update HIP graph (MLP policies on a GPU): set use_graph=False to disable
+        self.use_graph = on_gpu and not getattr(self.actor_critic, "is_recurrent", False) and \
+            self.optimizer.defaults.get("capturable", False) and \
+            (self.world_size == 1 or dist.get_backend() == "nccl")
+        self._graph = None
+        self._graph_calls = 0
         if self.world_size > 1:
             for p in params:  # identical initial policy on every rank
                 dist.broadcast(p.data, src=0)
@@ -130,67 +141,116 @@ class PPO:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
-    def update(self):
-        dev = self.device
-        sum_value_loss = torch.zeros((), device=dev)
-        sum_surrogate_loss = torch.zeros((), device=dev)
-        if self.actor_critic.is_recurrent:
-            generator = self.storage.reccurent_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        else:
-            generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
-             old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
-            self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
-            actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
-            value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch,
-                                                     hidden_states=hid_states_batch[1])
-            mu_batch = self.actor_critic.action_mean
-            sigma_batch = self.actor_critic.action_std
-            entropy_batch = self.actor_critic.entropy
+    def _minibatch_step(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+                        returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
+                        masks_batch, acc):
+        """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
+        self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+        actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
+        value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
+        mu_batch = self.actor_critic.action_mean
+        sigma_batch = self.actor_critic.action_std
+        entropy_batch = self.actor_critic.entropy
 
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                with torch.inference_mode():
-                    kl = torch.sum(torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
-                                   + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
-                                   / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
-                    kl_mean = torch.mean(kl)
-                    if self.world_size > 1:
-                        dist.all_reduce(kl_mean)
-                        kl_mean /= self.world_size
-                    lr = self._lr
-                    new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
-                                         torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
-                                                     torch.clamp(lr * 1.5, max=1e-2), lr))
+        if self.desired_kl is not None and self.schedule == "adaptive":
+            with torch.no_grad():
+                kl = torch.sum(torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
+                               + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
+                               / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
+                kl_mean = torch.mean(kl)
+                if self.world_size > 1:
+                    dist.all_reduce(kl_mean)
+                    kl_mean = kl_mean / self.world_size
+                lr = self._lr
+                new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
+                                     torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
+                                                 torch.clamp(lr * 1.5, max=1e-2), lr))
                 self._lr.copy_(new_lr)
-                if not self._lr_is_tensor:
-                    for g in self.optimizer.param_groups:
-                        g["lr"] = float(self._lr)
+            if not self._lr_is_tensor:
+                for g in self.optimizer.param_groups:
+                    g["lr"] = float(self._lr)
 
-            ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
-            surrogate = -torch.squeeze(advantages_batch) * ratio
-            surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
-                                                                               1.0 + self.clip_param)
-            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
-            if self.use_clipped_value_loss:
-                value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
-                                                                                                self.clip_param)
-                value_losses = (value_batch - returns_batch).pow(2)
-                value_losses_clipped = (value_clipped - returns_batch).pow(2)
-                value_loss = torch.max(value_losses, value_losses_clipped).mean()
-            else:
-                value_loss = (returns_batch - value_batch).pow(2).mean()
-            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+        ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
+        surrogate = -torch.squeeze(advantages_batch) * ratio
+        surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
+                                                                           1.0 + self.clip_param)
+        surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+        if self.use_clipped_value_loss:
+            value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
+                                                                                            self.clip_param)
+            value_losses = (value_batch - returns_batch).pow(2)
+            value_losses_clipped = (value_clipped - returns_batch).pow(2)
+            value_loss = torch.max(value_losses, value_losses_clipped).mean()
+        else:
+            value_loss = (returns_batch - value_batch).pow(2).mean()
+        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
 
-            self.optimizer.zero_grad()
-            loss.backward()
-            if self.world_size > 1:
-                self._allreduce_grads()
-            nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
-            self.optimizer.step()
-            sum_value_loss += value_loss.detach()
-            sum_surrogate_loss += surrogate_loss.detach()
+        self.optimizer.zero_grad()
+        loss.backward()
+        if self.world_size > 1:
+            self._allreduce_grads()
+        nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
+        self.optimizer.step()
+        with torch.no_grad():
+            acc[0] += value_loss.detach()
+            acc[1] += surrogate_loss.detach()
 
+    def update(self):
         num_updates = self.num_learning_epochs * self.num_mini_batches
-        means = (torch.stack([sum_value_loss, sum_surrogate_loss]) / num_updates).tolist()
+        self._graph_calls += 1
+        if self.use_graph and self._graph_calls >= 2:  # first call runs eagerly (warm-up)
+            acc = self._update_graphed()
+        else:
+            acc = torch.zeros(2, device=self.device)
+            if self.actor_critic.is_recurrent:
+                gen = self.storage.reccurent_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+            else:
+                gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+            for batch in gen:
+                self._minibatch_step(*batch, acc)
+        means = (acc / num_updates).tolist()
         self.storage.clear()
         return means[0], means[1]
+
+    def _update_graphed(self):
+        """All num_epochs x num_mini_batches optimizer steps replayed as ONE HIP graph.
+        The mini-batch permutation is drawn outside the graph each update, exactly as
+        RolloutStorage.mini_batch_generator draws it (one randperm per update)."""
+        st = self.storage
+        batch = st.num_envs * st.num_transitions_per_env
+        mb = batch // self.num_mini_batches
+        if self._graph is None:
+            self._perm = torch.randperm(self.num_mini_batches * mb, device=self.device)
+            self._acc = torch.zeros(2, device=self.device)
+            flat = [st.observations.flatten(0, 1),
+                    st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None
+                    else st.observations.flatten(0, 1),
+                    st.actions.flatten(0, 1), st.values.flatten(0, 1), None, st.returns.flatten(0, 1),
+                    st.actions_log_prob.flatten(0, 1), st.mu.flatten(0, 1), st.sigma.flatten(0, 1)]
+            self._flat = flat
+
+            def body():
+                self._acc.zero_()
+                adv = st.advantages.flatten(0, 1)
+                for _ in range(self.num_learning_epochs):
+                    for i in range(self.num_mini_batches):
+                        idx = self._perm[i * mb:(i + 1) * mb]
+                        tens = [None if t is None else t.index_select(0, idx) for t in flat]
+                        tens[4] = adv.index_select(0, idx)
+                        self._minibatch_step(*tens, (None, None), None, self._acc)
+
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                # advantages are re-bound by compute_returns: keep one static buffer
+                self._adv_static = st.advantages
+                with torch.cuda.graph(self._graph, stream=side):
+                    body()
+            torch.cuda.current_stream(self.device).wait_stream(side)
+        if st.advantages.data_ptr() != self._adv_static.data_ptr():
+            self._adv_static.copy_(st.advantages)
+            st.advantages = self._adv_static
+        self._perm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
+        self._graph.replay()
+        return self._acc

@@ -91,12 +91,13 @@ class RolloutStorage:
             delta = self.rewards[step] + not_terminal * gamma * next_values - self.values[step]
             advantage = delta + not_terminal * gamma * lam * advantage
             self.returns[step] = advantage + self.values[step]
-        self.advantages = self.returns - self.values
+        # in place: a captured update graph reads this buffer
+        torch.sub(self.returns, self.values, out=self.advantages)
         if adv_stats is None:
             mean, std = self.advantages.mean(), self.advantages.std()
         else:
             mean, std = adv_stats(self.advantages)
-        self.advantages = (self.advantages - mean) / (std + 1e-8)
+        self.advantages.sub_(mean).div_(std + 1e-8)
 
     def get_statistics(self):
         done = self.dones
