@@ -69,6 +69,7 @@ class PPO:
             (self.world_size == 1 or dist.get_backend() == "nccl")
         self._graph = None
         self._graph_calls = 0
+        self._capturing = False
         if self.world_size > 1:
             for p in params:  # identical initial policy on every rank
                 dist.broadcast(p.data, src=0)
@@ -145,7 +146,10 @@ class PPO:
                         returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
                         masks_batch, acc):
         """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
-        self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+        if self.actor_critic.is_recurrent:
+            self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+        else:  # v1.0.2 calls act() here and discards the sample; only the distribution is used
+            self.actor_critic.update_distribution(obs_batch)
         actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
         value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
         mu_batch = self.actor_critic.action_mean
@@ -185,7 +189,9 @@ class PPO:
             value_loss = (returns_batch - value_batch).pow(2).mean()
         loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
 
-        self.optimizer.zero_grad()
+        # inside a captured graph the grads are static buffers (set_to_none=False):
+        # no graph-pool tensor may escape the capture
+        self.optimizer.zero_grad(set_to_none=not self._capturing)
         loss.backward()
         if self.world_size > 1:
             self._allreduce_grads()
@@ -239,15 +245,34 @@ class PPO:
                         tens[4] = adv.index_select(0, idx)
                         self._minibatch_step(*tens, (None, None), None, self._acc)
 
-            side = torch.cuda.Stream(self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
+            # static grads (exist after the eager warm-up update) and optimizer state
+            for p_ in self.actor_critic.parameters():
+                if p_.grad is None:
+                    p_.grad = torch.zeros_like(p_)
+            self._side = torch.cuda.Stream(self.device)
+            self._side.wait_stream(torch.cuda.current_stream(self.device))
             self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(side):
-                # advantages are re-bound by compute_returns: keep one static buffer
-                self._adv_static = st.advantages
-                with torch.cuda.graph(self._graph, stream=side):
+            self._adv_static = st.advantages
+            # snapshot: the warm-up pass below really trains, so undo it afterwards
+            snap_p = [p_.detach().clone() for p_ in self.actor_critic.parameters()]
+            snap_o = {id(p_): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.optimizer.state[p_].items()}
+                      for p_ in self.actor_critic.parameters()}
+            snap_lr = self._lr.clone()
+            self._capturing = True
+            with torch.cuda.stream(self._side):
+                body()  # warm-up on the capture stream (allocator + autograd state)
+                with torch.cuda.graph(self._graph, stream=self._side):
                     body()
-            torch.cuda.current_stream(self.device).wait_stream(side)
+            self._capturing = False
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            with torch.no_grad():
+                for p_, v in zip(self.actor_critic.parameters(), snap_p):
+                    p_.copy_(v)
+                for p_ in self.actor_critic.parameters():
+                    for k, v in self.optimizer.state[p_].items():
+                        if torch.is_tensor(v):
+                            v.copy_(snap_o[id(p_)][k])
+                self._lr.copy_(snap_lr)
         if st.advantages.data_ptr() != self._adv_static.data_ptr():
             self._adv_static.copy_(st.advantages)
             st.advantages = self._adv_static

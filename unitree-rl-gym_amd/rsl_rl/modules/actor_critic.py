@@ -45,11 +45,10 @@ class ActorCritic(nn.Module):
         self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
         self.distribution = None
         self.mixed_precision = mixed_precision
-        Normal.set_default_validate_args = False
 
     def _run(self, net, x):
         if self.mixed_precision and x.is_cuda:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
                 y = net(x)
             return y.float()
         return net(x)
@@ -79,7 +78,10 @@ class ActorCritic(nn.Module):
 
     def update_distribution(self, observations):
         mean = self._run(self.actor, observations)
-        self.distribution = Normal(mean, mean * 0.0 + self.std)
+        # validate_args=False: v1.0.2 meant to disable validation (it assigns
+        # Normal.set_default_validate_args = False, which does not); validation
+        # costs a device->host sync per call and breaks graph capture.
+        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=False)
 
     def act(self, observations, **kwargs):
         self.update_distribution(observations)
