@@ -245,6 +245,10 @@ LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step
 /* name/index queries */
 LGS_API int lgs_get_counts(lgs_sim* sim, int32_t* num_envs, int32_t* num_bodies, int32_t* num_dofs);
 
+/* diagnostics: per-phase s_memtime cycle sums [N][24] of the last lgs_step
+ * (only in a library built with -DLGS_PHASE_STAMPS; otherwise LGS_ERR_STATE) */
+LGS_API int lgs_debug_set_phase_buffer(void* dev_ptr);
+
 /* counter-based RNG used by every random draw of the step (Philox4x32-10);
  * exposed so tests and the oracle can reproduce the draws bit-exactly. */
 LGS_API float lgs_uniform(uint64_t seed, uint32_t env, uint32_t step, uint32_t stream, uint32_t index);

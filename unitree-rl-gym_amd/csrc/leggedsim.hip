@@ -26,6 +26,36 @@
 
 #include "../../include/leggedsim.h"
 
+// Diagnostic build only (-DLGS_PHASE_STAMPS): lane 0 accumulates s_memtime
+// deltas per phase into a global [N][LGS_NPHASE] buffer.  Never in the real build.
+#define LGS_NPHASE 24
+#ifdef LGS_PHASE_STAMPS
+__device__ unsigned long long* g_phase_buf;
+#define STAMP(i)                                                                                 \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long _t;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if (threadIdx.x == 0) {                                                                  \
+            if ((i) > 0) s.stamps[(i)] += _t - s.tlast;                                          \
+            s.tlast = _t;                                                                        \
+        }                                                                                        \
+    } while (0)
+#define STAMP_FLUSH(e)                                                                           \
+    do {                                                                                         \
+        if (threadIdx.x < LGS_NPHASE && g_phase_buf)                                             \
+            g_phase_buf[(size_t)(e) * LGS_NPHASE + threadIdx.x] = s.stamps[threadIdx.x];         \
+    } while (0)
+#define STAMP_INIT()                                                                             \
+    do {                                                                                         \
+        if (threadIdx.x < LGS_NPHASE) s.stamps[threadIdx.x] = 0;                                 \
+    } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(e) do {} while (0)
+#define STAMP_INIT() do {} while (0)
+#endif
 #define MAXB LGS_MAX_BODIES
 #define MAXD LGS_MAX_DEPTH
 #define WAVE 64
@@ -206,6 +236,10 @@ struct Smem {
     float obs_tmp[LGS_MAX_OBS];
     float misc[32];
     int flags[8];
+#ifdef LGS_PHASE_STAMPS
+    unsigned long long stamps[LGS_NPHASE];
+    unsigned long long tlast;
+#endif
 };
 
 // -------------------------------------------------------------- substep --
@@ -220,6 +254,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     const int lane = threadIdx.x;
     const float dt = sp.dt;
 
+    STAMP(0);
     // ---- 1. forward kinematics: lane b walks root..b
     if (lane < B) {
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
@@ -255,6 +290,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
     }
     __syncthreads();
+    STAMP(1);
     const float O[3] = {s.p[0][0], s.p[0][1], s.p[0][2]};
     float w0[3] = {s.root[10], s.root[11], s.root[12]};
     float vO[3];
@@ -296,6 +332,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < 3; ++k) { s.u.dyn.Sw[lane][k] = a[k]; s.u.dyn.Sv[lane][k] = sv[k]; }
     }
     __syncthreads();
+    STAMP(2);
     // ---- 3. velocity + bias acceleration down the chain, bias force per body
     if (lane < B) {
         float Vw[3] = {w0[0], w0[1], w0[2]}, Vv[3] = {vO[0], vO[1], vO[2]};
@@ -338,6 +375,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
     }
     __syncthreads();
+    STAMP(3);
     // ---- 4. subtree (composite) sums: lane b adds the contiguous DFS range.
     // Summation order mirrors the oracle's leaf-to-root accumulation.
     if (lane < B) {
@@ -363,6 +401,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int t = 0; t < 6; ++t) s.u.dyn.cI[lane][t] = cI[t];
     }
     __syncthreads();
+    STAMP(4);
     // ---- 5. mass matrix (lower triangle) and rhs = tau - C
     for (int idx = lane; idx < n * (n + 1) / 2; idx += WAVE) {
         int r = (int)((sqrtf(8.f * idx + 1.f) - 1.f) * 0.5f);
@@ -425,6 +464,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         x = s.tau[j] - C;
     }
     __syncthreads();
+    STAMP(5);
     // ---- 6. Cholesky (left-looking, in place, lane per row)
     for (int k = 0; k < n; ++k) {
         if (lane >= k && lane < n) {
@@ -441,6 +481,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
         __syncthreads();
     }
+    STAMP(6);
     // ---- 7. qdd = M^-1 rhs by column sweeps (lane i owns x_i)
     for (int i = 0; i < n; ++i) {
         if (lane == i) x = x / s.M[i][i];
@@ -465,6 +506,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         else if (lane < n) s.qf[lane] = s.qd[lane - 6] + dt * x;
     }
     __syncthreads();
+    STAMP(7);
     // ---- 8. constraint rows.  Joint limits first (DOF order), then contacts.
     const float beta = sp.beta;
     int nlimit;
@@ -524,6 +566,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     const int nrows = nlimit + 3 * nc;
     __syncthreads();
+    STAMP(8);
     // contact rows (lane per row): J row into Y[r]
     if (lane >= nlimit && lane < nrows) {
         const int cc = (lane - nlimit) / 3, dd = (lane - nlimit) % 3;
@@ -556,6 +599,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
     }
     __syncthreads();
+    STAMP(9);
     // ---- 9. v = J qf ; Y = L^-1 J^T (lane r, registers)
     float y[n];
     float v = 0.f, lam = 0.f;
@@ -575,6 +619,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = y[i];
     }
     __syncthreads();
+    STAMP(10);
     // ---- 10. A = Y^T Y (lane r computes row r)
     float diag = 1.f;
     if (lane < nrows) {
@@ -587,6 +632,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
     }
     __syncthreads();
+    STAMP(11);
     // ---- 11. projected Gauss-Seidel
     const float mu = 0.5f * (sp.ground_friction + shape_mu);
     const float tg = (lane < nrows) ? s.tgt[lane] : 0.f;
@@ -616,6 +662,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             }
         }
     }
+    STAMP(12);
     // ---- 12. z = Y^T lambda ; dq = L^-T z ; qd' = qf + dq
     float z = 0.f;
     for (int r = 0; r < nrows; ++r) {
@@ -642,6 +689,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         }
         if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
     }
+    STAMP(13);
     // ---- 13. integrate
     const float qw0 = rl(qn, 0), qw1 = rl(qn, 1), qw2 = rl(qn, 2);
     const float qv0 = rl(qn, 3), qv1 = rl(qn, 4), qv2 = rl(qn, 5);
@@ -673,6 +721,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         rt[7] = qv0 + wc[0]; rt[8] = qv1 + wc[1]; rt[9] = qv2 + wc[2];
     }
     __syncthreads();
+    STAMP(14);
 }
 
 // rigid body states [B][13] of the block's env into global memory
@@ -1116,6 +1165,7 @@ __global__ __launch_bounds__(WAVE) void k_step(DevModel md, DevSim sp, DevState 
     const float lqd = (lane < D) ? E.last_dof_vel[D * e + lane] : 0.f;
     const float am = st.added_mass ? st.added_mass[e] : 0.f;
     const float mu = st.friction ? st.friction[e] : 1.f;
+    STAMP_INIT();
     __syncthreads();
     for (int it = 0; it < T.decimation; ++it) {  // :627-639
         if (lane < D) {  // _compute_torques :649-671
@@ -1130,13 +1180,18 @@ __global__ __launch_bounds__(WAVE) void k_step(DevModel md, DevSim sp, DevState 
         __syncthreads();
         substep(s, md, sp, am, mu);
     }
+    STAMP(0);
     if (lane < D) E.torques[D * e + lane] = s.tau[lane];
     float* rbs = st.rbs + (size_t)13 * B * e;
     body_states(s, md, rbs);  // refresh_rigid_body_state (h1_env.py:49)
     __syncthreads();
+    STAMP(15);
     post_physics(s, T, E, rbs, N, e, step, false);
     __syncthreads();
+    STAMP(16);
     store_state(s, st, e);
+    STAMP(17);
+    STAMP_FLUSH(e);
 }
 
 template <int D, int B, int ROWS>
@@ -1408,6 +1463,17 @@ LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_c
     LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
     HIP_TRY(hipGetLastError());
     return LGS_OK;
+}
+
+LGS_API int lgs_debug_set_phase_buffer(void* dev_ptr) {
+#ifdef LGS_PHASE_STAMPS
+    unsigned long long* p = (unsigned long long*)dev_ptr;
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &p, sizeof(p)));
+    return LGS_OK;
+#else
+    (void)dev_ptr;
+    return set_err(LGS_ERR_STATE, "library built without -DLGS_PHASE_STAMPS");
+#endif
 }
 
 LGS_API int lgs_get_counts(lgs_sim* s, int32_t* n, int32_t* b, int32_t* d) {
