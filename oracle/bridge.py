@@ -26,11 +26,16 @@ ENV_KEYS = ("actions", "last_actions", "last_dof_vel", "last_root_vel", "torques
             "leg_phase")
 
 
+_made = False
+
+
 def ensure_built():
-    path = cabi.oracle_path()
-    if not os.path.exists(path):
+    """(Re)build the oracle if its source changed (make is incremental), then load it."""
+    global _made
+    if not _made:
         import subprocess
-        subprocess.check_call(["make", "-C", _HERE], stdout=subprocess.DEVNULL)
+        subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+        _made = True
     return cabi.load_oracle()
 
 

@@ -354,7 +354,9 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     }
     for (int j = 0; j < D; ++j) qf[6 + j] = dofs[2 * j + 1] + dt * rhs[6 + j];
 
-    /* ---- constraint rows: joint limits then contacts (n, t1, t2) ---- */
+    /* ---- constraint rows: contacts (n, t1, t2) first, then joint limits.
+     * Gauss-Seidel visits them in this order (the HIP kernel keeps contact c at
+     * rows 3c..3c+2 so its row registers are compile-time indexed). ---- */
     static __thread float J[ROWMAX][NMAX];
     float tgt[ROWMAX], lam[ROWMAX], v[ROWMAX];
     int kind[ROWMAX]; /* 0 unilateral, 1 friction pair head, 2 friction pair tail */
@@ -364,24 +366,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     const float beta = sp->baumgarte;
     const int max_rows = sp->max_rows < ROWMAX ? sp->max_rows : ROWMAX;
     const int max_limit = max_rows - 3 * sp->max_contacts;
-    for (int j = 0; j < D && nr < max_limit; ++j) {
-        float q = dofs[2 * j], lo = md->dof_lower[j], hi = md->dof_upper[j];
-        float qn = q + dt * qf[6 + j];
-        if (qn < lo) {
-            memset(J[nr], 0, sizeof(float) * n);
-            J[nr][6 + j] = 1.f;
-            float gap = q - lo;
-            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
-            kind[nr++] = 0;
-        } else if (qn > hi) {
-            memset(J[nr], 0, sizeof(float) * n);
-            J[nr][6 + j] = -1.f;
-            float gap = hi - q;
-            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
-            kind[nr++] = 0;
-        }
-    }
-    int nlimit = nr, nc = 0;
+    int nc = 0;
     float cpt[ROWMAX / 3 + 1][3];
     for (int k = 0; k < md->num_points; ++k) {
         if (nc >= sp->max_contacts || nr + 3 > max_rows) break;
@@ -417,6 +402,24 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         nr += 3;
         ++nc;
     }
+    const int nr_c = nr;
+    for (int j = 0; j < D && nr - nr_c < max_limit; ++j) {
+        float q = dofs[2 * j], lo = md->dof_lower[j], hi = md->dof_upper[j];
+        float qn = q + dt * qf[6 + j];
+        if (qn < lo) {
+            memset(J[nr], 0, sizeof(float) * n);
+            J[nr][6 + j] = 1.f;
+            float gap = q - lo;
+            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            kind[nr++] = 0;
+        } else if (qn > hi) {
+            memset(J[nr], 0, sizeof(float) * n);
+            J[nr][6 + j] = -1.f;
+            float gap = hi - q;
+            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            kind[nr++] = 0;
+        }
+    }
     /* Y = L^-1 J^T ; A = Y^T Y ; v = J qf */
     static __thread float Y[ROWMAX][NMAX];
     static __thread float A[ROWMAX][ROWMAX];
@@ -434,17 +437,19 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
             for (int i = 0; i < n; ++i) a += Y[r][i] * Y[s][i];
             A[r][s] = A[s][r] = a;
         }
+    float inv[ROWMAX];
+    for (int r = 0; r < nr; ++r) inv[r] = 1.f / (A[r][r] + 1e-9f);
     for (int it = 0; it < sp->solver_iterations; ++it) {
         for (int r = 0; r < nr; ++r) {
             if (kind[r] == 0) {
-                float ln = fmaxf(0.f, lam[r] + (tgt[r] - v[r]) / (A[r][r] + 1e-9f));
+                float ln = fmaxf(0.f, lam[r] + (tgt[r] - v[r]) * inv[r]);
                 float d = ln - lam[r];
                 lam[r] = ln;
                 if (d != 0.f) for (int s = 0; s < nr; ++s) v[s] += A[s][r] * d;
             } else if (kind[r] == 1) {
                 float lim = mu * lam[r - 1];
-                float l1 = lam[r] - v[r] / (A[r][r] + 1e-9f);
-                float l2 = lam[r + 1] - v[r + 1] / (A[r + 1][r + 1] + 1e-9f);
+                float l1 = lam[r] - v[r] * inv[r];
+                float l2 = lam[r + 1] - v[r + 1] * inv[r + 1];
                 float nrm = sqrtf(l1 * l1 + l2 * l2);
                 if (nrm > lim) {
                     float s = nrm > 0.f ? lim / nrm : 0.f;
@@ -474,7 +479,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     /* contact forces (last substep), world frame */
     for (int b = 0; b < B; ++b) cforce[3 * b] = cforce[3 * b + 1] = cforce[3 * b + 2] = 0.f;
     for (int c = 0; c < nc; ++c) {
-        int r = nlimit + 3 * c;
+        int r = 3 * c;
         float* F = cforce + 3 * cb[c];
         F[0] += lam[r + 1] / dt;
         F[1] += lam[r + 2] / dt;

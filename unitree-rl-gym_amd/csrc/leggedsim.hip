@@ -59,6 +59,7 @@ __device__ unsigned long long* g_phase_buf;
 #define MAXB LGS_MAX_BODIES
 #define MAXD LGS_MAX_DEPTH
 #define WAVE 64
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------ errors --
 static thread_local std::string g_err;
@@ -115,6 +116,8 @@ __device__ __forceinline__ float rl(float x, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 __device__ __forceinline__ int rli(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// wave-uniform copy (SGPR) of a value that is identical in every lane
+__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
 
 __device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
     float x = a[1] * b[2] - a[2] * b[1];
@@ -203,11 +206,22 @@ __device__ __forceinline__ float rand_range(float lo, float hi, float u) { retur
 __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
 // ------------------------------------------------------------ LDS layout --
+// Model topology/geometry cached in LDS at kernel start: every chain walk and
+// subtree test below is an LDS access instead of a dependent global load.
+template <int D, int B>
+struct ModelCache {
+    int dof[B], depth[B], se[B], dofbody[D > 0 ? D : 1];
+    unsigned char chain[B][MAXD];
+    float jr[B][9], jp[B][3], ax[B][3], com[B][3], mass[B], in[B][6];
+    float lo[D > 0 ? D : 1], hi[D > 0 ? D : 1], vl[D > 0 ? D : 1];
+};
+
 template <int D, int B, int ROWS>
 struct Smem {
     static constexpr int n = 6 + D;
     static constexpr int NP = (n % 2 == 0) ? n + 1 : n;     // odd row stride: conflict-free columns
     static constexpr int AS = (ROWS % 2 == 0) ? ROWS + 1 : ROWS;
+    ModelCache<D, B> mc;
     float root[16];
     float q[D], qd[D], tau[D], act[D];
     float R[B][9], p[B][3], aw[B][3], cw[B][3];
@@ -218,23 +232,26 @@ struct Smem {
             float fn[B][3], ff[B][3];
             float cm[B], ch[B][3], cI[B][6];
             float Fn[B][3], Ff[B][3];
+            float Fj[D][6];
         } dyn;
         struct {
             float Y[ROWS][NP];
-            float A[ROWS][AS];
+            // <= 32 rows: A never leaves registers (one MFMA tile, columns per lane)
+            float A[ROWS > 32 ? ROWS : 1][ROWS > 32 ? AS : 1];
         } con;
+        struct {  // post-physics scratch
+            float obs_tmp[LGS_MAX_OBS];
+            float terms[LGS_MAX_REWARDS + 1];
+            float misc[32];
+        } post;
     } u;
-    float M[n][NP];
+    float L[n][NP];
     float qf[n];
     float tgt[ROWS];
-    int kind[ROWS];
     int c_body[ROWS / 3];
     float c_pt[ROWS / 3][3];
     float c_sep[ROWS / 3];
     float cf[B][3];
-    // post-physics scratch
-    float obs_tmp[LGS_MAX_OBS];
-    float misc[32];
     int flags[8];
 #ifdef LGS_PHASE_STAMPS
     unsigned long long stamps[LGS_NPHASE];
@@ -242,15 +259,50 @@ struct Smem {
 #endif
 };
 
+template <int D, int B, int ROWS>
+__device__ __forceinline__ void load_model(Smem<D, B, ROWS>& s, const DevModel& md) {
+    const int lane = threadIdx.x;
+    ModelCache<D, B>& c = s.mc;
+    if (lane < B) {
+        const int j = md.dof[lane];
+        c.dof[lane] = j;
+        c.depth[lane] = md.depth[lane];
+        c.se[lane] = md.subtree_end[lane];
+        c.mass[lane] = md.mass[lane];
+        if (j >= 0) c.dofbody[j] = lane;
+    }
+    for (int i = lane; i < B * MAXD; i += WAVE) (&c.chain[0][0])[i] = (unsigned char)md.chain[i];
+    for (int i = lane; i < 9 * B; i += WAVE) (&c.jr[0][0])[i] = md.joint_rot[i];
+    for (int i = lane; i < 3 * B; i += WAVE) {
+        (&c.jp[0][0])[i] = md.joint_pos[i];
+        (&c.ax[0][0])[i] = md.axis[i];
+        (&c.com[0][0])[i] = md.com[i];
+    }
+    for (int i = lane; i < 6 * B; i += WAVE) (&c.in[0][0])[i] = md.inertia[i];
+    if (lane < D) {
+        c.lo[lane] = md.dof_lower[lane];
+        c.hi[lane] = md.dof_upper[lane];
+        c.vl[lane] = md.dof_velocity[lane];
+    }
+}
+
 // -------------------------------------------------------------- substep --
 // One physics substep of this block's env.  Preconditions: s.root/q/qd/tau hold
-// the state and the torques.  Postcondition: state integrated, s.cf = contact
-// forces of this substep.  All 64 lanes must call it.
+// the state and the torques, s.mc the model.  Postcondition: state integrated,
+// s.cf = contact forces of this substep.  All 64 lanes must call it.
+//
+// Register-resident linear algebra (lane i < n owns row i of M / L):
+//   mass matrix row assembled in-lane from the composites; right-looking
+//   Cholesky with v_readlane broadcasts (per entry the same subtraction order
+//   as the oracle's left-looking loop); triangular solves on register rows
+//   (forward) and register columns (backward); Y = L^-1 J^T with L entries
+//   broadcast by readlane; A = Y Y^T on the matrix cores
+//   (v_mfma_f32_32x32x2_f32: exact fp32 fma chain over k); PGS with each lane
+//   holding its column of A in registers.
 template <int D, int B, int ROWS>
 __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& sp, float added_mass, float shape_mu) {
     constexpr int n = 6 + D;
-    constexpr int NP = Smem<D, B, ROWS>::NP;
-    constexpr int AS = Smem<D, B, ROWS>::AS;
+    const ModelCache<D, B>& mc = s.mc;
     const int lane = threadIdx.x;
     const float dt = sp.dt;
 
@@ -260,18 +312,18 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
         quat_to_mat(s.root + 3, R);
         p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
-        const int d = md.depth[lane];
+        const int d = mc.depth[lane];
         for (int l = 1; l <= d; ++l) {
-            const int a = md.chain[lane * MAXD + l];
+            const int a = mc.chain[lane][l];
             float Rj[9], t[3];
-            matmul(R, md.joint_rot + 9 * a, Rj);
-            matvec(R, md.joint_pos + 3 * a, t);
+            matmul(R, mc.jr[a], Rj);
+            matvec(R, mc.jp[a], t);
             p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
-            const int j = md.dof[a];
+            const int j = mc.dof[a];
             if (j >= 0) {
-                if (l == d) matvec(Rj, md.axis + 3 * a, aw);
+                if (l == d) matvec(Rj, mc.ax[a], aw);
                 float Ra[9];
-                axis_angle(md.axis + 3 * a, s.q[j], Ra);
+                axis_angle(mc.ax[a], s.q[j], Ra);
                 matmul(Rj, Ra, R);
             } else {
 #pragma unroll
@@ -279,7 +331,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             }
         }
         float c[3];
-        matvec(R, md.com + 3 * lane, c);
+        matvec(R, mc.com[lane], c);
 #pragma unroll
         for (int k = 0; k < 9; ++k) s.R[lane][k] = R[k];
 #pragma unroll
@@ -301,9 +353,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     // ---- 2. per-body spatial inertia at O and motion subspace
     if (lane < B) {
-        float m = md.mass[lane], scale = 1.f;
+        float m = mc.mass[lane], scale = 1.f;
         if (lane == 0 && added_mass != 0.f && m > 0.f) { scale = (m + added_mass) / m; m = m + added_mass; }
-        const float* Il = md.inertia + 6 * lane;
+        const float* Il = mc.in[lane];
         float IL[9] = {Il[0] * scale, Il[3] * scale, Il[4] * scale, Il[3] * scale, Il[1] * scale,
                        Il[5] * scale, Il[4] * scale, Il[5] * scale, Il[2] * scale};
         float R[9], Rt[9], T[9], Iw[9];
@@ -337,10 +389,10 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     if (lane < B) {
         float Vw[3] = {w0[0], w0[1], w0[2]}, Vv[3] = {vO[0], vO[1], vO[2]};
         float Aw[3] = {0.f, 0.f, 0.f}, Av[3] = {-sp.gx, -sp.gy, -sp.gz};
-        const int d = md.depth[lane];
+        const int d = mc.depth[lane];
         for (int l = 1; l <= d; ++l) {
-            const int a = md.chain[lane * MAXD + l];
-            const int j = md.dof[a];
+            const int a = mc.chain[lane][l];
+            const int j = mc.dof[a];
             if (j < 0) continue;
             const float qd = s.qd[j];
             float sw[3] = {s.u.dyn.Sw[a][0] * qd, s.u.dyn.Sw[a][1] * qd, s.u.dyn.Sw[a][2] * qd};
@@ -376,17 +428,14 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     __syncthreads();
     STAMP(3);
-    // ---- 4. subtree (composite) sums: lane b adds the contiguous DFS range.
-    // Summation order mirrors the oracle's leaf-to-root accumulation.
+    // ---- 4. subtree (composite) sums: lane b adds its contiguous DFS range,
+    // last to first (the oracle's order).  Loads of an iteration are independent;
+    // unrolling lets them overlap the 16 add chains.
     if (lane < B) {
-        // oracle: for b = B-1..1: Ic[parent] += Ic[b]  -> per node the children are
-        // added in descending child order, each child's value already complete.
-        // A descending scan of the subtree with a per-node stack reproduces that;
-        // for simplicity we recompute composite values with the same recursion
-        // bottom-up per lane (trees here are <= 32 nodes).
-        const int end = md.subtree_end[lane];
+        const int end = mc.se[lane];
         float cm = 0.f, ch[3] = {0.f, 0.f, 0.f}, cI[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         float Fn[3] = {0.f, 0.f, 0.f}, Ff[3] = {0.f, 0.f, 0.f};
+#pragma unroll 4
         for (int k = end - 1; k >= lane; --k) {
             cm += s.u.dyn.m[k];
 #pragma unroll
@@ -401,61 +450,63 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int t = 0; t < 6; ++t) s.u.dyn.cI[lane][t] = cI[t];
     }
     __syncthreads();
-    STAMP(4);
-    // ---- 5. mass matrix (lower triangle) and rhs = tau - C
-    for (int idx = lane; idx < n * (n + 1) / 2; idx += WAVE) {
-        int r = (int)((sqrtf(8.f * idx + 1.f) - 1.f) * 0.5f);
-        while ((r + 1) * (r + 2) / 2 <= idx) ++r;
-        while (r * (r + 1) / 2 > idx) --r;
-        const int c = idx - r * (r + 1) / 2;  // r >= c
-        float val;
-        if (r < 6) {  // base-base block of the root composite
-            const float* I = s.u.dyn.cI[0];
-            const float* h = s.u.dyn.ch[0];
-            if (r < 3) {  // c < 3
-                const int m3[9] = {0, 3, 4, 3, 1, 5, 4, 5, 2};
-                val = I[m3[3 * r + c]];
-            } else if (c < 3) {  // row 3+i, col c : [h]x^T (i, c) = [h]x (c, i)
-                const int i = r - 3;
-                const float H[9] = {0, -h[2], h[1], h[2], 0, -h[0], -h[1], h[0], 0};
-                val = H[3 * c + i];
-            } else {
-                val = (r == c) ? s.u.dyn.cm[0] : 0.f;
-            }
-        } else {
-            const int j = r - 6;
-            int bj = -1;
-            for (int b = 1; b < B; ++b) if (md.dof[b] == j) bj = b;
-            float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
-            float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
-            float cn[3], cf[3];
-            sin_apply(s.u.dyn.cm[bj], s.u.dyn.ch[bj], s.u.dyn.cI[bj], Sw, Sv, cn, cf);
-            if (c < 3) val = cn[c];
-            else if (c < 6) val = cf[c - 3];
-            else {
-                const int i = c - 6;  // i <= j
-                int bi = -1;
-                for (int b = 1; b < B; ++b) if (md.dof[b] == i) bi = b;
-                if (bj >= bi && bj < md.subtree_end[bi]) {
-                    float Si_w[3] = {s.u.dyn.Sw[bi][0], s.u.dyn.Sw[bi][1], s.u.dyn.Sw[bi][2]};
-                    float Si_v[3] = {s.u.dyn.Sv[bi][0], s.u.dyn.Sv[bi][1], s.u.dyn.Sv[bi][2]};
-                    val = dot3(Si_w, cn) + dot3(Si_v, cf);
-                    if (i == j) val += sp.armature;
-                } else {
-                    val = 0.f;
-                }
-            }
-        }
-        s.M[r][c] = val;
+    // F_j = Ic(b_j) S_j (lane per DOF): the base block of M's row 6+j and, dotted
+    // with S_i, every DOF-DOF entry of that row.
+    if (lane < D) {
+        const int bj = mc.dofbody[lane];
+        float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
+        float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
+        float cn[3], cf[3];
+        sin_apply(s.u.dyn.cm[bj], s.u.dyn.ch[bj], s.u.dyn.cI[bj], Sw, Sv, cn, cf);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { s.u.dyn.Fj[lane][k] = cn[k]; s.u.dyn.Fj[lane][3 + k] = cf[k]; }
     }
-    // rhs in lanes 0..n-1 (registers), C from the composites
+    __syncthreads();
+    STAMP(4);
+    // ---- 5. row `lane` of the mass matrix (lower triangle) into registers, rhs = tau - C
+    float m[n];
     float x = 0.f;
+#pragma unroll
+    for (int c = 0; c < n; ++c) m[c] = 0.f;
     if (lane < 6) {
+        const float* I = s.u.dyn.cI[0];
+        const float* h = s.u.dyn.ch[0];
+        const float cm0 = s.u.dyn.cm[0];
+        // [[I, [h]x], [[h]x^T, m 1]]: rows 0-2 need cols 0-2 only (lower triangle)
+        if (lane < 3) {
+            const int r = lane;
+            m[0] = I[r == 0 ? 0 : (r == 1 ? 3 : 4)];
+            m[1] = I[r == 0 ? 3 : (r == 1 ? 1 : 5)];
+            m[2] = I[r == 0 ? 4 : (r == 1 ? 5 : 2)];
+        } else {
+            const int i = lane - 3;  // ([h]x)^T row i = column i of [h]x
+            const float H[9] = {0.f, -h[2], h[1], h[2], 0.f, -h[0], -h[1], h[0], 0.f};
+            m[0] = H[i]; m[1] = H[3 + i]; m[2] = H[6 + i];
+            m[3] = (i == 0) ? cm0 : 0.f;
+            m[4] = (i == 1) ? cm0 : 0.f;
+            m[5] = (i == 2) ? cm0 : 0.f;
+        }
         x = -(lane < 3 ? s.u.dyn.Fn[0][lane] : s.u.dyn.Ff[0][lane - 3]);
     } else if (lane < n) {
         const int j = lane - 6;
-        int bj = -1;
-        for (int b = 1; b < B; ++b) if (md.dof[b] == j) bj = b;
+        const int bj = mc.dofbody[j];
+        float cn[3], cf[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { cn[k] = s.u.dyn.Fj[j][k]; cf[k] = s.u.dyn.Fj[j][3 + k]; }
+        m[0] = cn[0]; m[1] = cn[1]; m[2] = cn[2];
+        m[3] = cf[0]; m[4] = cf[1]; m[5] = cf[2];
+#pragma unroll
+        for (int c = 6; c < n; ++c) {
+            const int i = c - 6;
+            const int bi = mc.dofbody[i];
+            if (i <= j && bj >= bi && bj < mc.se[bi]) {
+                float Si_w[3] = {s.u.dyn.Sw[bi][0], s.u.dyn.Sw[bi][1], s.u.dyn.Sw[bi][2]};
+                float Si_v[3] = {s.u.dyn.Sv[bi][0], s.u.dyn.Sv[bi][1], s.u.dyn.Sv[bi][2]};
+                float val = dot3(Si_w, cn) + dot3(Si_v, cf);
+                if (i == j) val += sp.armature;
+                m[c] = val;
+            }
+        }
         float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
         float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
         float Fn[3] = {s.u.dyn.Fn[bj][0], s.u.dyn.Fn[bj][1], s.u.dyn.Fn[bj][2]};
@@ -463,35 +514,46 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         float C = dot3(Sw, Fn) + dot3(Sv, Ff);
         x = s.tau[j] - C;
     }
-    __syncthreads();
     STAMP(5);
-    // ---- 6. Cholesky (left-looking, in place, lane per row)
+    // ---- 6. Cholesky, right-looking on register rows.  Entry (i,j) receives
+    // -L_ik L_jk for k = 0..j-1 in ascending order, then / L_jj: the oracle's
+    // left-looking arithmetic, operation for operation.
+#pragma unroll
     for (int k = 0; k < n; ++k) {
-        if (lane >= k && lane < n) {
-            float d = s.M[k][k];
-            for (int t = 0; t < k; ++t) d -= s.M[k][t] * s.M[k][t];
-            d = sqrtf(fmaxf(d, 1e-12f));
-            if (lane == k) {
-                s.M[k][k] = d;
-            } else {
-                float v = s.M[lane][k];
-                for (int t = 0; t < k; ++t) v -= s.M[lane][t] * s.M[k][t];
-                s.M[lane][k] = v / d;
-            }
+        const float d = sqrtf(fmaxf(rl(m[k], k), 1e-12f));
+        if (lane == k) m[k] = d;
+        else if (lane > k) m[k] = m[k] / d;
+#pragma unroll
+        for (int j = k + 1; j < n; ++j) {
+            const float ljk = rl(m[k], j);
+            if (lane >= j) m[j] -= m[k] * ljk;
         }
-        __syncthreads();
+    }
+    // rows of L to LDS; lane j then holds column j (c[k] = L[k][j], k >= j)
+    if (lane < n) {
+#pragma unroll
+        for (int c = 0; c < n; ++c)
+            if (c <= lane) s.L[lane][c] = m[c];
     }
     STAMP(6);
-    // ---- 7. qdd = M^-1 rhs by column sweeps (lane i owns x_i)
+    // ---- 7. qdd = M^-1 rhs: forward on rows (registers), backward on columns
+#pragma unroll
     for (int i = 0; i < n; ++i) {
-        if (lane == i) x = x / s.M[i][i];
+        if (lane == i) x = x / m[i];
         const float xi = rl(x, i);
-        if (lane > i && lane < n) x -= s.M[lane][i] * xi;
+        if (lane > i) x -= m[i] * xi;
     }
-    for (int i = n - 1; i >= 0; --i) {
-        if (lane == i) x = x / s.M[i][i];
-        const float xi = rl(x, i);
-        if (lane < i) x -= s.M[i][lane] * xi;
+    __syncthreads();
+    {
+        float lc[n];
+#pragma unroll
+        for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
+#pragma unroll
+        for (int i = n - 1; i >= 0; --i) {
+            if (lane == i) x = x / lc[i];
+            const float xi = rl(x, i);
+            if (lane < i) x -= lc[i] * xi;
+        }
     }
     // free velocity (classical velocity of the root origin after dt)
     {
@@ -507,36 +569,14 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     __syncthreads();
     STAMP(7);
-    // ---- 8. constraint rows.  Joint limits first (DOF order), then contacts.
+    // ---- 8. constraint rows.  Fixed layout: contact c at rows 3c (normal),
+    // 3c+1, 3c+2 (friction), c < CM; joint limit l at row 3*CM + l, l < LM.
+    // Gauss-Seidel order: contacts ascending, then limits (oracle's row order).
+    constexpr int CM = ROWS / 4, LM = ROWS - 3 * CM;
     const float beta = sp.beta;
-    int nlimit;
-    {
-        bool lo_act = false, hi_act = false;
-        float gap = 0.f;
-        if (lane < D) {
-            const float qj = s.q[lane], lo = md.dof_lower[lane], hi = md.dof_upper[lane];
-            const float qn = qj + dt * s.qf[6 + lane];
-            if (qn < lo) { lo_act = true; gap = qj - lo; }
-            else if (qn > hi) { hi_act = true; gap = hi - qj; }
-        }
-        const bool act = lo_act || hi_act;
-        const uint64_t mask = __ballot(act);
-        const int slot = __popcll(mask & ((1ull << lane) - 1ull));
-        const int max_limit = sp.max_rows - 3 * sp.max_contacts;
-        nlimit = __popcll(mask);
-        if (nlimit > max_limit) nlimit = max_limit;
-        if (act && slot < max_limit) {
-            float* row = s.u.con.Y[slot];
-            for (int i = 0; i < n; ++i) row[i] = 0.f;
-            row[6 + lane] = lo_act ? 1.f : -1.f;
-            s.tgt[slot] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
-            s.kind[slot] = 0;
-        }
-    }
     int nc = 0;
     {
-        const int maxc0 = (sp.max_rows - nlimit) / 3;
-        const int maxc = maxc0 < sp.max_contacts ? maxc0 : sp.max_contacts;
+        const int maxc = sp.max_contacts < CM ? sp.max_contacts : CM;
         for (int base = 0; base < md.P && nc < maxc; base += WAVE) {
             const int k = base + lane;
             bool act = false;
@@ -544,12 +584,13 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             int b = 0;
             if (k < md.P) {
                 b = md.pt_body[k];
+                float pp[3] = {md.pt_pos[3 * k], md.pt_pos[3 * k + 1], md.pt_pos[3 * k + 2]};
+                rad = md.pt_radius[k];
                 float R[9];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) R[t] = s.R[b][t];
-                matvec(R, md.pt_pos + 3 * k, c);
+                matvec(R, pp, c);
                 c[0] += s.p[b][0]; c[1] += s.p[b][1]; c[2] += s.p[b][2];
-                rad = md.pt_radius[k];
                 sep = c[2] - rad - sp.rest_offset;
                 act = sep < sp.contact_offset;
             }
@@ -564,12 +605,36 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             if (nc > maxc) nc = maxc;
         }
     }
-    const int nrows = nlimit + 3 * nc;
+    int nlimit;
+    {
+        bool lo_act = false, hi_act = false;
+        float gap = 0.f;
+        if (lane < D) {
+            const float qj = s.q[lane], lo = mc.lo[lane], hi = mc.hi[lane];
+            const float qn = qj + dt * s.qf[6 + lane];
+            if (qn < lo) { lo_act = true; gap = qj - lo; }
+            else if (qn > hi) { hi_act = true; gap = hi - qj; }
+        }
+        const bool act = lo_act || hi_act;
+        const uint64_t mask = __ballot(act);
+        const int slot = __popcll(mask & ((1ull << lane) - 1ull));
+        int max_limit = sp.max_rows - 3 * sp.max_contacts;
+        if (max_limit > LM) max_limit = LM;
+        nlimit = __popcll(mask);
+        if (nlimit > max_limit) nlimit = max_limit;
+        if (act && slot < max_limit) {
+            const int r = 3 * CM + slot;
+            float* row = s.u.con.Y[r];
+            for (int i = 0; i < n; ++i) row[i] = 0.f;
+            row[6 + lane] = lo_act ? 1.f : -1.f;
+            s.tgt[r] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+        }
+    }
     __syncthreads();
     STAMP(8);
     // contact rows (lane per row): J row into Y[r]
-    if (lane >= nlimit && lane < nrows) {
-        const int cc = (lane - nlimit) / 3, dd = (lane - nlimit) % 3;
+    if (lane < 3 * nc) {
+        const int cc = lane / 3, dd = lane % 3;
         const float d[3] = {dd == 1 ? 1.f : 0.f, dd == 2 ? 1.f : 0.f, dd == 0 ? 1.f : 0.f};
         const int b = s.c_body[cc];
         float pc[3] = {s.c_pt[cc][0], s.c_pt[cc][1], s.c_pt[cc][2]};
@@ -579,114 +644,192 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int i = 0; i < n; ++i) row[i] = 0.f;
         row[0] = rxd[0]; row[1] = rxd[1]; row[2] = rxd[2];
         row[3] = d[0]; row[4] = d[1]; row[5] = d[2];
-        const int dep = md.depth[b];
+        const int dep = mc.depth[b];
         for (int l = 1; l <= dep; ++l) {
-            const int a = md.chain[b * MAXD + l];
-            const int j = md.dof[a];
+            const int a = mc.chain[b][l];
+            const int j = mc.dof[a];
             if (j < 0) continue;
             float rp[3] = {pc[0] - s.p[a][0], pc[1] - s.p[a][1], pc[2] - s.p[a][2]}, t[3];
             float aw[3] = {s.aw[a][0], s.aw[a][1], s.aw[a][2]};
             cross3(aw, rp, t);
             row[6 + j] = dot3(d, t);
         }
-        if (dd == 0) {
-            const float sep = s.c_sep[cc];
-            s.tgt[lane] = sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp.max_depen);
-            s.kind[lane] = 0;
-        } else {
-            s.tgt[lane] = 0.f;
-            s.kind[lane] = dd;  // 1 = friction head, 2 = tail
-        }
+        const float sep = s.c_sep[cc];
+        s.tgt[lane] = dd != 0 ? 0.f : (sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp.max_depen));
     }
     __syncthreads();
     STAMP(9);
-    // ---- 9. v = J qf ; Y = L^-1 J^T (lane r, registers)
-    float y[n];
-    float v = 0.f, lam = 0.f;
-    if (lane < nrows) {
+    const bool used = (lane < 3 * nc) || (lane >= 3 * CM && lane < 3 * CM + nlimit);
+    // ---- 9. v = J qf ; Y = L^-1 J^T (lane r; L entries broadcast from their row lanes)
+    float v = 0.f;
+    {
+        float y[n];
 #pragma unroll
-        for (int i = 0; i < n; ++i) y[i] = s.u.con.Y[lane][i];
+        for (int i = 0; i < n; ++i) y[i] = used ? s.u.con.Y[lane][i] : 0.f;
 #pragma unroll
         for (int i = 0; i < n; ++i) v += y[i] * s.qf[i];
 #pragma unroll
         for (int i = 0; i < n; ++i) {
             float t = y[i];
 #pragma unroll
-            for (int k = 0; k < i; ++k) t -= s.M[i][k] * y[k];
-            y[i] = t / s.M[i][i];
+            for (int k = 0; k < i; ++k) t -= rl(m[k], i) * y[k];
+            y[i] = t / rl(m[i], i);
         }
+        if (lane < ROWS) {
 #pragma unroll
-        for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = y[i];
+            for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = y[i];
+        }
     }
     __syncthreads();
     STAMP(10);
-    // ---- 10. A = Y^T Y (lane r computes row r)
-    float diag = 1.f;
-    if (lane < nrows) {
-        for (int t = 0; t < nrows; ++t) {
-            float a = 0.f;
+    // ---- 10. A = Y Y^T on the matrix cores, 32x32 tiles, k = 2 per instruction.
+    // Lane l feeds Y[row0 + (l&31)][2t + (l>>5)]; D element (row, col) is the fp32
+    // fma chain over k ascending (the oracle's loop).  Unused rows are zero.
+    // ---- 11. projected Gauss-Seidel.  Lane s holds column s of A (registers) and
+    // v_s; per-row lambda are wave-uniform (SGPRs).  One contact = normal row,
+    // then its friction pair against the post-normal velocities.
+    const int li = lane & 31, lk = lane >> 5;
+    float acol[ROWS];
+    if constexpr (ROWS <= 32) {
+        // one tile; lane l < 32 owns column l: rows (t&3)+8(t>>2) from its own
+        // accumulators, rows +4 from lane l+32's.
+        floatx16 acc;
 #pragma unroll
-            for (int i = 0; i < n; ++i) a += y[i] * s.u.con.Y[t][i];
-            s.u.con.A[lane][t] = a;
-            if (t == lane) diag = a;
+        for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+#pragma unroll
+        for (int st = 0; st < (n + 1) / 2; ++st) {
+            const int kk = 2 * st + lk;
+            const float a = (li < ROWS && kk < n) ? s.u.con.Y[li][kk] : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, acc, 0, 0, 0);
         }
-    }
-    __syncthreads();
-    STAMP(11);
-    // ---- 11. projected Gauss-Seidel
-    const float mu = 0.5f * (sp.ground_friction + shape_mu);
-    const float tg = (lane < nrows) ? s.tgt[lane] : 0.f;
-    for (int it = 0; it < sp.iters; ++it) {
-        for (int r = 0; r < nrows; ++r) {
-            const int kd = s.kind[r];
-            if (kd == 0) {
-                const float vr = rl(v, r), lr = rl(lam, r), ar = rl(diag, r), tr = rl(tg, r);
-                const float ln = fmaxf(0.f, lr + (tr - vr) / (ar + 1e-9f));
-                const float dl = ln - lr;
-                if (lane == r) lam = ln;
-                if (dl != 0.f && lane < nrows) v += s.u.con.A[r][lane] * dl;
-            } else if (kd == 1) {
-                const float lim = mu * rl(lam, r - 1);
-                const float l1o = rl(lam, r), l2o = rl(lam, r + 1);
-                float l1 = l1o - rl(v, r) / (rl(diag, r) + 1e-9f);
-                float l2 = l2o - rl(v, r + 1) / (rl(diag, r + 1) + 1e-9f);
-                const float nrm = sqrtf(l1 * l1 + l2 * l2);
-                if (nrm > lim) {
-                    const float sc = nrm > 0.f ? lim / nrm : 0.f;
-                    l1 *= sc; l2 *= sc;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int r0 = (t & 3) + 8 * (t >> 2);
+            const float other = __shfl_xor(acc[t], 32);
+            if (r0 < ROWS) acol[r0] = acc[t];
+            if (r0 + 4 < ROWS) acol[r0 + 4] = other;
+        }
+        STAMP(11);
+    } else {
+        const int hi_row = nlimit > 0 ? 3 * CM + nlimit : 3 * nc;
+        const int nt = (hi_row + 31) >> 5;
+        for (int ti = 0; ti < nt; ++ti) {
+            for (int tj = 0; tj <= ti; ++tj) {
+                const int ra = 32 * ti + li, rb = 32 * tj + li;
+                floatx16 acc;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+#pragma unroll
+                for (int st = 0; st < (n + 1) / 2; ++st) {
+                    const int kk = 2 * st + lk;
+                    const float a = (ra < ROWS && kk < n) ? s.u.con.Y[ra][kk] : 0.f;
+                    const float b = (rb < ROWS && kk < n) ? s.u.con.Y[rb][kk] : 0.f;
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
                 }
-                const float d1 = l1 - l1o, d2 = l2 - l2o;
-                if (lane == r) lam = l1;
-                if (lane == r + 1) lam = l2;
-                if (lane < nrows) v += s.u.con.A[r][lane] * d1 + s.u.con.A[r + 1][lane] * d2;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int R_ = 32 * ti + (t & 3) + 8 * (t >> 2) + 4 * lk;
+                    const int C_ = 32 * tj + li;
+                    if (R_ < ROWS && C_ < ROWS) {
+                        s.u.con.A[R_][C_] = acc[t];
+                        if (ti != tj) s.u.con.A[C_][R_] = acc[t];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(11);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acol[r] = (lane < ROWS) ? s.u.con.A[r][lane < ROWS ? lane : 0] : 0.f;
+    }
+    float lamv[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) lamv[r] = 0.f;
+    {
+        const float mu = 0.5f * (sp.ground_friction + shape_mu);
+        const float tg = used ? s.tgt[lane] : 0.f;
+        float dg = 0.f;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) dg = (lane == r) ? acol[r] : dg;
+        const float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
+        for (int it = 0; it < sp.iters; ++it) {
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                if (c < nc) {
+                    const int r = 3 * c;
+                    const float vn = rl(v, r), v1 = rl(v, r + 1), v2 = rl(v, r + 2);
+                    const float ln = fmaxf(0.f, lamv[r] + (rl(tg, r) - vn) * rl(inv, r));
+                    const float dn = ln - lamv[r];
+                    v = fmaf(acol[r], dn, v);
+                    const float v1n = fmaf(rl(acol[r], r + 1), dn, v1);
+                    const float v2n = fmaf(rl(acol[r], r + 2), dn, v2);
+                    const float lim = mu * ln;
+                    const float l1o = lamv[r + 1], l2o = lamv[r + 2];
+                    float l1 = l1o - v1n * rl(inv, r + 1);
+                    float l2 = l2o - v2n * rl(inv, r + 2);
+                    const float nrm = sqrtf(l1 * l1 + l2 * l2);
+                    if (nrm > lim) {
+                        const float sc = nrm > 0.f ? lim / nrm : 0.f;
+                        l1 *= sc; l2 *= sc;
+                    }
+                    const float d1 = l1 - l1o, d2 = l2 - l2o;
+                    v += acol[r + 1] * d1 + acol[r + 2] * d2;
+                    lamv[r] = rfl(ln);
+                    lamv[r + 1] = rfl(l1);
+                    lamv[r + 2] = rfl(l2);
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < LM; ++l) {
+                if (l < nlimit) {
+                    const int r = 3 * CM + l;
+                    const float ln = fmaxf(0.f, lamv[r] + (rl(tg, r) - rl(v, r)) * rl(inv, r));
+                    const float dl = ln - lamv[r];
+                    v = fmaf(acol[r], dl, v);
+                    lamv[r] = rfl(ln);
+                }
             }
         }
     }
     STAMP(12);
-    // ---- 12. z = Y^T lambda ; dq = L^-T z ; qd' = qf + dq
+    // ---- 12. z = Y^T lambda ; dq = L^-T z (register columns) ; qd' = qf + dq
     float z = 0.f;
-    for (int r = 0; r < nrows; ++r) {
-        const float lr = rl(lam, r);
-        if (lane < n) z += s.u.con.Y[r][lane] * lr;
+    if (lane < n) {
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < nc) {
+                z += s.u.con.Y[3 * c][lane] * lamv[3 * c];
+                z += s.u.con.Y[3 * c + 1][lane] * lamv[3 * c + 1];
+                z += s.u.con.Y[3 * c + 2][lane] * lamv[3 * c + 2];
+            }
+#pragma unroll
+        for (int l = 0; l < LM; ++l)
+            if (l < nlimit) z += s.u.con.Y[3 * CM + l][lane] * lamv[3 * CM + l];
     }
-    for (int i = n - 1; i >= 0; --i) {
-        if (lane == i) z = z / s.M[i][i];
-        const float zi = rl(z, i);
-        if (lane < i) z -= s.M[i][lane] * zi;
+    {
+        float lc[n];
+#pragma unroll
+        for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
+#pragma unroll
+        for (int i = n - 1; i >= 0; --i) {
+            if (lane == i) z = z / lc[i];
+            const float zi = rl(z, i);
+            if (lane < i) z -= lc[i] * zi;
+        }
     }
     float qn = (lane < n) ? s.qf[lane] + z : 0.f;
     if (sp.clamp_qd && lane >= 6 && lane < n) {
-        const float lim = md.dof_velocity[lane - 6];
+        const float lim = mc.vl[lane - 6];
         if (lim > 0.f) qn = fminf(fmaxf(qn, -lim), lim);
     }
     // contact forces of this substep
     {
         float F[3] = {0.f, 0.f, 0.f};
-        for (int c = 0; c < nc; ++c) {
-            const int r = nlimit + 3 * c;
-            const float ln = rl(lam, r), l1 = rl(lam, r + 1), l2 = rl(lam, r + 2);
-            if (s.c_body[c] == lane) { F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt; }
-        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+            if (c < nc && s.c_body[c] == lane) {
+                F[0] += lamv[3 * c + 1] / dt; F[1] += lamv[3 * c + 2] / dt; F[2] += lamv[3 * c] / dt;
+            }
         if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
     }
     STAMP(13);
@@ -715,7 +858,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < 4; ++k) q[k] *= nn;
         float R[9], c[3], wc[3];
         quat_to_mat(q, R);
-        matvec(R, md.com, c);
+        matvec(R, mc.com[0], c);
         cross3(w, c, wc);
         rt[10] = w[0]; rt[11] = w[1]; rt[12] = w[2];
         rt[7] = qv0 + wc[0]; rt[8] = qv1 + wc[1]; rt[9] = qv2 + wc[2];
@@ -726,7 +869,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 
 // rigid body states [B][13] of the block's env into global memory
 template <int D, int B, int ROWS>
-__device__ void body_states(Smem<D, B, ROWS>& s, const DevModel& md, float* rbs_out) {
+__device__ void body_states(Smem<D, B, ROWS>& s, float* rbs_out) {
+    const ModelCache<D, B>& mc = s.mc;
     const int lane = threadIdx.x;
     if (lane < B) {
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
@@ -734,23 +878,23 @@ __device__ void body_states(Smem<D, B, ROWS>& s, const DevModel& md, float* rbs_
         p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
         const float O[3] = {p[0], p[1], p[2]};
         float c0[3];
-        matvec(R, md.com, c0);
+        matvec(R, mc.com[0], c0);
         float w[3] = {s.root[10], s.root[11], s.root[12]}, t[3];
         cross3(w, c0, t);
         float Vw[3] = {w[0], w[1], w[2]};
         float Vv[3] = {s.root[7] - t[0], s.root[8] - t[1], s.root[9] - t[2]};
-        const int d = md.depth[lane];
+        const int d = mc.depth[lane];
         for (int l = 1; l <= d; ++l) {
-            const int a = md.chain[lane * MAXD + l];
+            const int a = mc.chain[lane][l];
             float Rj[9], tp[3];
-            matmul(R, md.joint_rot + 9 * a, Rj);
-            matvec(R, md.joint_pos + 3 * a, tp);
+            matmul(R, mc.jr[a], Rj);
+            matvec(R, mc.jp[a], tp);
             p[0] += tp[0]; p[1] += tp[1]; p[2] += tp[2];
-            const int j = md.dof[a];
+            const int j = mc.dof[a];
             if (j >= 0) {
-                matvec(Rj, md.axis + 3 * a, aw);
+                matvec(Rj, mc.ax[a], aw);
                 float Ra[9];
-                axis_angle(md.axis + 3 * a, s.q[j], Ra);
+                axis_angle(mc.ax[a], s.q[j], Ra);
                 matmul(Rj, Ra, R);
                 const float qd = s.qd[j];
                 float rp[3] = {p[0] - O[0], p[1] - O[1], p[2] - O[2]}, sv[3];
@@ -763,7 +907,7 @@ __device__ void body_states(Smem<D, B, ROWS>& s, const DevModel& md, float* rbs_
             }
         }
         float c[3];
-        matvec(R, md.com + 3 * lane, c);
+        matvec(R, mc.com[lane], c);
         float r[3] = {p[0] + c[0] - O[0], p[1] + c[1] - O[1], p[2] + c[2] - O[2]}, wr[3];
         cross3(Vw, r, wr);
         float* o = rbs_out + 13 * lane;
@@ -799,12 +943,13 @@ __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevSt
     __shared__ Smem<D, B, ROWS> s;
     const int e = blockIdx.x;
     if (e >= N) return;
+    load_model(s, md);
     load_state(s, st, e);
     if (threadIdx.x < D) s.tau[threadIdx.x] = st.torques_in[(size_t)D * e + threadIdx.x];
     __syncthreads();
     substep(s, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
     store_state(s, st, e);
-    if (st.rbs) body_states(s, md, st.rbs + (size_t)13 * B * e);
+    if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
 }
 
 template <int D, int B, int ROWS>
@@ -812,9 +957,10 @@ __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = blockIdx.x;
     if (e >= N) return;
+    load_model(s, md);
     load_state(s, st, e);
     __syncthreads();
-    body_states(s, md, st.rbs + (size_t)13 * B * e);
+    body_states(s, st.rbs + (size_t)13 * B * e);
 }
 
 struct DevEnv {
@@ -1045,9 +1191,9 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
         E.base_ang_vel[3 * e + i] = ba[i];
         E.projected_gravity[3 * e + i] = pg[i];
         E.rpy[3 * e + i] = rpy[i];
-        s.misc[i] = bl[i]; s.misc[3 + i] = ba[i]; s.misc[6 + i] = pg[i];
+        s.u.post.misc[i] = bl[i]; s.u.post.misc[3 + i] = ba[i]; s.u.post.misc[6 + i] = pg[i];
     }
-    s.misc[9] = phase;
+    s.u.post.misc[9] = phase;
     if (E.phase) E.phase[e] = phase;
     if (E.leg_phase) { E.leg_phase[2 * e] = leg_phase[0]; E.leg_phase[2 * e + 1] = leg_phase[1]; }
     s.flags[0] = reset;
@@ -1112,19 +1258,19 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     if (lane == 0) {
         const float* cmd = E.commands + 4 * e;
         // quadruped obs = tmp[0:O]; humanoid priv = tmp[0:P], obs = tmp[3:3+O]
-        float* tmp = s.obs_tmp;
-        tmp[0] = s.misc[0] * T.obs_scale_lin_vel;
-        tmp[1] = s.misc[1] * T.obs_scale_lin_vel;
-        tmp[2] = s.misc[2] * T.obs_scale_lin_vel;
+        float* tmp = s.u.post.obs_tmp;
+        tmp[0] = s.u.post.misc[0] * T.obs_scale_lin_vel;
+        tmp[1] = s.u.post.misc[1] * T.obs_scale_lin_vel;
+        tmp[2] = s.u.post.misc[2] * T.obs_scale_lin_vel;
         int k = 3;
-        for (int i = 0; i < 3; ++i) tmp[k++] = s.misc[3 + i] * T.obs_scale_ang_vel;
-        for (int i = 0; i < 3; ++i) tmp[k++] = s.misc[6 + i];
+        for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[3 + i] * T.obs_scale_ang_vel;
+        for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[6 + i];
         for (int i = 0; i < 3; ++i) tmp[k++] = cmd[i] * T.commands_scale[i];
         for (int j = 0; j < D; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
         for (int j = 0; j < D; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
         for (int j = 0; j < A; ++j) tmp[k++] = act[j];
         if (T.obs_layout == LGS_OBS_HUMANOID) {
-            float ph = 2.0f * 3.14159265358979323846f * s.misc[9];
+            float ph = 2.0f * 3.14159265358979323846f * s.u.post.misc[9];
             tmp[k++] = sinf(ph);
             tmp[k++] = cosf(ph);
         }
@@ -1133,13 +1279,13 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     const int O = T.num_obs, P = T.num_privileged_obs;
     const int off = (T.obs_layout == LGS_OBS_HUMANOID) ? 3 : 0;
     for (int i = lane; i < O; i += WAVE) {
-        float x = s.obs_tmp[off + i];
+        float x = s.u.post.obs_tmp[off + i];
         if (T.add_noise) x += (2.f * philox_uniform(seed, e, step, LGS_STREAM_NOISE, i) - 1.f) * T.noise_vec[i];
         E.obs[(size_t)O * e + i] = clipf(x, -T.clip_observations, T.clip_observations);
     }
     if (P > 0 && E.priv_obs && T.obs_layout == LGS_OBS_HUMANOID)
         for (int i = lane; i < P; i += WAVE)
-            E.priv_obs[(size_t)P * e + i] = clipf(s.obs_tmp[i], -T.clip_observations, T.clip_observations);
+            E.priv_obs[(size_t)P * e + i] = clipf(s.u.post.obs_tmp[i], -T.clip_observations, T.clip_observations);
     // bookkeeping (:707-709)
     if (lane < A) E.last_actions[A * e + lane] = act[lane];
     if (lane < D) E.last_dof_vel[D * e + lane] = s.qd[lane];
@@ -1147,13 +1293,14 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
 }
 
 template <int D, int B, int ROWS>
-__global__ __launch_bounds__(WAVE) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? 4 : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = blockIdx.x;
     if (e >= N) return;
     const lgs_task_params& T = *Tp;
     const int lane = threadIdx.x;
+    load_model(s, md);
     load_state(s, st, e);
     const int A = T.num_actions;
     float a = 0.f;
@@ -1183,7 +1330,7 @@ __global__ __launch_bounds__(WAVE) void k_step(DevModel md, DevSim sp, DevState 
     STAMP(0);
     if (lane < D) E.torques[D * e + lane] = s.tau[lane];
     float* rbs = st.rbs + (size_t)13 * B * e;
-    body_states(s, md, rbs);  // refresh_rigid_body_state (h1_env.py:49)
+    body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49)
     __syncthreads();
     STAMP(15);
     post_physics(s, T, E, rbs, N, e, step, false);
@@ -1200,13 +1347,14 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     __shared__ Smem<D, B, ROWS> s;
     const int e = blockIdx.x;
     if (e >= N) return;
+    load_model(s, md);
     load_state(s, st, e);
     if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
     __syncthreads();
     post_physics(s, *Tp, E, nullptr, N, e, step, true);
     __syncthreads();
     store_state(s, st, e);
-    if (st.rbs) body_states(s, md, st.rbs + (size_t)13 * B * e);
+    if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
 }
 
 __global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, int n, int width) {
@@ -1292,9 +1440,14 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     }
     {
         const int cap = variant_rows(pick(s));
-        if (p->max_rows > cap || p->max_rows < 3 * p->max_contacts || p->max_contacts < 0) {
+        // contact c occupies rows 3c..3c+2 (c < cap/4), limit rows the tail block
+        const int cm = cap / 4, lm = cap - 3 * cm;
+        if (p->max_rows > cap || p->max_rows < 3 * p->max_contacts || p->max_contacts < 0 || p->max_contacts > cm ||
+            p->max_rows - 3 * p->max_contacts > lm) {
             delete s;
-            return set_err(LGS_ERR_ARG, "lgs_create_sim: need 3*max_contacts <= max_rows <= " + std::to_string(cap));
+            return set_err(LGS_ERR_ARG, "lgs_create_sim: need max_contacts <= " + std::to_string(cm) +
+                                            ", 3*max_contacts <= max_rows <= " + std::to_string(cap) +
+                                            ", max_rows - 3*max_contacts <= " + std::to_string(lm));
         }
     }
     const int B = s->B, D = s->D, P = s->P;
