@@ -244,3 +244,42 @@ def test_ppo_update_graph_matches_eager():
     for a, b, c in zip(params, p_graph, p0):
         assert (a.detach() - b).abs().max() <= 2.5 * 3e-4
         assert (b - c).abs().max() > 0  # the graph really stepped
+
+
+def test_ppo_graph_tracks_eager_over_many_updates():
+    """The captured update (fp32) replayed on fresh rollouts each time stays finite
+    and on the eager trajectory.  Guards two failure modes seen on this ROCm: a
+    stale autograd graph pinning AccumulateGrad to another stream (replays race),
+    and bf16 library GEMMs drifting inside the graph (mixed precision => eager)."""
+    import copy
+    from rsl_rl.algorithms import PPO
+    from rsl_rl.modules import ActorCritic
+    torch.manual_seed(0)
+    N, T, O, A = 1024, 8, 48, 12
+    ac = ActorCritic(O, O, A, [128, 64], [128, 64]).cuda()
+    algs = []
+    for graph in (True, False):
+        alg = PPO(copy.deepcopy(ac), num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3,
+                  schedule="fixed", device="cuda")
+        alg.use_graph = graph
+        alg.init_storage(N, T, [O], [None], [A])
+        algs.append(alg)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for u in range(12):
+        obs = [torch.randn(N, O, device="cuda", generator=g) for _ in range(T + 1)]
+        act = [torch.randn(N, A, device="cuda", generator=g) for _ in range(T)]
+        rew = [0.1 * torch.randn(N, device="cuda", generator=g) for _ in range(T)]
+        for alg in algs:
+            with torch.inference_mode():
+                for t in range(T):
+                    alg.act(obs[t], obs[t])
+                    alg.transition.actions = act[t]  # identical actions for both twins
+                    alg.transition.actions_log_prob = alg.actor_critic.get_actions_log_prob(act[t]).detach()
+                    alg.process_env_step(rew[t], torch.zeros(N, device="cuda", dtype=torch.bool), {})
+                alg.compute_returns(obs[T])
+            alg.update()
+        pg, pe = (list(a.actor_critic.parameters()) for a in algs)
+        assert all(torch.isfinite(p).all() for p in pg), f"graphed update went non-finite at update {u}"
+        d = max(float((x - y).abs().max()) for x, y in zip(pg, pe))
+        assert d < 2e-2, f"update {u}: graphed params drifted {d:.3e} from eager"
+    assert algs[0]._graph is not None

@@ -64,10 +64,13 @@ class PPO:
         self.use_clipped_value_loss = use_clipped_value_loss
         self.world_size = _dist_world()
         # whole-update HIP graph (MLP policies on a GPU): set use_graph=False to disable
+        # (fp32 only: bf16 autocast GEMMs inside a captured graph drift, see ActorCritic)
         self.use_graph = on_gpu and not getattr(self.actor_critic, "is_recurrent", False) and \
+            not getattr(self.actor_critic, "mixed_precision", False) and \
             self.optimizer.defaults.get("capturable", False) and \
             (self.world_size == 1 or dist.get_backend() == "nccl")
         self._graph = None
+        self._diag, self._diag_i = None, 0
         self._graph_calls = 0
         self._capturing = False
         if self.world_size > 1:
@@ -200,6 +203,17 @@ class PPO:
         with torch.no_grad():
             acc[0] += value_loss.detach()
             acc[1] += surrogate_loss.detach()
+            if self._diag is not None:  # debugging aid: per-step scalars (also inside a captured graph)
+                row = self._diag[self._diag_i % self._diag.shape[0]]
+                row.copy_(torch.stack([value_loss.detach(), surrogate_loss.detach(), sigma_batch.mean(),
+                                       mu_batch.abs().mean(), actions_log_prob_batch.mean(), ratio.mean(),
+                                       advantages_batch.mean(), old_actions_log_prob_batch.mean()]))
+                self._diag_i += 1
+        # Release this step's autograd graph.  A distribution kept alive on the
+        # module pins the parameters' AccumulateGrad nodes from the stream they were
+        # created on; a later capture on another stream then syncs against that
+        # stream and the captured update is no longer self-contained (replays race).
+        self.actor_critic.distribution = None
 
     def update(self):
         num_updates = self.num_learning_epochs * self.num_mini_batches

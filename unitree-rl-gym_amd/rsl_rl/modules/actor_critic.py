@@ -26,13 +26,16 @@ def mlp(in_dim, hidden, out_dim, activation):
 class ActorCritic(nn.Module):
     """Gaussian MLP actor + MLP critic (rsl_rl v1.0.2 ActorCritic).
 
-    ``mixed_precision=True`` runs the Linear layers under bf16 autocast (MFMA
-    GEMMs on MI355X) while parameters, the distribution and all losses stay fp32.
+    fp32 throughout by default (the reference's precision).  ``mixed_precision=True``
+    runs the Linear layers under bf16 autocast for eager use only: captured into
+    the PPO update graph, the bf16 library GEMMs drift from their eager results
+    on this ROCm (tools/probes/graph_ppo_like.py NEWDATA=1), so PPO disables its
+    graph when mixed precision is on.
     """
     is_recurrent = False
 
     def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=[256, 256, 256],
-                 critic_hidden_dims=[256, 256, 256], activation="elu", init_noise_std=1.0, mixed_precision=True,
+                 critic_hidden_dims=[256, 256, 256], activation="elu", init_noise_std=1.0, mixed_precision=False,
                  **kwargs):
         if kwargs:
             print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str([k for k in kwargs]))
