@@ -255,7 +255,7 @@ def test_ppo_graph_tracks_eager_over_many_updates():
     from rsl_rl.algorithms import PPO
     from rsl_rl.modules import ActorCritic
     torch.manual_seed(0)
-    N, T, O, A = 1024, 8, 48, 12
+    N, T, O, A = 2048, 8, 48, 12  # 8192-row mini-batches: the split-K weight-gradient path
     ac = ActorCritic(O, O, A, [128, 64], [128, 64]).cuda()
     algs = []
     for graph in (True, False):
@@ -265,6 +265,7 @@ def test_ppo_graph_tracks_eager_over_many_updates():
         alg.init_storage(N, T, [O], [None], [A])
         algs.append(alg)
     g = torch.Generator(device="cuda").manual_seed(1)
+    losses = {True: [], False: []}
     for u in range(12):
         obs = [torch.randn(N, O, device="cuda", generator=g) for _ in range(T + 1)]
         act = [torch.randn(N, A, device="cuda", generator=g) for _ in range(T)]
@@ -277,9 +278,15 @@ def test_ppo_graph_tracks_eager_over_many_updates():
                     alg.transition.actions_log_prob = alg.actor_critic.get_actions_log_prob(act[t]).detach()
                     alg.process_env_step(rew[t], torch.zeros(N, device="cuda", dtype=torch.bool), {})
                 alg.compute_returns(obs[T])
-            alg.update()
+            losses[alg.use_graph].append(alg.update())
         pg, pe = (list(a.actor_critic.parameters()) for a in algs)
         assert all(torch.isfinite(p).all() for p in pg), f"graphed update went non-finite at update {u}"
+        # Adam turns rounding-level gradient differences into <= ~lr moves per step
         d = max(float((x - y).abs().max()) for x, y in zip(pg, pe))
-        assert d < 2e-2, f"update {u}: graphed params drifted {d:.3e} from eager"
+        assert d < 2 * 1e-3 * 4 * (u + 1), f"update {u}: graphed params drifted {d:.3e} from eager"
     assert algs[0]._graph is not None
+    # the failure mode seen before the fixes: the graph optimised systematically worse
+    vg, sg = np.array(losses[True]).T
+    ve, se = np.array(losses[False]).T
+    assert abs(vg.mean() - ve.mean()) <= 0.05 * abs(ve.mean()), (vg, ve)
+    assert abs(sg.mean() - se.mean()) <= 0.2 * abs(se.mean()) + 1e-4, (sg, se)

@@ -158,3 +158,21 @@ def test_lstm_export_matches_pretrained_policy(robot, tmp_path):
     ac.memory_a.hidden_states = None
     ys3 = np.stack([ac.act_inference(torch.from_numpy(x[None])).detach().numpy()[0] for x in g["inputs"]])
     np.testing.assert_allclose(ys3, g["outputs"], rtol=1e-5, atol=1e-5)
+
+
+def test_splitk_linear_matches_linear_grads():
+    """SplitKLinear (chunked weight gradient) == nn.Linear on CPU tensors via the same Function."""
+    import torch
+    from rsl_rl.modules import splitk_linear as skl
+    torch.manual_seed(0)
+    x = torch.randn(8192, 48, dtype=torch.float64, requires_grad=True)
+    lin = torch.nn.Linear(48, 32).double()
+    y = skl._SplitKLinearFn.apply(x, lin.weight, lin.bias)
+    g = torch.randn_like(y)
+    dx, dw, db = torch.autograd.grad(y, (x, lin.weight, lin.bias), g)
+    y2 = torch.nn.functional.linear(x, lin.weight, lin.bias)
+    dx2, dw2, db2 = torch.autograd.grad(y2, (x, lin.weight, lin.bias), g)
+    assert torch.allclose(y, y2) and torch.allclose(dx, dx2) and torch.allclose(db, db2)
+    assert torch.allclose(dw, dw2, rtol=1e-10, atol=1e-10)
+    # state_dict keys identical to nn.Linear (checkpoints interchange)
+    assert set(skl.SplitKLinear(48, 32).state_dict()) == set(lin.state_dict())

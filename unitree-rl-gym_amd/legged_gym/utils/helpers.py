@@ -126,8 +126,22 @@ def export_policy_as_jit(actor_critic, path):
         PolicyExporterLSTM(actor_critic).export(path)
         return
     os.makedirs(path, exist_ok=True)
-    model = copy.deepcopy(actor_critic.actor).to("cpu")
+    model = _plain_linear(copy.deepcopy(actor_critic.actor).to("cpu"))
     torch.jit.script(model).save(os.path.join(path, "policy_1.pt"))
+
+
+def _plain_linear(module):
+    """SplitKLinear -> nn.Linear (same parameters) so the exported module scripts
+    to exactly the reference's structure."""
+    from rsl_rl.modules.splitk_linear import SplitKLinear
+    for name, child in module.named_children():
+        if isinstance(child, SplitKLinear):
+            lin = torch.nn.Linear(child.in_features, child.out_features, bias=child.bias is not None)
+            lin.load_state_dict(child.state_dict())
+            setattr(module, name, lin)
+        else:
+            _plain_linear(child)
+    return module
 
 
 class PolicyExporterLSTM(torch.nn.Module):
@@ -136,7 +150,7 @@ class PolicyExporterLSTM(torch.nn.Module):
 
     def __init__(self, actor_critic):
         super().__init__()
-        self.actor = copy.deepcopy(actor_critic.actor)
+        self.actor = _plain_linear(copy.deepcopy(actor_critic.actor))
         self.is_recurrent = actor_critic.is_recurrent
         self.memory = copy.deepcopy(actor_critic.memory_a.rnn)
         self.memory.cpu()

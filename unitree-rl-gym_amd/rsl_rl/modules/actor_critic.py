@@ -2,6 +2,8 @@ import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
+from .splitk_linear import SplitKLinear
+
 
 def get_activation(name):
     table = {"elu": nn.ELU(), "selu": nn.SELU(), "relu": nn.ReLU(), "crelu": nn.ReLU(), "lrelu": nn.LeakyReLU(),
@@ -13,12 +15,12 @@ def get_activation(name):
 
 
 def mlp(in_dim, hidden, out_dim, activation):
-    layers = [nn.Linear(in_dim, hidden[0]), activation]
+    layers = [SplitKLinear(in_dim, hidden[0]), activation]
     for i in range(len(hidden)):
         if i == len(hidden) - 1:
-            layers.append(nn.Linear(hidden[i], out_dim))
+            layers.append(SplitKLinear(hidden[i], out_dim))
         else:
-            layers.append(nn.Linear(hidden[i], hidden[i + 1]))
+            layers.append(SplitKLinear(hidden[i], hidden[i + 1]))
             layers.append(activation)
     return nn.Sequential(*layers)
 
