@@ -189,7 +189,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32 env step; bf16 MFMA policy GEMMs (fp32 accumulate)",
         "data": "synthetic (random-init policy, simulated Go2 on flat ground)",
         "config": {"workload": "Go2 flat terrain, 4096 envs/GPU, MLP actor-critic 512-256-128, PPO 24 steps x 5 epochs x 4 mini-batches",
                    "num_envs_per_gpu": N, "decimation": env_cfg.control.decimation,

@@ -1,0 +1,78 @@
+/*
+ * ppo_mlp.h — C ABI of the hand-written bf16-MFMA kernels behind the rsl_rl
+ * actor-critic MLPs (ActorCritic.act/evaluate in the
+ * rollout and the PPO mini-batch forward/backward).
+ *
+ * The reference runs these as torch nn.Linear/nn.ELU modules (rsl_rl v1.0.2
+ * ActorCritic, called from OnPolicyRunner.learn / PPO.update; call sites
+ * train.py:14, task_registry.py:119).  Here a torch.autograd.Function
+ * (rsl_rl/modules/mfma_mlp.py) drives these entry points per layer; parameters,
+ * losses and the optimizer stay fp32 torch tensors.
+ *
+ * Conventions: every pointer is a DEVICE pointer; matrices are row-major with
+ * the given leading dimension (in elements, a multiple of 8 for bf16 operands,
+ * 16-byte aligned rows); "bf16" is the 16-bit bfloat16 storage type.  Work is
+ * enqueued on `stream` (a hipStream_t; NULL = default stream); nothing
+ * synchronises the host; nothing allocates, so every call is graph-capturable.
+ * Return value: 0, or a negative status with pmlp_last_error() describing it.
+ */
+#ifndef PPO_MLP_H
+#define PPO_MLP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define PMLP_EXTERN extern "C"
+#else
+#define PMLP_EXTERN
+#endif
+#define PMLP_API PMLP_EXTERN __attribute__((visibility("default")))
+
+typedef uint16_t pmlp_bf16;
+
+/* GEMM epilogues.  All GEMMs are C[M,N] = A[M,K] . B[N,K]^T with A and B bf16
+ * and k contiguous (the MFMA operand order).                                 */
+enum {
+    PMLP_EPI_FWD_HIDDEN = 0, /* y = ELU(acc + bias[n]) -> bf16 y[M,N] and y^T[N,M]           */
+    PMLP_EPI_FWD_OUT = 1,    /* out = acc + bias[n]    -> fp32 out[M,N]                      */
+    PMLP_EPI_BWD_DX = 2,     /* dz = acc * ELU'(yprev) -> bf16 dz[M,N] and dz^T[N,M]          */
+    PMLP_EPI_PARTIAL = 3     /* split-K slab s: fp32 slab[s][M,N] over k in [s*ks, (s+1)*ks)  */
+};
+
+PMLP_API const char* pmlp_last_error(void);
+
+/* fp32 x[M,K] (ld ldx) -> bf16 y[M,Kp] (ld ldy) and/or y^T[Kp,M] (ld ldyt);
+ * columns K..Kp-1 of y (rows of y^T) are zero.  y or yt may be NULL.
+ * Replaces the implicit fp32->bf16 casts autocast would insert.            */
+PMLP_API int pmlp_convert(const float* x, int32_t M, int32_t K, int32_t ldx, int32_t Kp, pmlp_bf16* y, int32_t ldy,
+                          pmlp_bf16* yt, int32_t ldyt, void* stream);
+
+/* All weight matrices of one network in one launch: job i converts fp32
+ * w[i] [n[i], k[i]] to bf16 y[i] [n[i], kp[i]] (row-major, zero-padded) and,
+ * when yt[i] != NULL, to yt[i] [k[i], ldyt[i]] (transposed; columns n..ldyt-1
+ * zero).  y / yt may be NULL arrays.                                          */
+#define PMLP_MAX_JOBS 16
+PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const int32_t* n, const int32_t* k,
+                                  const int32_t* kp, pmlp_bf16* const* y, pmlp_bf16* const* yt, const int32_t* ldyt,
+                                  void* stream);
+
+/* C = A . B^T with epilogue `epi` (see enum).  A: [M,K] (lda), B: [N,K] (ldb).
+ *   FWD_HIDDEN: bias[N]; cb[M,N] (ldcb); ct[N,M] (ldct, may be NULL)
+ *   FWD_OUT:    bias[N]; cf[M,N] (ldcf)
+ *   BWD_DX:     yprev[M,N] bf16 (ldyp) = the ELU output the gradient flows through;
+ *               cb/ct as FWD_HIDDEN
+ *   PARTIAL:    cf = slab base, slab s at cf + s*M*ldcf; ksplit = k per slab
+ *               (multiple of 32); number of slabs = ceil(K / ksplit)          */
+PMLP_API int pmlp_gemm(int32_t epi, const pmlp_bf16* A, int32_t lda, const pmlp_bf16* B, int32_t ldb, int32_t M,
+                       int32_t N, int32_t K, const float* bias, const pmlp_bf16* yprev, int32_t ldyp, float* cf,
+                       int32_t ldcf, pmlp_bf16* cb, int32_t ldcb, pmlp_bf16* ct, int32_t ldct, int32_t ksplit,
+                       void* stream);
+
+/* out[i] = sum_s slab[s*slab_stride + i], i < n (fp32): the split-K combine. */
+PMLP_API int pmlp_reduce_slabs(const float* slab, int32_t nslabs, int64_t slab_stride, int64_t n, float* out,
+                               void* stream);
+
+/* out[r] = sum_c x[r*ld + c] for c < cols (bf16 in, fp32 sum): bias gradient
+ * from dz^T rows.                                                           */
+PMLP_API int pmlp_rowsum(const pmlp_bf16* x, int32_t rows, int32_t cols, int32_t ld, float* out, void* stream);
+
+#endif

@@ -290,3 +290,31 @@ def test_ppo_graph_tracks_eager_over_many_updates():
     ve, se = np.array(losses[False]).T
     assert abs(vg.mean() - ve.mean()) <= 0.05 * abs(ve.mean()), (vg, ve)
     assert abs(sg.mean() - se.mean()) <= 0.2 * abs(se.mean()) + 1e-4, (sg, se)
+
+
+@pytest.mark.parametrize("rows", [4096, 24576, 200])
+def test_mfma_mlp_matches_fp32_torch(rows):
+    """bf16-MFMA MLP (csrc/ppo_mlp.hip) vs the same nn.Sequential in fp32 torch:
+    outputs and every parameter gradient within bf16 rounding (relative 2e-2)."""
+    from rsl_rl.modules import mfma_mlp
+    from rsl_rl.modules.actor_critic import mlp, get_activation
+    torch.manual_seed(0)
+    for out_dim, in_dim in ((12, 48), (1, 47)):
+        net = mlp(in_dim, [512, 256, 128], out_dim, get_activation("elu")).cuda()
+        x = torch.randn(rows, in_dim, device="cuda")
+        y_ref = net(x)
+        g = torch.randn_like(y_ref)
+        grads_ref = torch.autograd.grad(y_ref, list(net.parameters()), g)
+        if not mfma_mlp.usable(net, x):
+            assert rows % 8
+            continue
+        y = mfma_mlp.mlp_apply(net, x)
+        grads = torch.autograd.grad(y, list(net.parameters()), g)
+        rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))  # noqa: E731
+        assert rel(y, y_ref) < 2e-2, rel(y, y_ref)
+        for (name, _), a, b in zip(net.named_parameters(), grads, grads_ref):
+            assert a.shape == b.shape, name
+            assert rel(a, b) < 2e-2, (name, rel(a, b))
+        with torch.inference_mode():  # rollout path: no saved activations
+            y2 = mfma_mlp.mlp_apply(net, x)
+        assert torch.equal(y2, y.detach())  # row results independent of train/eval path

@@ -1,0 +1,402 @@
+// ppo_mlp.hip — bf16 MFMA kernels for the actor-critic MLPs (include/ppo_mlp.h).
+//
+// Every GEMM of an MLP layer's forward and backward is written as
+//     C[M,N] = A[M,K] . B[N,K]^T          (A, B bf16, k contiguous)
+// by keeping each activation in BOTH layouts (row-major for the next layer's
+// forward A operand, transposed for the weight gradient's B operand):
+//     forward        y_l   = ELU(x_l W_l^T + b_l)       A = x_l,     B = W_l
+//     input grad     dz_l-1 = (dz_l W_l) * ELU'(x_l)    A = dz_l,    B = W_l^T
+//     weight grad    dW_l  = dz_l^T x_l                 A = dz_l^T,  B = x_l^T
+// The weight gradient reduces over the 24,576-row mini-batch, so it is split
+// over k into fp32 slabs (grid.z) and combined by pmlp_reduce_slabs: every
+// output tile gets ~32-96 workgroups instead of one, and the sum order is fixed
+// (deterministic; no atomics).
+//
+// Tiles: BMxBN per 64*WM*WN-thread block, BK = 64 staged through LDS (row
+// stride 72 bf16 = 144 B keeps the 16-B fragment reads aligned), register
+// prefetch of the next k-tile while the MFMAs of this one run.  Each wave owns
+// a (BM/WM)x(BN/WN) sub-tile of 32x32 v_mfma_f32_32x32x16_bf16 accumulators
+// (operand map: lane l holds row l&31, k = 8(l>>5)..+7; result: column l&31,
+// rows (t&3)+8(t>>2)+4(l>>5), guide §3).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "../../include/ppo_mlp.h"
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& m) {
+    g_err = m;
+    return code;
+}
+#define PMLP_CHECK_LAUNCH(what)                                                                       \
+    do {                                                                                              \
+        hipError_t _e = hipGetLastError();                                                            \
+        if (_e != hipSuccess) return fail(-2, std::string(what) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+struct GemmArgs {
+    const bf16* A;
+    const bf16* B;
+    const float* bias;
+    const bf16* yp;
+    float* cf;
+    bf16* cb;
+    bf16* ct;
+    int lda, ldb, ldyp, ldcf, ldcb, ldct;
+    int M, N, K, ksplit;
+};
+
+__device__ __forceinline__ float elu(float v) { return v > 0.f ? v : expm1f(v); }
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmArgs g) {
+    constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
+    constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 32, FN = TN / 32;
+    constexpr int ACH = BM * BK / 8, BCH = BN * BK / 8;  // 16-byte chunks per tile
+    constexpr int AL = (ACH + NT - 1) / NT, BL = (BCH + NT - 1) / NT;
+    static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
+    constexpr int CS = BN + 8;  // epilogue tile row stride (bf16)
+    constexpr int STAGE = (BM + BN) * LS, CTILE = BM * CS;
+    __shared__ __attribute__((aligned(16))) bf16 smem[STAGE > CTILE ? STAGE : CTILE];
+    bf16* As = smem;
+    bf16* Bs = smem + BM * LS;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int kb = 0, ke = g.K;
+    if (EPI == PMLP_EPI_PARTIAL) {
+        kb = blockIdx.z * g.ksplit;
+        ke = min(g.K, kb + g.ksplit);
+    }
+    floatx16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) acc[i][j][t] = 0.f;
+
+    uint4 ra[AL], rb[BL];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int c = tid + i * NT;
+            const int r = c / CPR, kc = (c % CPR) * 8;
+            const int gr = m0 + r, gk = k0 + kc;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (c < ACH && gr < g.M && gk < ke) v = *(const uint4*)(g.A + (size_t)gr * g.lda + gk);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int c = tid + i * NT;
+            const int r = c / CPR, kc = (c % CPR) * 8;
+            const int gr = n0 + r, gk = k0 + kc;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (c < BCH && gr < g.N && gk < ke) v = *(const uint4*)(g.B + (size_t)gr * g.ldb + gk);
+            rb[i] = v;
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int c = tid + i * NT;
+            if (c < ACH) *(uint4*)(As + (c / CPR) * LS + (c % CPR) * 8) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int c = tid + i * NT;
+            if (c < BCH) *(uint4*)(Bs + (c / CPR) * LS + (c % CPR) * 8) = rb[i];
+        }
+    };
+
+    gload(kb);
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (k0 + BK < ke) gload(k0 + BK);
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            bf16x8 af[FM], bfr[FN];
+            const int ko = s * 16 + (lane >> 5) * 8;
+#pragma unroll
+            for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(As + (wm * TM + i * 32 + (lane & 31)) * LS + ko);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * TN + j * 32 + (lane & 31)) * LS + ko);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // ---- epilogue: lane owns column (lane&31), rows (t&3)+8(t>>2)+4(lane>>5)
+    if (EPI == PMLP_EPI_FWD_HIDDEN || EPI == PMLP_EPI_BWD_DX) __syncthreads();  // LDS reuse
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + wn * TN + j * 32 + (lane & 31);
+            const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
+            if (col >= g.N && (EPI == PMLP_EPI_PARTIAL || EPI == PMLP_EPI_FWD_OUT)) continue;
+            if (EPI == PMLP_EPI_PARTIAL) {
+                float* slab = g.cf + (size_t)blockIdx.z * g.M * g.ldcf;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int row = rbase + (t & 3) + 8 * (t >> 2);
+                    if (row < g.M) slab[(size_t)row * g.ldcf + col] = acc[i][j][t];
+                }
+            } else if (EPI == PMLP_EPI_FWD_OUT) {
+                const float b = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int row = rbase + (t & 3) + 8 * (t >> 2);
+                    if (row < g.M) g.cf[(size_t)row * g.ldcf + col] = acc[i][j][t] + b;
+                }
+            } else {
+                // bf16 result into the LDS tile; stored below in both layouts
+                const float b = (EPI == PMLP_EPI_FWD_HIDDEN && g.bias && col < g.N) ? g.bias[col] : 0.f;
+                const int lc = wn * TN + j * 32 + (lane & 31);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int lr = wm * TM + i * 32 + 4 * (lane >> 5) + (t & 3) + 8 * (t >> 2);
+                    const int row = m0 + lr;
+                    float v = acc[i][j][t];
+                    if (EPI == PMLP_EPI_FWD_HIDDEN) {
+                        v = elu(v + b);
+                    } else {  // BWD_DX: d/dx ELU from its output y: 1 (y>0) or y+1
+                        const float y = (row < g.M && col < g.N) ? (float)g.yp[(size_t)row * g.ldyp + col] : 0.f;
+                        v = y > 0.f ? v : v * (y + 1.f);
+                    }
+                    smem[lr * CS + lc] = (bf16)v;
+                }
+            }
+        }
+    }
+    if (EPI == PMLP_EPI_FWD_HIDDEN || EPI == PMLP_EPI_BWD_DX) {
+        __syncthreads();  // the tile is written by every wave
+        // row-major: 16-byte chunks along n; transposed: 16-byte chunks along m
+        constexpr int RCH = BM * BN / 8;
+        for (int c = tid; c < RCH; c += NT) {
+            const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
+            const int row = m0 + lr, col = n0 + lc;
+            if (row >= g.M || col >= g.N) continue;
+            const bf16* src = smem + lr * CS + lc;
+            if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
+                *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
+            } else {
+                for (int u = 0; u < 8 && col + u < g.N; ++u) g.cb[(size_t)row * g.ldcb + col + u] = src[u];
+            }
+        }
+        if (g.ct) {
+            for (int c = tid; c < RCH; c += NT) {
+                const int lc = c / (BM / 8), lr = (c % (BM / 8)) * 8;
+                const int col = n0 + lc, row = m0 + lr;
+                if (col >= g.N || row >= g.M) continue;
+                bf16x8 v;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = smem[(lr + u) * CS + lc];
+                if (row + 8 <= g.M && (g.ldct % 8) == 0) {
+                    *(bf16x8*)(g.ct + (size_t)col * g.ldct + row) = v;
+                } else {
+                    for (int u = 0; u < 8 && row + u < g.M; ++u) g.ct[(size_t)col * g.ldct + row + u] = v[u];
+                }
+            }
+        }
+    }
+}
+
+// fp32 [M,K] -> bf16 [M,Kp] and/or [Kp,M], 64x64 tiles through LDS.
+__global__ __launch_bounds__(256) void k_convert(const float* __restrict__ x, int M, int K, int ldx, int Kp,
+                                                 bf16* __restrict__ y, int ldy, bf16* __restrict__ yt, int ldyt) {
+    __shared__ float tile[64][65];
+    const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (int r = ty; r < 64; r += 4) {
+        const int m = m0 + r, k = k0 + tx;
+        float v = 0.f;
+        if (m < M && k < K) v = x[(size_t)m * ldx + k];
+        tile[r][tx] = v;
+        if (y && m < M && k < Kp) y[(size_t)m * ldy + k] = (bf16)v;
+    }
+    if (!yt) return;
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {  // row k0+c of y^T, columns m0..m0+63
+        const int k = k0 + c, m = m0 + tx;
+        if (k < Kp && m < M) yt[(size_t)k * ldyt + m] = (bf16)tile[tx][c];
+    }
+}
+
+__global__ void k_reduce_slabs(const float* __restrict__ slab, int S, int64_t stride, int64_t n,
+                               float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += slab[(size_t)k * stride + i];
+    out[i] = s;
+}
+
+__global__ __launch_bounds__(256) void k_rowsum(const bf16* __restrict__ x, int cols, int ld, float* __restrict__ out) {
+    __shared__ float part[4];
+    const int r = blockIdx.x, tid = threadIdx.x;
+    const bf16* row = x + (size_t)r * ld;
+    float s = 0.f;
+    const int full = cols / 8;
+    for (int c = tid; c < full; c += 256) {
+        bf16x8 v = *(const bf16x8*)(row + 8 * c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += (float)v[u];
+    }
+    for (int u = 8 * full + tid; u < cols; u += 256) s += (float)row[u];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((tid & 63) == 0) part[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) out[r] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// Several fp32 weight matrices W[N,K] -> bf16 W[N,Kp] (row-major) and W^T[K,ld]
+// in one launch (blockIdx.z = job); 64x64 tiles through LDS.
+struct CvtJob {
+    const float* w;
+    bf16* y;
+    bf16* yt;
+    int N, K, Kp, ldyt;
+};
+struct CvtJobs {
+    CvtJob j[PMLP_MAX_JOBS];
+};
+__global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
+    const CvtJob J = jobs.j[blockIdx.z];
+    const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+    if (m0 >= J.N || k0 >= J.Kp) return;
+    __shared__ float tile[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int m = m0 + r, k = k0 + tx;
+        float v = 0.f;
+        if (m < J.N && k < J.K) v = J.w[(size_t)m * J.K + k];
+        tile[r][tx] = v;
+        if (J.y && m < J.N && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v;
+    }
+    if (!J.yt) return;
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {
+        const int k = k0 + c, m = m0 + tx;
+        if (k < J.K && m < J.ldyt) J.yt[(size_t)k * J.ldyt + m] = (bf16)(m < J.N ? tile[tx][c] : 0.f);
+    }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void launch(int epi, const GemmArgs& g, int slabs, hipStream_t st) {
+    dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, slabs), block(64 * WM * WN);
+    switch (epi) {
+    case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, g); break;
+    case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, g); break;
+    case PMLP_EPI_BWD_DX: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, g); break;
+    default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, g); break;
+    }
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" {
+
+PMLP_API const char* pmlp_last_error(void) { return g_err.c_str(); }
+
+PMLP_API int pmlp_convert(const float* x, int32_t M, int32_t K, int32_t ldx, int32_t Kp, pmlp_bf16* y, int32_t ldy,
+                          pmlp_bf16* yt, int32_t ldyt, void* stream) {
+    if (!x || M <= 0 || K <= 0 || Kp < K || ldx < K || (y && ldy < Kp) || (yt && ldyt < M))
+        return fail(-1, "pmlp_convert: bad arguments");
+    dim3 grid((M + 63) / 64, (Kp + 63) / 64);
+    hipLaunchKernelGGL(k_convert, grid, dim3(256), 0, (hipStream_t)stream, x, M, K, ldx, Kp, (bf16*)y, ldy, (bf16*)yt,
+                       ldyt);
+    PMLP_CHECK_LAUNCH("pmlp_convert");
+    return 0;
+}
+
+PMLP_API int pmlp_gemm(int32_t epi, const pmlp_bf16* A, int32_t lda, const pmlp_bf16* B, int32_t ldb, int32_t M,
+                       int32_t N, int32_t K, const float* bias, const pmlp_bf16* yprev, int32_t ldyp, float* cf,
+                       int32_t ldcf, pmlp_bf16* cb, int32_t ldcb, pmlp_bf16* ct, int32_t ldct, int32_t ksplit,
+                       void* stream) {
+    if (epi < 0 || epi > 3) return fail(-1, "pmlp_gemm: unknown epilogue");
+    if (!A || !B || M <= 0 || N <= 0 || K <= 0) return fail(-1, "pmlp_gemm: null operand or empty shape");
+    if (K % 8 || lda % 8 || ldb % 8 || lda < K || ldb < K || !al16(A) || !al16(B))
+        return fail(-1, "pmlp_gemm: K, lda, ldb must be multiples of 8 with 16-byte aligned operands");
+    if ((epi == PMLP_EPI_FWD_OUT || epi == PMLP_EPI_PARTIAL) && (!cf || ldcf < N))
+        return fail(-1, "pmlp_gemm: fp32 output missing or ldcf < N");
+    if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) && (!cb || ldcb < N || (ct && (ldct < M || ldct % 4))))
+        return fail(-1, "pmlp_gemm: bf16 output missing or bad leading dimension");
+    if (epi == PMLP_EPI_BWD_DX && (!yprev || ldyp < N)) return fail(-1, "pmlp_gemm: BWD_DX needs yprev");
+    int slabs = 1;
+    if (epi == PMLP_EPI_PARTIAL) {
+        if (ksplit <= 0 || ksplit % 32) return fail(-1, "pmlp_gemm: ksplit must be a positive multiple of 32");
+        slabs = (K + ksplit - 1) / ksplit;
+    }
+    GemmArgs g;
+    g.A = (const bf16*)A; g.B = (const bf16*)B; g.bias = bias; g.yp = (const bf16*)yprev;
+    g.cf = cf; g.cb = (bf16*)cb; g.ct = (bf16*)ct;
+    g.lda = lda; g.ldb = ldb; g.ldyp = ldyp; g.ldcf = ldcf; g.ldcb = ldcb; g.ldct = ldct;
+    g.M = M; g.N = N; g.K = K; g.ksplit = ksplit;
+    hipStream_t st = (hipStream_t)stream;
+    if (M <= 32) launch<32, 128, 1, 4>(epi, g, slabs, st);
+    else if (N <= 32) launch<128, 32, 4, 1>(epi, g, slabs, st);
+    else if (N <= 64) launch<128, 64, 4, 1>(epi, g, slabs, st);
+    else launch<128, 128, 2, 2>(epi, g, slabs, st);
+    PMLP_CHECK_LAUNCH("pmlp_gemm");
+    return 0;
+}
+
+PMLP_API int pmlp_reduce_slabs(const float* slab, int32_t nslabs, int64_t slab_stride, int64_t n, float* out,
+                               void* stream) {
+    if (!slab || !out || nslabs <= 0 || n <= 0 || slab_stride < n) return fail(-1, "pmlp_reduce_slabs: bad arguments");
+    const int bs = 256;
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, (hipStream_t)stream, slab,
+                       nslabs, slab_stride, n, out);
+    PMLP_CHECK_LAUNCH("pmlp_reduce_slabs");
+    return 0;
+}
+
+PMLP_API int pmlp_rowsum(const pmlp_bf16* x, int32_t rows, int32_t cols, int32_t ld, float* out, void* stream) {
+    if (!x || !out || rows <= 0 || cols <= 0 || ld < cols || ld % 8 || !al16(x))
+        return fail(-1, "pmlp_rowsum: bad arguments");
+    hipLaunchKernelGGL(k_rowsum, dim3(rows), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, cols, ld, out);
+    PMLP_CHECK_LAUNCH("pmlp_rowsum");
+    return 0;
+}
+
+PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const int32_t* n, const int32_t* k,
+                                  const int32_t* kp, pmlp_bf16* const* y, pmlp_bf16* const* yt, const int32_t* ldyt,
+                                  void* stream) {
+    if (njobs <= 0 || njobs > PMLP_MAX_JOBS) return fail(-1, "pmlp_convert_weights: 1..PMLP_MAX_JOBS jobs");
+    CvtJobs jobs{};
+    int maxn = 0, maxk = 0;
+    for (int i = 0; i < njobs; ++i) {
+        if (!w[i] || n[i] <= 0 || k[i] <= 0 || kp[i] < k[i] || (yt && yt[i] && ldyt[i] < n[i]))
+            return fail(-1, "pmlp_convert_weights: bad job " + std::to_string(i));
+        jobs.j[i] = CvtJob{w[i], (bf16*)(y ? y[i] : nullptr), (bf16*)(yt ? yt[i] : nullptr), n[i], k[i], kp[i],
+                           yt && yt[i] ? ldyt[i] : 0};
+        maxn = std::max(maxn, std::max(n[i], yt && yt[i] ? ldyt[i] : 0));
+        maxk = std::max(maxk, kp[i]);
+    }
+    dim3 grid((maxn + 63) / 64, (maxk + 63) / 64, njobs);
+    hipLaunchKernelGGL(k_convert_jobs, grid, dim3(256), 0, (hipStream_t)stream, jobs);
+    PMLP_CHECK_LAUNCH("pmlp_convert_weights");
+    return 0;
+}
+
+}  // extern "C"

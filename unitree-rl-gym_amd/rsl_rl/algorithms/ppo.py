@@ -64,9 +64,9 @@ class PPO:
         self.use_clipped_value_loss = use_clipped_value_loss
         self.world_size = _dist_world()
         # whole-update HIP graph (MLP policies on a GPU): set use_graph=False to disable
-        # (fp32 only: bf16 autocast GEMMs inside a captured graph drift, see ActorCritic)
+        # (library bf16 GEMMs under autocast drift inside a captured graph on this ROCm;
+        #  the MFMA MLP kernels are deterministic and capture cleanly)
         self.use_graph = on_gpu and not getattr(self.actor_critic, "is_recurrent", False) and \
-            not getattr(self.actor_critic, "mixed_precision", False) and \
             self.optimizer.defaults.get("capturable", False) and \
             (self.world_size == 1 or dist.get_backend() == "nccl")
         self._graph = None

@@ -2,6 +2,7 @@ import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
+from . import mfma_mlp
 from .splitk_linear import SplitKLinear
 
 
@@ -28,16 +29,15 @@ def mlp(in_dim, hidden, out_dim, activation):
 class ActorCritic(nn.Module):
     """Gaussian MLP actor + MLP critic (rsl_rl v1.0.2 ActorCritic).
 
-    fp32 throughout by default (the reference's precision).  ``mixed_precision=True``
-    runs the Linear layers under bf16 autocast for eager use only: captured into
-    the PPO update graph, the bf16 library GEMMs drift from their eager results
-    on this ROCm (tools/probes/graph_ppo_like.py NEWDATA=1), so PPO disables its
-    graph when mixed precision is on.
+    ``mixed_precision=True`` (default) runs both MLPs' forward and backward on the
+    hand-written bf16 MFMA kernels (modules/mfma_mlp.py, csrc/ppo_mlp.hip): bf16
+    operands, fp32 accumulation, fp32 parameters, gradients, distribution and
+    losses.  ``False`` is plain fp32 torch (the reference's arithmetic).
     """
     is_recurrent = False
 
     def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=[256, 256, 256],
-                 critic_hidden_dims=[256, 256, 256], activation="elu", init_noise_std=1.0, mixed_precision=False,
+                 critic_hidden_dims=[256, 256, 256], activation="elu", init_noise_std=1.0, mixed_precision=True,
                  **kwargs):
         if kwargs:
             print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str([k for k in kwargs]))
@@ -52,10 +52,8 @@ class ActorCritic(nn.Module):
         self.mixed_precision = mixed_precision
 
     def _run(self, net, x):
-        if self.mixed_precision and x.is_cuda:
-            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
-                y = net(x)
-            return y.float()
+        if self.mixed_precision and mfma_mlp.usable(net, x):
+            return mfma_mlp.mlp_apply(net, x)  # hand-written bf16 MFMA forward/backward
         return net(x)
 
     @staticmethod
