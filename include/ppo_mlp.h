@@ -24,6 +24,26 @@
 #define PMLP_EXTERN extern "C"
 #else
 #define PMLP_EXTERN
+/* Fused PPO loss of rsl_rl v1.0.2 PPO.update for a diagonal Gaussian policy
+ * (ratio, clipped surrogate, optionally clipped value loss, entropy bonus,
+ * and the KL the adaptive learning rate reads).  Inputs fp32, row-major:
+ * mu/actions/old_mu/old_sigma [M,A], stdv [A], value/old_logp/adv/ret/target [M].
+ * fwd: loss[1]; stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean};
+ *      partial = scratch of 4*pmlp_ppo_loss_blocks(M) floats.
+ * bwd: gout = device scalar d(total)/d(loss); dmu [M,A], dvalue [M], dstd [A];
+ *      partial_std = scratch of A*pmlp_ppo_loss_blocks(M) floats.          */
+PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M);
+PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
+                               float* stats, void* stream);
+PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
+                               float* dvalue, float* partial_std, float* dstd, void* stream);
+
 #endif
 #define PMLP_API PMLP_EXTERN __attribute__((visibility("default")))
 
@@ -74,5 +94,25 @@ PMLP_API int pmlp_reduce_slabs(const float* slab, int32_t nslabs, int64_t slab_s
 /* out[r] = sum_c x[r*ld + c] for c < cols (bf16 in, fp32 sum): bias gradient
  * from dz^T rows.                                                           */
 PMLP_API int pmlp_rowsum(const pmlp_bf16* x, int32_t rows, int32_t cols, int32_t ld, float* out, void* stream);
+
+/* Fused PPO loss of rsl_rl v1.0.2 PPO.update for a diagonal Gaussian policy
+ * (ratio, clipped surrogate, optionally clipped value loss, entropy bonus,
+ * and the KL the adaptive learning rate reads).  Inputs fp32, row-major:
+ * mu/actions/old_mu/old_sigma [M,A], stdv [A], value/old_logp/adv/ret/target [M].
+ * fwd: loss[1]; stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean};
+ *      partial = scratch of 4*pmlp_ppo_loss_blocks(M) floats.
+ * bwd: gout = device scalar d(total)/d(loss); dmu [M,A], dvalue [M], dstd [A];
+ *      partial_std = scratch of A*pmlp_ppo_loss_blocks(M) floats.          */
+PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M);
+PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
+                               float* stats, void* stream);
+PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
+                               float* dvalue, float* partial_std, float* dstd, void* stream);
 
 #endif

@@ -318,3 +318,49 @@ def test_mfma_mlp_matches_fp32_torch(rows):
         with torch.inference_mode():  # rollout path: no saved activations
             y2 = mfma_mlp.mlp_apply(net, x)
         assert torch.equal(y2, y.detach())  # row results independent of train/eval path
+
+
+@pytest.mark.parametrize("clipped", [True, False])
+def test_fused_ppo_loss_matches_reference_loss(clipped):
+    """mfma_mlp.ppo_loss (fused kernels) vs rsl_rl's torch statement of the loss:
+    value, statistics, KL and the gradients w.r.t. mean, std and value."""
+    from torch.distributions import Normal
+    from rsl_rl.modules import mfma_mlp
+    torch.manual_seed(0)
+    M, A, clip, vcoef, ecoef = 24576, 12, 0.2, 1.0, 0.01
+    mu = torch.randn(M, A, device="cuda", requires_grad=True)
+    std = (0.5 + torch.rand(A, device="cuda")).requires_grad_()
+    value = torch.randn(M, 1, device="cuda", requires_grad=True)
+    actions = mu.detach() + 0.3 * torch.randn(M, A, device="cuda")
+    old_mu = mu.detach() + 0.05 * torch.randn(M, A, device="cuda")
+    old_sigma = (std.detach() * (1 + 0.1 * torch.rand(M, A, device="cuda")))
+    old_logp = Normal(old_mu, old_sigma).log_prob(actions).sum(-1, keepdim=True)
+    adv, ret = torch.randn(M, 1, device="cuda"), torch.randn(M, 1, device="cuda")
+    target = value.detach() + 0.3 * torch.randn(M, 1, device="cuda")  # some rows clip, some do not
+
+    # torch statement (rsl_rl v1.0.2 PPO.update)
+    d = Normal(mu, mu * 0.0 + std)
+    ratio = torch.exp(d.log_prob(actions).sum(-1) - torch.squeeze(old_logp))
+    s1 = -torch.squeeze(adv) * ratio
+    s2 = -torch.squeeze(adv) * torch.clamp(ratio, 1 - clip, 1 + clip)
+    surr = torch.max(s1, s2).mean()
+    if clipped:
+        vc = target + (value - target).clamp(-clip, clip)
+        vl = torch.max((value - ret).pow(2), (vc - ret).pow(2)).mean()
+    else:
+        vl = (ret - value).pow(2).mean()
+    loss_ref = surr + vcoef * vl - ecoef * d.entropy().sum(-1).mean()
+    sig = mu.detach() * 0 + std.detach()
+    kl_ref = torch.sum(torch.log(sig / old_sigma + 1.0e-5) + (old_sigma ** 2 + (old_mu - mu.detach()) ** 2)
+                       / (2.0 * sig ** 2) - 0.5, axis=-1).mean()
+    g_ref = torch.autograd.grad(loss_ref, (mu, std, value))
+
+    loss, stats = mfma_mlp.ppo_loss(mu, std, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, clip,
+                                    clipped, vcoef, ecoef)
+    g = torch.autograd.grad(loss, (mu, std, value))
+    close = lambda a, b, tol: abs(float(a) - float(b)) <= tol * (abs(float(b)) + 1e-6)  # noqa: E731
+    assert close(loss, loss_ref, 1e-4) and close(stats[0], surr, 1e-4) and close(stats[1], vl, 1e-4)
+    assert close(stats[2], kl_ref, 1e-4)
+    for a, b in zip(g, g_ref):
+        assert a.shape == b.shape
+        assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-4

@@ -301,6 +301,161 @@ __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
     }
 }
 
+
+// ---------------------------------------------------------------- PPO loss --
+// rsl_rl v1.0.2 PPO.update loss for a diagonal Gaussian policy, one row per
+// thread, forward and backward fused (see ppo.py _minibatch_step for the torch
+// statement it replaces).  Reductions: per-block partials, then one block sums
+// them in a fixed order (deterministic).
+#define PMLP_LOSS_THREADS 256
+struct LossArgs {
+    const float *mu, *stdv, *value, *actions, *old_logp, *old_mu, *old_sigma, *adv, *ret, *target;
+    int M, A, clipped_value;
+    float clip, vcoef, ecoef;
+};
+static constexpr float kHalfLog2Pi = 0.91893853320467274f;  // log(sqrt(2 pi))
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_fwd(LossArgs a, float* __restrict__ partial) {
+    __shared__ float sh[4];
+    const int i = blockIdx.x * PMLP_LOSS_THREADS + threadIdx.x;
+    float surr = 0.f, vl = 0.f, kl = 0.f;
+    if (i < a.M) {
+        float logp = 0.f;
+        for (int k = 0; k < a.A; ++k) {
+            const float sg = a.stdv[k], mu = a.mu[(size_t)i * a.A + k];
+            const float d = a.actions[(size_t)i * a.A + k] - mu;
+            logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
+            const float os = a.old_sigma[(size_t)i * a.A + k], om = a.old_mu[(size_t)i * a.A + k] - mu;
+            kl += logf(sg / os + 1.0e-5f) + (os * os + om * om) / (2.f * sg * sg) - 0.5f;
+        }
+        const float ratio = expf(logp - a.old_logp[i]);
+        const float adv = a.adv[i];
+        const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip);
+        surr = fmaxf(s1, s2);
+        const float v = a.value[i], r = a.ret[i];
+        if (a.clipped_value) {
+            const float t = a.target[i];
+            const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
+            vl = fmaxf((v - r) * (v - r), (vc - r) * (vc - r));
+        } else {
+            vl = (r - v) * (r - v);
+        }
+    }
+    surr = block_sum(surr, sh);
+    vl = block_sum(vl, sh);
+    kl = block_sum(kl, sh);
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x * 4 + 0] = surr;
+        partial[blockIdx.x * 4 + 1] = vl;
+        partial[blockIdx.x * 4 + 2] = kl;
+    }
+}
+
+// loss[0]; stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]
+__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_final(LossArgs a, const float* __restrict__ partial,
+                                                                      int nblocks, float* __restrict__ loss,
+                                                                      float* __restrict__ stats) {
+    __shared__ float sh[4];
+    float s[3] = {0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < nblocks; b += PMLP_LOSS_THREADS)
+        for (int k = 0; k < 3; ++k) s[k] += partial[b * 4 + k];
+    for (int k = 0; k < 3; ++k) s[k] = block_sum(s[k], sh);
+    if (threadIdx.x == 0) {
+        float ent = 0.f;
+        for (int k = 0; k < a.A; ++k) ent += 0.5f + kHalfLog2Pi + logf(a.stdv[k]);
+        const float inv = 1.f / (float)a.M;
+        const float surr = s[0] * inv, vl = s[1] * inv;
+        loss[0] = surr + a.vcoef * vl - a.ecoef * ent;
+        stats[0] = surr;
+        stats[1] = vl;
+        stats[2] = s[2] * inv;
+        stats[3] = ent;
+    }
+}
+
+// torch.maximum backward: the larger input takes the gradient, ties split it
+__device__ __forceinline__ void max_weights(float x, float y, float& wx, float& wy) {
+    wx = x > y ? 1.f : (x == y ? 0.5f : 0.f);
+    wy = y > x ? 1.f : (x == y ? 0.5f : 0.f);
+}
+
+__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_bwd(LossArgs a, const float* __restrict__ gout,
+                                                                    float* __restrict__ dmu, float* __restrict__ dvalue,
+                                                                    float* __restrict__ partial_std) {
+    __shared__ float sh[4];
+    const int i = blockIdx.x * PMLP_LOSS_THREADS + threadIdx.x;
+    const float g = gout[0];
+    const float gs = g / (float)a.M, gv = g * a.vcoef / (float)a.M;
+    float dlogp = 0.f;
+    if (i < a.M) {
+        float logp = 0.f;
+        for (int k = 0; k < a.A; ++k) {
+            const float sg = a.stdv[k];
+            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
+        }
+        const float ratio = expf(logp - a.old_logp[i]);
+        const float adv = a.adv[i];
+        const float lo = 1.f - a.clip, hi = 1.f + a.clip;
+        const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, lo), hi);
+        float w1, w2;
+        max_weights(s1, s2, w1, w2);
+        const float dclamp = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        dlogp = gs * (-adv) * (w1 + w2 * dclamp) * ratio;
+        for (int k = 0; k < a.A; ++k) {
+            const float sg = a.stdv[k];
+            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            dmu[(size_t)i * a.A + k] = dlogp * d / (sg * sg);
+        }
+        const float v = a.value[i], r = a.ret[i];
+        float dv;
+        if (a.clipped_value) {
+            const float t = a.target[i];
+            const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
+            float u1, u2;
+            max_weights((v - r) * (v - r), (vc - r) * (vc - r), u1, u2);
+            const float dcv = (v - t >= -a.clip && v - t <= a.clip) ? 1.f : 0.f;
+            dv = gv * (u1 * 2.f * (v - r) + u2 * 2.f * (vc - r) * dcv);
+        } else {
+            dv = gv * 2.f * (v - r);
+        }
+        dvalue[i] = dv;
+    }
+    // d logp / d sigma_k summed over the block's rows
+    for (int k = 0; k < a.A; ++k) {
+        float c = 0.f;
+        if (i < a.M) {
+            const float sg = a.stdv[k];
+            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            c = dlogp * (d * d / (sg * sg * sg) - 1.f / sg);
+        }
+        c = block_sum(c, sh);
+        if (threadIdx.x == 0) partial_std[(size_t)blockIdx.x * a.A + k] = c;
+    }
+}
+
+__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_std(LossArgs a, const float* __restrict__ gout,
+                                                                    const float* __restrict__ partial_std, int nblocks,
+                                                                    float* __restrict__ dstd) {
+    __shared__ float sh[4];
+    for (int k = 0; k < a.A; ++k) {
+        float c = 0.f;
+        for (int b = threadIdx.x; b < nblocks; b += PMLP_LOSS_THREADS) c += partial_std[(size_t)b * a.A + k];
+        c = block_sum(c, sh);
+        if (threadIdx.x == 0) dstd[k] = c - a.ecoef * gout[0] / a.stdv[k];  // + entropy term
+    }
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch(int epi, const GemmArgs& g, int slabs, hipStream_t st) {
     dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, slabs), block(64 * WM * WN);
@@ -396,6 +551,57 @@ PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const in
     dim3 grid((maxn + 63) / 64, (maxk + 63) / 64, njobs);
     hipLaunchKernelGGL(k_convert_jobs, grid, dim3(256), 0, (hipStream_t)stream, jobs);
     PMLP_CHECK_LAUNCH("pmlp_convert_weights");
+    return 0;
+}
+
+static int loss_args(LossArgs& a, const float* mu, const float* stdv, const float* value, const float* actions,
+                     const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                     const float* ret, const float* target, int32_t M, int32_t A, float clip, int32_t clipped_value,
+                     float vcoef, float ecoef) {
+    if (!mu || !stdv || !value || !actions || !old_logp || !old_mu || !old_sigma || !adv || !ret ||
+        (clipped_value && !target) || M <= 0 || A <= 0)
+        return fail(-1, "pmlp_ppo_loss: null input or empty batch");
+    a = LossArgs{mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clipped_value,
+                 clip, vcoef, ecoef};
+    return 0;
+}
+
+PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M) { return (M + PMLP_LOSS_THREADS - 1) / PMLP_LOSS_THREADS; }
+
+PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
+                               float* stats, void* stream) {
+    LossArgs a;
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clip,
+                          clipped_value, vcoef, ecoef))
+        return e;
+    if (!partial || !loss || !stats) return fail(-1, "pmlp_ppo_loss_fwd: null output");
+    const int nb = pmlp_ppo_loss_blocks(M);
+    hipLaunchKernelGGL(k_ppo_loss_fwd, dim3(nb), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, partial);
+    hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, partial, nb,
+                       loss, stats);
+    PMLP_CHECK_LAUNCH("pmlp_ppo_loss_fwd");
+    return 0;
+}
+
+PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
+                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
+                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
+                               float* dvalue, float* partial_std, float* dstd, void* stream) {
+    LossArgs a;
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clip,
+                          clipped_value, vcoef, ecoef))
+        return e;
+    if (!gout || !dmu || !dvalue || !partial_std || !dstd) return fail(-1, "pmlp_ppo_loss_bwd: null output");
+    const int nb = pmlp_ppo_loss_blocks(M);
+    hipLaunchKernelGGL(k_ppo_loss_bwd, dim3(nb), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, gout, dmu, dvalue,
+                       partial_std);
+    hipLaunchKernelGGL(k_ppo_loss_std, dim3(1), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, gout,
+                       partial_std, nb, dstd);
+    PMLP_CHECK_LAUNCH("pmlp_ppo_loss_bwd");
     return 0;
 }
 

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.optim as optim
 
 from rsl_rl.modules import ActorCritic
+from rsl_rl.modules import mfma_mlp
 from rsl_rl.storage import RolloutStorage
 
 
@@ -31,7 +32,7 @@ class PPO:
 
     def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998, lam=0.95,
                  value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
-                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu", fused_loss=True):
         self.device = device
         self.desired_kl = desired_kl
         self.schedule = schedule
@@ -70,6 +71,9 @@ class PPO:
             self.optimizer.defaults.get("capturable", False) and \
             (self.world_size == 1 or dist.get_backend() == "nccl")
         self._graph = None
+        # fused PPO-loss kernels for the Gaussian MLP policy on a GPU (fused_loss=False:
+        # the torch statement of the loss, _reference_loss)
+        self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "policy_mean")
         self._diag, self._diag_i = None, 0
         self._graph_calls = 0
         self._capturing = False
@@ -145,10 +149,10 @@ class PPO:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
-    def _minibatch_step(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+    def _reference_loss(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
                         returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
-                        masks_batch, acc):
-        """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
+                        masks_batch):
+        """The loss exactly as rsl_rl v1.0.2 PPO.update states it (torch ops)."""
         if self.actor_critic.is_recurrent:
             self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
         else:  # v1.0.2 calls act() here and discards the sample; only the distribution is used
@@ -164,18 +168,7 @@ class PPO:
                 kl = torch.sum(torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
                                + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
                                / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
-                kl_mean = torch.mean(kl)
-                if self.world_size > 1:
-                    dist.all_reduce(kl_mean)
-                    kl_mean = kl_mean / self.world_size
-                lr = self._lr
-                new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
-                                     torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
-                                                 torch.clamp(lr * 1.5, max=1e-2), lr))
-                self._lr.copy_(new_lr)
-            if not self._lr_is_tensor:
-                for g in self.optimizer.param_groups:
-                    g["lr"] = float(self._lr)
+                self._adapt_lr(torch.mean(kl))
 
         ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
         surrogate = -torch.squeeze(advantages_batch) * ratio
@@ -191,10 +184,47 @@ class PPO:
         else:
             value_loss = (returns_batch - value_batch).pow(2).mean()
         loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+        return loss, surrogate_loss, value_loss
 
-        # inside a captured graph the grads are static buffers (set_to_none=False):
-        # no graph-pool tensor may escape the capture
-        self.optimizer.zero_grad(set_to_none=not self._capturing)
+    def _adapt_lr(self, kl_mean):
+        """KL-adaptive learning rate (rsl_rl v1.0.2), on device: no host sync."""
+        with torch.no_grad():
+            if self.world_size > 1:
+                dist.all_reduce(kl_mean)
+                kl_mean = kl_mean / self.world_size
+            lr = self._lr
+            new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
+                                 torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
+                                             torch.clamp(lr * 1.5, max=1e-2), lr))
+            self._lr.copy_(new_lr)
+        if not self._lr_is_tensor:
+            for g in self.optimizer.param_groups:
+                g["lr"] = float(self._lr)
+
+    def _minibatch_step(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+                        returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
+                        masks_batch, acc):
+        """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
+        if self._fused_loss and not self.actor_critic.is_recurrent:
+            # same loss, two fused kernels forward + two backward (modules/mfma_mlp.ppo_loss)
+            mu_batch = self.actor_critic.policy_mean(obs_batch)
+            value_batch = self.actor_critic.evaluate(critic_obs_batch)
+            loss, stats = mfma_mlp.ppo_loss(mu_batch, self.actor_critic.std, value_batch, actions_batch,
+                                            old_actions_log_prob_batch, old_mu_batch, old_sigma_batch,
+                                            advantages_batch, returns_batch, target_values_batch, self.clip_param,
+                                            self.use_clipped_value_loss, self.value_loss_coef, self.entropy_coef)
+            surrogate_loss, value_loss = stats[0], stats[1]
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                self._adapt_lr(stats[2])
+        else:
+            loss, surrogate_loss, value_loss = self._reference_loss(
+                obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
+                old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch)
+
+        # set_to_none: backward then hands its fresh gradient buffers to .grad (no
+        # zero-fill + accumulate kernels); inside the captured update these are
+        # graph-pool buffers at fixed addresses, which the captured Adam step reads
+        self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         if self.world_size > 1:
             self._allreduce_grads()
@@ -203,11 +233,9 @@ class PPO:
         with torch.no_grad():
             acc[0] += value_loss.detach()
             acc[1] += surrogate_loss.detach()
-            if self._diag is not None:  # debugging aid: per-step scalars (also inside a captured graph)
+            if self._diag is not None:  # debugging aid: per-step losses (also inside a captured graph)
                 row = self._diag[self._diag_i % self._diag.shape[0]]
-                row.copy_(torch.stack([value_loss.detach(), surrogate_loss.detach(), sigma_batch.mean(),
-                                       mu_batch.abs().mean(), actions_log_prob_batch.mean(), ratio.mean(),
-                                       advantages_batch.mean(), old_actions_log_prob_batch.mean()]))
+                row[:2].copy_(torch.stack([value_loss.detach(), surrogate_loss.detach()]))
                 self._diag_i += 1
         # Release this step's autograd graph.  A distribution kept alive on the
         # module pins the parameters' AccumulateGrad nodes from the stream they were
@@ -259,10 +287,6 @@ class PPO:
                         tens[4] = adv.index_select(0, idx)
                         self._minibatch_step(*tens, (None, None), None, self._acc)
 
-            # static grads (exist after the eager warm-up update) and optimizer state
-            for p_ in self.actor_critic.parameters():
-                if p_.grad is None:
-                    p_.grad = torch.zeros_like(p_)
             self._side = torch.cuda.Stream(self.device)
             self._side.wait_stream(torch.cuda.current_stream(self.device))
             self._graph = torch.cuda.CUDAGraph()

@@ -93,6 +93,10 @@ class ActorCritic(nn.Module):
     def get_actions_log_prob(self, actions):
         return self.distribution.log_prob(actions).sum(dim=-1)
 
+    def policy_mean(self, observations):
+        """Actor output (the Gaussian mean) without building the distribution."""
+        return self._run(self.actor, observations)
+
     def act_inference(self, observations):
         return self._run(self.actor, observations)
 

@@ -43,6 +43,11 @@ def load():
         L.pmlp_reduce_slabs.argtypes = [vp, i32, i64, i64, vp, vp]
         L.pmlp_rowsum.argtypes = [vp, i32, i32, i32, vp, vp]
         L.pmlp_convert_weights.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp]
+        f32 = C.c_float
+        L.pmlp_ppo_loss_blocks.argtypes = [i32]
+        L.pmlp_ppo_loss_blocks.restype = i32
+        L.pmlp_ppo_loss_fwd.argtypes = [vp] * 10 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp]
+        L.pmlp_ppo_loss_bwd.argtypes = [vp] * 10 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -215,3 +220,46 @@ def mlp_apply(seq, x):
             params += [m.weight, m.bias]
     train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     return _MfmaMLPFn.apply(x, train, *params)
+
+
+class _PPOLossFn(torch.autograd.Function):
+    """rsl_rl v1.0.2 PPO loss (Gaussian policy), forward + backward in two fused
+    kernels each (csrc/ppo_mlp.hip k_ppo_loss_*).  Returns (loss, stats) with
+    stats = [surrogate_loss, value_loss, kl_mean, entropy_mean] (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, mu, std, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, clip, clipped, vcoef,
+                ecoef):
+        M, A = mu.shape
+        ins = [t.contiguous().float() for t in (mu, std, value.reshape(M), actions, old_logp.reshape(M), old_mu,
+                                                  old_sigma, adv.reshape(M), ret.reshape(M), target.reshape(M))]
+        nb = load().pmlp_ppo_loss_blocks(M)
+        partial = torch.empty(4 * nb, device=mu.device)
+        loss = torch.empty((), device=mu.device)
+        stats = torch.empty(4, device=mu.device)
+        _ok(load().pmlp_ppo_loss_fwd(*[_p(t) for t in ins], M, A, float(clip), int(bool(clipped)), float(vcoef),
+                                     float(ecoef), _p(partial), _p(loss), _p(stats), _stream()), "pmlp_ppo_loss_fwd")
+        ctx.save_for_backward(*ins)
+        ctx.cfg = (M, A, float(clip), int(bool(clipped)), float(vcoef), float(ecoef), tuple(value.shape))
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, gloss, gstats):
+        ins = ctx.saved_tensors
+        M, A, clip, clipped, vcoef, ecoef, vshape = ctx.cfg
+        dev = ins[0].device
+        g = gloss.contiguous().float().reshape(1)
+        nb = load().pmlp_ppo_loss_blocks(M)
+        dmu = torch.empty(M, A, device=dev)
+        dvalue = torch.empty(M, device=dev)
+        dstd = torch.empty(A, device=dev)
+        partial = torch.empty(A * nb, device=dev)
+        _ok(load().pmlp_ppo_loss_bwd(*[_p(t) for t in ins], M, A, clip, clipped, vcoef, ecoef, _p(g), _p(dmu),
+                                     _p(dvalue), _p(partial), _p(dstd), _stream()), "pmlp_ppo_loss_bwd")
+        return (dmu, dstd, dvalue.view(vshape)) + (None,) * 11
+
+
+def ppo_loss(mu, std, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, clip, clipped, vcoef, ecoef):
+    return _PPOLossFn.apply(mu, std, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, clip, clipped,
+                            vcoef, ecoef)
