@@ -1,16 +1,16 @@
 /*
  * ppo_mlp.h — C ABI of the hand-written bf16-MFMA kernels behind the rsl_rl
- * actor-critic MLPs (ActorCritic.act/evaluate in the
- * rollout and the PPO mini-batch forward/backward).
+ * actor-critic MLPs and the PPO loss (ActorCritic.act/
+ * evaluate in the rollout and the PPO mini-batch forward/backward).
  *
- * The reference runs these as torch nn.Linear/nn.ELU modules (rsl_rl v1.0.2
- * ActorCritic, called from OnPolicyRunner.learn / PPO.update; call sites
- * train.py:14, task_registry.py:119).  Here a torch.autograd.Function
- * (rsl_rl/modules/mfma_mlp.py) drives these entry points per layer; parameters,
- * losses and the optimizer stay fp32 torch tensors.
+ * The reference runs these as torch nn.Linear/nn.ELU modules and torch loss
+ * ops (rsl_rl v1.0.2 ActorCritic, PPO.update; called from OnPolicyRunner.learn,
+ * call sites train.py:14, task_registry.py:119).  Here torch.autograd.Functions
+ * (rsl_rl/modules/mfma_mlp.py) drive these entry points; parameters and the
+ * optimizer stay fp32 torch tensors.
  *
  * Conventions: every pointer is a DEVICE pointer; matrices are row-major with
- * the given leading dimension (in elements, a multiple of 8 for bf16 operands,
+ * the given leading dimension (in elements; a multiple of 8 for bf16 operands,
  * 16-byte aligned rows); "bf16" is the 16-bit bfloat16 storage type.  Work is
  * enqueued on `stream` (a hipStream_t; NULL = default stream); nothing
  * synchronises the host; nothing allocates, so every call is graph-capturable.
@@ -24,30 +24,15 @@
 #define PMLP_EXTERN extern "C"
 #else
 #define PMLP_EXTERN
-/* Fused PPO loss of rsl_rl v1.0.2 PPO.update for a diagonal Gaussian policy
- * (ratio, clipped surrogate, optionally clipped value loss, entropy bonus,
- * and the KL the adaptive learning rate reads).  Inputs fp32, row-major:
- * mu/actions/old_mu/old_sigma [M,A], stdv [A], value/old_logp/adv/ret/target [M].
- * fwd: loss[1]; stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean};
- *      partial = scratch of 4*pmlp_ppo_loss_blocks(M) floats.
- * bwd: gout = device scalar d(total)/d(loss); dmu [M,A], dvalue [M], dstd [A];
- *      partial_std = scratch of A*pmlp_ppo_loss_blocks(M) floats.          */
-PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M);
-PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
-                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
-                               float* stats, void* stream);
-PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
-                               const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
-                               float* dvalue, float* partial_std, float* dstd, void* stream);
-
 #endif
 #define PMLP_API PMLP_EXTERN __attribute__((visibility("default")))
 
 typedef uint16_t pmlp_bf16;
+
+/* Every entry point takes a batch of independent jobs (the actor and the
+ * critic of a step run as one launch each).                                 */
+#define PMLP_MAX_JOBS 16
+#define PMLP_MAX_GEMM_JOBS 4
 
 /* GEMM epilogues.  All GEMMs are C[M,N] = A[M,K] . B[N,K]^T with A and B bf16
  * and k contiguous (the MFMA operand order).                                 */
@@ -60,20 +45,16 @@ enum {
 
 PMLP_API const char* pmlp_last_error(void);
 
-/* fp32 x[M,K] (ld ldx) -> bf16 y[M,Kp] (ld ldy) and/or y^T[Kp,M] (ld ldyt);
- * columns K..Kp-1 of y (rows of y^T) are zero.  y or yt may be NULL.
- * Replaces the implicit fp32->bf16 casts autocast would insert.            */
-PMLP_API int pmlp_convert(const float* x, int32_t M, int32_t K, int32_t ldx, int32_t Kp, pmlp_bf16* y, int32_t ldy,
-                          pmlp_bf16* yt, int32_t ldyt, void* stream);
-
-/* All weight matrices of one network in one launch: job i converts fp32
- * w[i] [n[i], k[i]] to bf16 y[i] [n[i], kp[i]] (row-major, zero-padded) and,
- * when yt[i] != NULL, to yt[i] [k[i], ldyt[i]] (transposed; columns n..ldyt-1
- * zero).  y / yt may be NULL arrays.                                          */
-#define PMLP_MAX_JOBS 16
-PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const int32_t* n, const int32_t* k,
-                                  const int32_t* kp, pmlp_bf16* const* y, pmlp_bf16* const* yt, const int32_t* ldyt,
-                                  void* stream);
+/* fp32 x[M,K] (ld ldx) -> bf16 y[M,Kp] (ld Kp; columns K..Kp-1 zero) and/or
+ * y^T[Kp,ldyt] (rows K..Kp-1 and columns M..ldyt-1 zero); y or yt may be NULL.
+ * Used for observations, output gradients and weights (W and W^T).          */
+typedef struct {
+    const float* x;
+    pmlp_bf16* y;
+    pmlp_bf16* yt;
+    int32_t M, K, ldx, Kp, ldyt;
+} pmlp_convert_job;
+PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream);
 
 /* C = A . B^T with epilogue `epi` (see enum).  A: [M,K] (lda), B: [N,K] (ldb).
  *   FWD_HIDDEN: bias[N]; cb[M,N] (ldcb); ct[N,M] (ldct, may be NULL)
@@ -81,19 +62,36 @@ PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const in
  *   BWD_DX:     yprev[M,N] bf16 (ldyp) = the ELU output the gradient flows through;
  *               cb/ct as FWD_HIDDEN
  *   PARTIAL:    cf = slab base, slab s at cf + s*M*ldcf; ksplit = k per slab
- *               (multiple of 32); number of slabs = ceil(K / ksplit)          */
-PMLP_API int pmlp_gemm(int32_t epi, const pmlp_bf16* A, int32_t lda, const pmlp_bf16* B, int32_t ldb, int32_t M,
-                       int32_t N, int32_t K, const float* bias, const pmlp_bf16* yprev, int32_t ldyp, float* cf,
-                       int32_t ldcf, pmlp_bf16* cb, int32_t ldcb, pmlp_bf16* ct, int32_t ldct, int32_t ksplit,
-                       void* stream);
+ *               (multiple of 32); every job must give the same ceil(K/ksplit) */
+typedef struct {
+    const pmlp_bf16* A;
+    const pmlp_bf16* B;
+    const float* bias;
+    const pmlp_bf16* yprev;
+    float* cf;
+    pmlp_bf16* cb;
+    pmlp_bf16* ct;
+    int32_t lda, ldb, ldyp, ldcf, ldcb, ldct;
+    int32_t M, N, K;
+} pmlp_gemm_job;
+PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
 
-/* out[i] = sum_s slab[s*slab_stride + i], i < n (fp32): the split-K combine. */
-PMLP_API int pmlp_reduce_slabs(const float* slab, int32_t nslabs, int64_t slab_stride, int64_t n, float* out,
-                               void* stream);
+/* out[i] = sum_s slab[s*stride + i], i < n (fp32): the split-K combine. */
+typedef struct {
+    const float* slab;
+    float* out;
+    int64_t stride, n;
+    int32_t nslabs;
+} pmlp_reduce_job;
+PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream);
 
-/* out[r] = sum_c x[r*ld + c] for c < cols (bf16 in, fp32 sum): bias gradient
- * from dz^T rows.                                                           */
-PMLP_API int pmlp_rowsum(const pmlp_bf16* x, int32_t rows, int32_t cols, int32_t ld, float* out, void* stream);
+/* out[r] = sum_c x[r*ld + c], c < cols (bf16 in, fp32 sum): bias gradients. */
+typedef struct {
+    const pmlp_bf16* x;
+    float* out;
+    int32_t rows, cols, ld;
+} pmlp_rowsum_job;
+PMLP_API int pmlp_rowsum(int32_t njobs, const pmlp_rowsum_job* jobs, void* stream);
 
 /* Fused PPO loss of rsl_rl v1.0.2 PPO.update for a diagonal Gaussian policy
  * (ratio, clipped surrogate, optionally clipped value loss, entropy bonus,

@@ -320,6 +320,26 @@ def test_mfma_mlp_matches_fp32_torch(rows):
         assert torch.equal(y2, y.detach())  # row results independent of train/eval path
 
 
+def test_mfma_twin_mlps_match_single_launches():
+    """Actor + critic through shared launches == each net alone (bitwise), grads too."""
+    from rsl_rl.modules import mfma_mlp
+    from rsl_rl.modules.actor_critic import mlp, get_activation
+    torch.manual_seed(1)
+    a = mlp(48, [512, 256, 128], 12, get_activation("elu")).cuda()
+    c = mlp(50, [512, 256, 128], 1, get_activation("elu")).cuda()
+    xa, xc = torch.randn(8192, 48, device="cuda"), torch.randn(8192, 50, device="cuda")
+    ya, yc = mfma_mlp.mlps_apply([a, c], [xa, xc])
+    ga = torch.randn_like(ya)
+    gc = torch.randn_like(yc)
+    g2 = torch.autograd.grad((ya * ga).sum() + (yc * gc).sum(), list(a.parameters()) + list(c.parameters()))
+    ya1 = mfma_mlp.mlp_apply(a, xa)
+    yc1 = mfma_mlp.mlp_apply(c, xc)
+    g1 = torch.autograd.grad((ya1 * ga).sum() + (yc1 * gc).sum(), list(a.parameters()) + list(c.parameters()))
+    assert torch.equal(ya, ya1) and torch.equal(yc, yc1)
+    for u, v in zip(g2, g1):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("clipped", [True, False])
 def test_fused_ppo_loss_matches_reference_loss(clipped):
     """mfma_mlp.ppo_loss (fused kernels) vs rsl_rl's torch statement of the loss:

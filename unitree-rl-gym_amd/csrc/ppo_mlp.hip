@@ -56,8 +56,16 @@ struct GemmArgs {
 
 __device__ __forceinline__ float elu(float v) { return v > 0.f ? v : expm1f(v); }
 
+struct GemmBatch {
+    GemmArgs j[PMLP_MAX_GEMM_JOBS];
+    int slabs;  // PARTIAL: slabs per job (grid.z = njobs * slabs)
+};
+
 template <int BM, int BN, int WM, int WN, int EPI>
-__global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmArgs g) {
+__global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
+    const int job = blockIdx.z / gb.slabs, slice = blockIdx.z % gb.slabs;
+    const GemmArgs& g = gb.j[job];
+    if ((int)blockIdx.x * BM >= g.M || (int)blockIdx.y * BN >= g.N) return;  // grid covers the largest job
     constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
     constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
     constexpr int NT = 64 * WM * WN;
@@ -77,7 +85,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmArgs g) {
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     int kb = 0, ke = g.K;
     if (EPI == PMLP_EPI_PARTIAL) {
-        kb = blockIdx.z * g.ksplit;
+        kb = slice * g.ksplit;
         ke = min(g.K, kb + g.ksplit);
     }
     floatx16 acc[FM][FN];
@@ -154,7 +162,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmArgs g) {
             const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
             if (col >= g.N && (EPI == PMLP_EPI_PARTIAL || EPI == PMLP_EPI_FWD_OUT)) continue;
             if (EPI == PMLP_EPI_PARTIAL) {
-                float* slab = g.cf + (size_t)blockIdx.z * g.M * g.ldcf;
+                float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const int row = rbase + (t & 3) + 8 * (t >> 2);
@@ -220,62 +228,14 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmArgs g) {
     }
 }
 
-// fp32 [M,K] -> bf16 [M,Kp] and/or [Kp,M], 64x64 tiles through LDS.
-__global__ __launch_bounds__(256) void k_convert(const float* __restrict__ x, int M, int K, int ldx, int Kp,
-                                                 bf16* __restrict__ y, int ldy, bf16* __restrict__ yt, int ldyt) {
-    __shared__ float tile[64][65];
-    const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-    for (int r = ty; r < 64; r += 4) {
-        const int m = m0 + r, k = k0 + tx;
-        float v = 0.f;
-        if (m < M && k < K) v = x[(size_t)m * ldx + k];
-        tile[r][tx] = v;
-        if (y && m < M && k < Kp) y[(size_t)m * ldy + k] = (bf16)v;
-    }
-    if (!yt) return;
-    __syncthreads();
-    for (int c = ty; c < 64; c += 4) {  // row k0+c of y^T, columns m0..m0+63
-        const int k = k0 + c, m = m0 + tx;
-        if (k < Kp && m < M) yt[(size_t)k * ldyt + m] = (bf16)tile[tx][c];
-    }
-}
-
-__global__ void k_reduce_slabs(const float* __restrict__ slab, int S, int64_t stride, int64_t n,
-                               float* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += slab[(size_t)k * stride + i];
-    out[i] = s;
-}
-
-__global__ __launch_bounds__(256) void k_rowsum(const bf16* __restrict__ x, int cols, int ld, float* __restrict__ out) {
-    __shared__ float part[4];
-    const int r = blockIdx.x, tid = threadIdx.x;
-    const bf16* row = x + (size_t)r * ld;
-    float s = 0.f;
-    const int full = cols / 8;
-    for (int c = tid; c < full; c += 256) {
-        bf16x8 v = *(const bf16x8*)(row + 8 * c);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += (float)v[u];
-    }
-    for (int u = 8 * full + tid; u < cols; u += 256) s += (float)row[u];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if ((tid & 63) == 0) part[tid >> 6] = s;
-    __syncthreads();
-    if (tid == 0) out[r] = (part[0] + part[1]) + (part[2] + part[3]);
-}
-
-// Several fp32 weight matrices W[N,K] -> bf16 W[N,Kp] (row-major) and W^T[K,ld]
-// in one launch (blockIdx.z = job); 64x64 tiles through LDS.
+// Batched fp32 -> bf16 conversion, 64x64 tiles through LDS (blockIdx.z = job):
+// x[M,K] (ld ldx) -> y[M,Kp] (ld Kp, columns K.. zero) and/or y^T[Kp,ldyt]
+// (rows K.. and columns M.. zero).
 struct CvtJob {
-    const float* w;
+    const float* x;
     bf16* y;
     bf16* yt;
-    int N, K, Kp, ldyt;
+    int M, K, ldx, Kp, ldyt;
 };
 struct CvtJobs {
     CvtJob j[PMLP_MAX_JOBS];
@@ -283,22 +243,70 @@ struct CvtJobs {
 __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
     const CvtJob J = jobs.j[blockIdx.z];
     const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    if (m0 >= J.N || k0 >= J.Kp) return;
+    const int mext = J.yt ? max(J.M, J.ldyt) : J.M;
+    if (m0 >= mext || k0 >= J.Kp) return;
     __shared__ float tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
         const int m = m0 + r, k = k0 + tx;
         float v = 0.f;
-        if (m < J.N && k < J.K) v = J.w[(size_t)m * J.K + k];
+        if (m < J.M && k < J.K) v = J.x[(size_t)m * J.ldx + k];
         tile[r][tx] = v;
-        if (J.y && m < J.N && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v;
+        if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v;
     }
     if (!J.yt) return;
     __syncthreads();
     for (int c = ty; c < 64; c += 4) {
         const int k = k0 + c, m = m0 + tx;
-        if (k < J.K && m < J.ldyt) J.yt[(size_t)k * J.ldyt + m] = (bf16)(m < J.N ? tile[tx][c] : 0.f);
+        if (k < J.Kp && m < J.ldyt) J.yt[(size_t)k * J.ldyt + m] = (bf16)tile[tx][c];
     }
+}
+
+struct RedJob {
+    const float* slab;
+    float* out;
+    int64_t stride, n;
+    int nslabs;
+};
+struct RedJobs {
+    RedJob j[PMLP_MAX_JOBS];
+};
+__global__ void k_reduce_jobs(RedJobs jobs) {
+    const RedJob J = jobs.j[blockIdx.y];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.n) return;
+    float s = 0.f;
+    for (int k = 0; k < J.nslabs; ++k) s += J.slab[(size_t)k * J.stride + i];
+    J.out[i] = s;
+}
+
+struct SumJob {
+    const bf16* x;
+    float* out;
+    int rows, cols, ld;
+};
+struct SumJobs {
+    SumJob j[PMLP_MAX_JOBS];
+};
+__global__ __launch_bounds__(256) void k_rowsum_jobs(SumJobs jobs) {
+    __shared__ float part[4];
+    const SumJob J = jobs.j[blockIdx.y];
+    const int r = blockIdx.x, tid = threadIdx.x;
+    if (r >= J.rows) return;
+    const bf16* row = J.x + (size_t)r * J.ld;
+    float s = 0.f;
+    const int full = J.cols / 8;
+    for (int c = tid; c < full; c += 256) {
+        bf16x8 v = *(const bf16x8*)(row + 8 * c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += (float)v[u];
+    }
+    for (int u = 8 * full + tid; u < J.cols; u += 256) s += (float)row[u];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((tid & 63) == 0) part[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) J.out[r] = (part[0] + part[1]) + (part[2] + part[3]);
 }
 
 
@@ -457,13 +465,13 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_std(LossArgs a, 
 }
 
 template <int BM, int BN, int WM, int WN>
-static void launch(int epi, const GemmArgs& g, int slabs, hipStream_t st) {
-    dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, slabs), block(64 * WM * WN);
+static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, hipStream_t st) {
+    dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
     switch (epi) {
-    case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, g); break;
-    case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, g); break;
-    case PMLP_EPI_BWD_DX: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, g); break;
-    default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, g); break;
+    case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, gb); break;
+    case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, gb); break;
+    case PMLP_EPI_BWD_DX: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, gb); break;
+    default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, gb); break;
     }
 }
 
@@ -473,86 +481,99 @@ extern "C" {
 
 PMLP_API const char* pmlp_last_error(void) { return g_err.c_str(); }
 
-PMLP_API int pmlp_convert(const float* x, int32_t M, int32_t K, int32_t ldx, int32_t Kp, pmlp_bf16* y, int32_t ldy,
-                          pmlp_bf16* yt, int32_t ldyt, void* stream) {
-    if (!x || M <= 0 || K <= 0 || Kp < K || ldx < K || (y && ldy < Kp) || (yt && ldyt < M))
-        return fail(-1, "pmlp_convert: bad arguments");
-    dim3 grid((M + 63) / 64, (Kp + 63) / 64);
-    hipLaunchKernelGGL(k_convert, grid, dim3(256), 0, (hipStream_t)stream, x, M, K, ldx, Kp, (bf16*)y, ldy, (bf16*)yt,
-                       ldyt);
+PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream) {
+    if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_convert: 1..PMLP_MAX_JOBS jobs");
+    CvtJobs cj{};
+    int maxm = 0, maxk = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_convert_job& J = jobs[i];
+        if (!J.x || J.M <= 0 || J.K <= 0 || J.Kp < J.K || J.ldx < J.K || (!J.y && !J.yt) || (J.yt && J.ldyt < J.M))
+            return fail(-1, "pmlp_convert: bad job " + std::to_string(i));
+        cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0};
+        maxm = std::max(maxm, std::max(J.M, J.yt ? J.ldyt : 0));
+        maxk = std::max(maxk, J.Kp);
+    }
+    dim3 grid((maxm + 63) / 64, (maxk + 63) / 64, njobs);
+    hipLaunchKernelGGL(k_convert_jobs, grid, dim3(256), 0, (hipStream_t)stream, cj);
     PMLP_CHECK_LAUNCH("pmlp_convert");
     return 0;
 }
 
-PMLP_API int pmlp_gemm(int32_t epi, const pmlp_bf16* A, int32_t lda, const pmlp_bf16* B, int32_t ldb, int32_t M,
-                       int32_t N, int32_t K, const float* bias, const pmlp_bf16* yprev, int32_t ldyp, float* cf,
-                       int32_t ldcf, pmlp_bf16* cb, int32_t ldcb, pmlp_bf16* ct, int32_t ldct, int32_t ksplit,
-                       void* stream) {
+PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream) {
     if (epi < 0 || epi > 3) return fail(-1, "pmlp_gemm: unknown epilogue");
-    if (!A || !B || M <= 0 || N <= 0 || K <= 0) return fail(-1, "pmlp_gemm: null operand or empty shape");
-    if (K % 8 || lda % 8 || ldb % 8 || lda < K || ldb < K || !al16(A) || !al16(B))
-        return fail(-1, "pmlp_gemm: K, lda, ldb must be multiples of 8 with 16-byte aligned operands");
-    if ((epi == PMLP_EPI_FWD_OUT || epi == PMLP_EPI_PARTIAL) && (!cf || ldcf < N))
-        return fail(-1, "pmlp_gemm: fp32 output missing or ldcf < N");
-    if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) && (!cb || ldcb < N || (ct && (ldct < M || ldct % 4))))
-        return fail(-1, "pmlp_gemm: bf16 output missing or bad leading dimension");
-    if (epi == PMLP_EPI_BWD_DX && (!yprev || ldyp < N)) return fail(-1, "pmlp_gemm: BWD_DX needs yprev");
-    int slabs = 1;
+    if (njobs <= 0 || njobs > PMLP_MAX_GEMM_JOBS || !jobs) return fail(-1, "pmlp_gemm: 1..PMLP_MAX_GEMM_JOBS jobs");
+    GemmBatch gb{};
+    gb.slabs = 1;
+    int maxm = 0, maxn = 0, maxk = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_gemm_job& J = jobs[i];
+        const std::string w = "pmlp_gemm job " + std::to_string(i) + ": ";
+        if (!J.A || !J.B || J.M <= 0 || J.N <= 0 || J.K <= 0) return fail(-1, w + "null operand or empty shape");
+        if (J.K % 8 || J.lda % 8 || J.ldb % 8 || J.lda < J.K || J.ldb < J.K || !al16(J.A) || !al16(J.B))
+            return fail(-1, w + "K, lda, ldb must be multiples of 8 with 16-byte aligned operands");
+        if ((epi == PMLP_EPI_FWD_OUT || epi == PMLP_EPI_PARTIAL) && (!J.cf || J.ldcf < J.N))
+            return fail(-1, w + "fp32 output missing or ldcf < N");
+        if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) &&
+            (!J.cb || J.ldcb < J.N || (J.ct && (J.ldct < J.M || J.ldct % 4))))
+            return fail(-1, w + "bf16 output missing or bad leading dimension");
+        if (epi == PMLP_EPI_BWD_DX && (!J.yprev || J.ldyp < J.N)) return fail(-1, w + "BWD_DX needs yprev");
+        GemmArgs& g = gb.j[i];
+        g.A = (const bf16*)J.A; g.B = (const bf16*)J.B; g.bias = J.bias; g.yp = (const bf16*)J.yprev;
+        g.cf = J.cf; g.cb = (bf16*)J.cb; g.ct = (bf16*)J.ct;
+        g.lda = J.lda; g.ldb = J.ldb; g.ldyp = J.ldyp; g.ldcf = J.ldcf; g.ldcb = J.ldcb; g.ldct = J.ldct;
+        g.M = J.M; g.N = J.N; g.K = J.K; g.ksplit = ksplit;
+        maxm = std::max(maxm, J.M); maxn = std::max(maxn, J.N); maxk = std::max(maxk, J.K);
+    }
     if (epi == PMLP_EPI_PARTIAL) {
         if (ksplit <= 0 || ksplit % 32) return fail(-1, "pmlp_gemm: ksplit must be a positive multiple of 32");
-        slabs = (K + ksplit - 1) / ksplit;
+        for (int i = 0; i < njobs; ++i)
+            if ((jobs[i].K + ksplit - 1) / ksplit != (maxk + ksplit - 1) / ksplit)
+                return fail(-1, "pmlp_gemm: PARTIAL jobs must have the same number of slabs");
+        gb.slabs = (maxk + ksplit - 1) / ksplit;
     }
-    GemmArgs g;
-    g.A = (const bf16*)A; g.B = (const bf16*)B; g.bias = bias; g.yp = (const bf16*)yprev;
-    g.cf = cf; g.cb = (bf16*)cb; g.ct = (bf16*)ct;
-    g.lda = lda; g.ldb = ldb; g.ldyp = ldyp; g.ldcf = ldcf; g.ldcb = ldcb; g.ldct = ldct;
-    g.M = M; g.N = N; g.K = K; g.ksplit = ksplit;
     hipStream_t st = (hipStream_t)stream;
-    if (M <= 32) launch<32, 128, 1, 4>(epi, g, slabs, st);
-    else if (N <= 32) launch<128, 32, 4, 1>(epi, g, slabs, st);
-    else if (N <= 64) launch<128, 64, 4, 1>(epi, g, slabs, st);
-    else launch<128, 128, 2, 2>(epi, g, slabs, st);
+    if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, st);
+    else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, st);
+    else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, st);
+    else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, st);
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
 }
 
-PMLP_API int pmlp_reduce_slabs(const float* slab, int32_t nslabs, int64_t slab_stride, int64_t n, float* out,
-                               void* stream) {
-    if (!slab || !out || nslabs <= 0 || n <= 0 || slab_stride < n) return fail(-1, "pmlp_reduce_slabs: bad arguments");
+PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream) {
+    if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_reduce_slabs: 1..PMLP_MAX_JOBS jobs");
+    RedJobs rj{};
+    int64_t maxn = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_reduce_job& J = jobs[i];
+        if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n)
+            return fail(-1, "pmlp_reduce_slabs: bad job " + std::to_string(i));
+        rj.j[i] = RedJob{J.slab, J.out, J.stride, J.n, J.nslabs};
+        maxn = std::max(maxn, J.n);
+    }
     const int bs = 256;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, (hipStream_t)stream, slab,
-                       nslabs, slab_stride, n, out);
+    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)((maxn + bs - 1) / bs), njobs), dim3(bs), 0, (hipStream_t)stream,
+                       rj);
     PMLP_CHECK_LAUNCH("pmlp_reduce_slabs");
     return 0;
 }
 
-PMLP_API int pmlp_rowsum(const pmlp_bf16* x, int32_t rows, int32_t cols, int32_t ld, float* out, void* stream) {
-    if (!x || !out || rows <= 0 || cols <= 0 || ld < cols || ld % 8 || !al16(x))
-        return fail(-1, "pmlp_rowsum: bad arguments");
-    hipLaunchKernelGGL(k_rowsum, dim3(rows), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, cols, ld, out);
+PMLP_API int pmlp_rowsum(int32_t njobs, const pmlp_rowsum_job* jobs, void* stream) {
+    if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_rowsum: 1..PMLP_MAX_JOBS jobs");
+    SumJobs sj{};
+    int maxr = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_rowsum_job& J = jobs[i];
+        if (!J.x || !J.out || J.rows <= 0 || J.cols <= 0 || J.ld < J.cols || J.ld % 8 || !al16(J.x))
+            return fail(-1, "pmlp_rowsum: bad job " + std::to_string(i));
+        sj.j[i] = SumJob{(const bf16*)J.x, J.out, J.rows, J.cols, J.ld};
+        maxr = std::max(maxr, J.rows);
+    }
+    hipLaunchKernelGGL(k_rowsum_jobs, dim3(maxr, njobs), dim3(256), 0, (hipStream_t)stream, sj);
     PMLP_CHECK_LAUNCH("pmlp_rowsum");
     return 0;
 }
 
-PMLP_API int pmlp_convert_weights(int32_t njobs, const float* const* w, const int32_t* n, const int32_t* k,
-                                  const int32_t* kp, pmlp_bf16* const* y, pmlp_bf16* const* yt, const int32_t* ldyt,
-                                  void* stream) {
-    if (njobs <= 0 || njobs > PMLP_MAX_JOBS) return fail(-1, "pmlp_convert_weights: 1..PMLP_MAX_JOBS jobs");
-    CvtJobs jobs{};
-    int maxn = 0, maxk = 0;
-    for (int i = 0; i < njobs; ++i) {
-        if (!w[i] || n[i] <= 0 || k[i] <= 0 || kp[i] < k[i] || (yt && yt[i] && ldyt[i] < n[i]))
-            return fail(-1, "pmlp_convert_weights: bad job " + std::to_string(i));
-        jobs.j[i] = CvtJob{w[i], (bf16*)(y ? y[i] : nullptr), (bf16*)(yt ? yt[i] : nullptr), n[i], k[i], kp[i],
-                           yt && yt[i] ? ldyt[i] : 0};
-        maxn = std::max(maxn, std::max(n[i], yt && yt[i] ? ldyt[i] : 0));
-        maxk = std::max(maxk, kp[i]);
-    }
-    dim3 grid((maxn + 63) / 64, (maxk + 63) / 64, njobs);
-    hipLaunchKernelGGL(k_convert_jobs, grid, dim3(256), 0, (hipStream_t)stream, jobs);
-    PMLP_CHECK_LAUNCH("pmlp_convert_weights");
-    return 0;
-}
 
 static int loss_args(LossArgs& a, const float* mu, const float* stdv, const float* value, const float* actions,
                      const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,

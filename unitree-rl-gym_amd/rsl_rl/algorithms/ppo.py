@@ -73,7 +73,7 @@ class PPO:
         self._graph = None
         # fused PPO-loss kernels for the Gaussian MLP policy on a GPU (fused_loss=False:
         # the torch statement of the loss, _reference_loss)
-        self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "policy_mean")
+        self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "mean_and_value")
         self._diag, self._diag_i = None, 0
         self._graph_calls = 0
         self._capturing = False
@@ -106,8 +106,12 @@ class PPO:
     def act(self, obs, critic_obs):
         if self.actor_critic.is_recurrent:
             self.transition.hidden_states = self.actor_critic.get_hidden_states()
-        self.transition.actions = self.actor_critic.act(obs).detach()
-        self.transition.values = self.actor_critic.evaluate(critic_obs).detach()
+        if not self.actor_critic.is_recurrent and hasattr(self.actor_critic, "act_and_value"):  # shared launches
+            actions, values = self.actor_critic.act_and_value(obs, critic_obs)
+            self.transition.actions, self.transition.values = actions.detach(), values.detach()
+        else:
+            self.transition.actions = self.actor_critic.act(obs).detach()
+            self.transition.values = self.actor_critic.evaluate(critic_obs).detach()
         self.transition.actions_log_prob = self.actor_critic.get_actions_log_prob(self.transition.actions).detach()
         self.transition.action_mean = self.actor_critic.action_mean.detach()
         self.transition.action_sigma = self.actor_critic.action_std.detach()
@@ -207,8 +211,7 @@ class PPO:
         """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
         if self._fused_loss and not self.actor_critic.is_recurrent:
             # same loss, two fused kernels forward + two backward (modules/mfma_mlp.ppo_loss)
-            mu_batch = self.actor_critic.policy_mean(obs_batch)
-            value_batch = self.actor_critic.evaluate(critic_obs_batch)
+            mu_batch, value_batch = self.actor_critic.mean_and_value(obs_batch, critic_obs_batch)
             loss, stats = mfma_mlp.ppo_loss(mu_batch, self.actor_critic.std, value_batch, actions_batch,
                                             old_actions_log_prob_batch, old_mu_batch, old_sigma_batch,
                                             advantages_batch, returns_batch, target_values_batch, self.clip_param,

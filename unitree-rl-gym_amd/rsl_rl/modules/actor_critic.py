@@ -97,6 +97,21 @@ class ActorCritic(nn.Module):
         """Actor output (the Gaussian mean) without building the distribution."""
         return self._run(self.actor, observations)
 
+    def mean_and_value(self, observations, critic_observations):
+        """Actor mean and critic value; on the MFMA path both nets share every launch."""
+        if self.mixed_precision and mfma_mlp.usable(self.actor, observations) and \
+                mfma_mlp.usable(self.critic, critic_observations) and \
+                observations.shape[0] == critic_observations.shape[0] and \
+                (len(self.actor) == len(self.critic)):
+            return mfma_mlp.mlps_apply([self.actor, self.critic], [observations, critic_observations])
+        return self._run(self.actor, observations), self._run(self.critic, critic_observations)
+
+    def act_and_value(self, observations, critic_observations):
+        """act() + evaluate() of one rollout step (the distribution is kept, as act() does)."""
+        mean, value = self.mean_and_value(observations, critic_observations)
+        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=False)
+        return self.distribution.sample(), value
+
     def act_inference(self, observations):
         return self._run(self.actor, observations)
 

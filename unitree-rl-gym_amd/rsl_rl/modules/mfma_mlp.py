@@ -29,6 +29,31 @@ def lib_path():
     return os.path.normpath(os.path.join(_HERE, "..", "..", "csrc", "build", "libppomlp.so"))
 
 
+class ConvertJob(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("yt", C.c_void_p), ("M", C.c_int32), ("K", C.c_int32),
+                ("ldx", C.c_int32), ("Kp", C.c_int32), ("ldyt", C.c_int32)]
+
+
+class GemmJob(C.Structure):
+    _fields_ = [("A", C.c_void_p), ("B", C.c_void_p), ("bias", C.c_void_p), ("yprev", C.c_void_p),
+                ("cf", C.c_void_p), ("cb", C.c_void_p), ("ct", C.c_void_p), ("lda", C.c_int32), ("ldb", C.c_int32),
+                ("ldyp", C.c_int32), ("ldcf", C.c_int32), ("ldcb", C.c_int32), ("ldct", C.c_int32),
+                ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32)]
+
+
+class ReduceJob(C.Structure):
+    _fields_ = [("slab", C.c_void_p), ("out", C.c_void_p), ("stride", C.c_int64), ("n", C.c_int64),
+                ("nslabs", C.c_int32)]
+
+
+class RowsumJob(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("out", C.c_void_p), ("rows", C.c_int32), ("cols", C.c_int32),
+                ("ld", C.c_int32)]
+
+
+MAX_JOBS, MAX_GEMM_JOBS = 16, 4
+
+
 def load():
     global _lib
     if _lib is None:
@@ -36,13 +61,12 @@ def load():
         if not os.path.exists(path):
             raise RuntimeError(f"libppomlp.so not found at {path}: build it (make -C unitree-rl-gym_amd/csrc)")
         L = C.CDLL(path)
-        vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+        vp, i32 = C.c_void_p, C.c_int32
         L.pmlp_last_error.restype = C.c_char_p
-        L.pmlp_convert.argtypes = [vp, i32, i32, i32, i32, vp, i32, vp, i32, vp]
-        L.pmlp_gemm.argtypes = [i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp, i32, vp, i32, vp, i32, i32, vp]
-        L.pmlp_reduce_slabs.argtypes = [vp, i32, i64, i64, vp, vp]
-        L.pmlp_rowsum.argtypes = [vp, i32, i32, i32, vp, vp]
-        L.pmlp_convert_weights.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.pmlp_convert.argtypes = [i32, C.POINTER(ConvertJob), vp]
+        L.pmlp_gemm.argtypes = [i32, i32, C.POINTER(GemmJob), i32, vp]
+        L.pmlp_reduce_slabs.argtypes = [i32, C.POINTER(ReduceJob), vp]
+        L.pmlp_rowsum.argtypes = [i32, C.POINTER(RowsumJob), vp]
         f32 = C.c_float
         L.pmlp_ppo_loss_blocks.argtypes = [i32]
         L.pmlp_ppo_loss_blocks.restype = i32
@@ -65,6 +89,10 @@ def _ceil8(n):
     return (n + 7) // 8 * 8
 
 
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
 def supported(seq):
     """Linear (ELU(alpha=1) Linear)* with hidden widths that are multiples of 8."""
     if not isinstance(seq, nn.Sequential) or len(seq) % 2 != 1:
@@ -80,32 +108,41 @@ def supported(seq):
     return True
 
 
-def _convert(x, Kp, y=None, yt=None):
-    M, K = x.shape
-    _ok(load().pmlp_convert(_p(x), M, K, x.stride(0), Kp, _p(y), 0 if y is None else y.stride(0), _p(yt),
-                            0 if yt is None else yt.stride(0), _stream()), "pmlp_convert")
+def _convert(jobs):
+    """jobs: (x fp32 [M,K], Kp, y bf16 [M,Kp] | None, yt bf16 [Kp,ld] | None)"""
+    for i in range(0, len(jobs), MAX_JOBS):
+        chunk = jobs[i:i + MAX_JOBS]
+        arr = (ConvertJob * len(chunk))(*[
+            ConvertJob(_p(x), _p(y), _p(yt), x.shape[0], x.shape[1], x.stride(0), kp, 0 if yt is None else yt.shape[1])
+            for x, kp, y, yt in chunk])
+        _ok(load().pmlp_convert(len(chunk), arr, _stream()), "pmlp_convert")
 
 
-def _convert_weights(ws, ys, yts):
-    n = len(ws)
-    arr = lambda T, v: (T * n)(*v)  # noqa: E731
-    vp = C.c_void_p
-    _ok(load().pmlp_convert_weights(
-        n, arr(vp, [w.data_ptr() for w in ws]), arr(C.c_int32, [w.shape[0] for w in ws]),
-        arr(C.c_int32, [w.shape[1] for w in ws]), arr(C.c_int32, [y.shape[1] for y in ys]),
-        arr(vp, [y.data_ptr() for y in ys]), arr(vp, [None if t is None else t.data_ptr() for t in yts]),
-        arr(C.c_int32, [0 if t is None else t.shape[1] for t in yts]), _stream()), "pmlp_convert_weights")
+def _gemm(epi, jobs, ksplit=0):
+    """jobs: dicts with A, B, M, N, K and optional bias, yprev, cf, cb, ct (tensors)."""
+    def mk(j):
+        g = lambda k: j.get(k)  # noqa: E731
+        ld = lambda t: 0 if t is None else t.stride(0)  # noqa: E731
+        return GemmJob(_p(j["A"]), _p(j["B"]), _p(g("bias")), _p(g("yprev")), _p(g("cf")), _p(g("cb")), _p(g("ct")),
+                       j["A"].stride(0), j["B"].stride(0), ld(g("yprev")),
+                       0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"])
+    arr = (GemmJob * len(jobs))(*[mk(j) for j in jobs])
+    _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+def _reduce(jobs):
+    for i in range(0, len(jobs), MAX_JOBS):
+        chunk = jobs[i:i + MAX_JOBS]
+        arr = (ReduceJob * len(chunk))(*[ReduceJob(_p(sl), _p(out), n, n, ns) for sl, out, n, ns in chunk])
+        _ok(load().pmlp_reduce_slabs(len(chunk), arr, _stream()), "pmlp_reduce_slabs")
 
 
-def _gemm(epi, A, B, M, N, K, bias=None, yprev=None, cf=None, cb=None, ct=None, ksplit=0):
-    _ok(load().pmlp_gemm(epi, _p(A), A.stride(0), _p(B), B.stride(0), M, N, K, _p(bias), _p(yprev),
-                         0 if yprev is None else yprev.stride(0), _p(cf), 0 if cf is None else cf.shape[-1], _p(cb),
-                         0 if cb is None else cb.stride(0), _p(ct), 0 if ct is None else ct.stride(0), ksplit,
-                         _stream()), "pmlp_gemm")
+def _rowsum(jobs):
+    for i in range(0, len(jobs), MAX_JOBS):
+        chunk = jobs[i:i + MAX_JOBS]
+        arr = (RowsumJob * len(chunk))(*[RowsumJob(_p(x), _p(out), rows, x.shape[1], x.stride(0))
+                                         for x, out, rows in chunk])
+        _ok(load().pmlp_rowsum(len(chunk), arr, _stream()), "pmlp_rowsum")
 
 
 def _tiles(M, N):
@@ -122,88 +159,124 @@ def _tiles(M, N):
 
 
 def _ksplit(batch, tiles, target_blocks=256):
-    # >= ~1024 rows per slab: the slab combine (pmlp_reduce_slabs) reads every slab once
+    # >= ~1024 rows per slab: the slab combine reads every slab once
     slabs = max(1, min(batch // 1024, round(target_blocks / tiles)))
     ks = (batch + slabs - 1) // slabs
     return (ks + 63) // 64 * 64
 
 
-class _MfmaMLPFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, train, *params):
-        Ws, bs = params[0::2], params[1::2]
-        L = len(Ws)
-        x = x.contiguous()
-        M = x.shape[0]
-        dev = x.device
-        bf = torch.bfloat16
-        k0p = _ceil8(x.shape[1])
-        xb = torch.empty(M, k0p, dtype=bf, device=dev)
-        xt = torch.empty(k0p, M, dtype=bf, device=dev) if train else None
-        _convert(x, k0p, xb, xt)
-        acts, acts_t = [xb], [xt]
-        # every layer's bf16 W [N, kp] and (training) W^T [K, N8] in one launch
-        wbs = [torch.empty(W.shape[0], k0p if l == 0 else W.shape[1], dtype=bf, device=dev) for l, W in enumerate(Ws)]
-        wts = [torch.empty(W.shape[1], _ceil8(W.shape[0]), dtype=bf, device=dev) if (train and l > 0) else None
-               for l, W in enumerate(Ws)]
-        _convert_weights([W.detach() for W in Ws], wbs, wts)
-        h = xb
-        for l in range(L):
-            W, b = Ws[l], bs[l]
-            N, K = W.shape
-            kp = k0p if l == 0 else K
-            wb = wbs[l]
-            if l < L - 1:
-                y = torch.empty(M, N, dtype=bf, device=dev)
-                yt = torch.empty(N, M, dtype=bf, device=dev) if train else None
-                _gemm(EPI_FWD_HIDDEN, h, wb, M, N, kp, bias=b.detach(), cb=y, ct=yt)
-                acts.append(y)
-                acts_t.append(yt)
-                h = y
-            else:
-                out = torch.empty(M, N, dtype=torch.float32, device=dev)
-                _gemm(EPI_FWD_OUT, h, wb, M, N, kp, bias=b.detach(), cf=out)
-        if train:
-            ctx.acts, ctx.acts_t, ctx.wts = acts, acts_t, wts
-            ctx.shapes = [tuple(W.shape) for W in Ws]
-            ctx.k0p = k0p
-        return out
+class _MfmaMLPsFn(torch.autograd.Function):
+    """Several same-depth Linear/ELU MLPs on the same batch size, every stage of all of
+    them in one launch (the actor and the critic of PPO)."""
 
     @staticmethod
-    def backward(ctx, dout):
-        shapes, acts, acts_t, wts = ctx.shapes, ctx.acts, ctx.acts_t, ctx.wts
-        L = len(shapes)
-        dout = dout.contiguous().float()
-        M = dout.shape[0]
-        dev = dout.device
-        bf = torch.bfloat16
-        n_last = shapes[-1][0]
-        np_ = _ceil8(n_last)
-        dz = torch.empty(M, np_, dtype=bf, device=dev)
-        dzt = torch.empty(np_, M, dtype=bf, device=dev)
-        _convert(dout, np_, dz, dzt)
-        grads = [None] * (2 * L)
+    def forward(ctx, nnets, train, *args):
+        xs = [x.contiguous() for x in args[:nnets]]
+        params = args[nnets:]
+        L = len(params) // (2 * nnets)
+        Ws = [params[2 * L * n:2 * L * (n + 1)][0::2] for n in range(nnets)]
+        bs = [params[2 * L * n:2 * L * (n + 1)][1::2] for n in range(nnets)]
+        M = xs[0].shape[0]
+        assert all(x.shape[0] == M for x in xs)
+        dev, bf = xs[0].device, torch.bfloat16
+        k0p = [_ceil8(x.shape[1]) for x in xs]
+        xb = [torch.empty(M, k0p[n], dtype=bf, device=dev) for n in range(nnets)]
+        xt = [torch.empty(k0p[n], M, dtype=bf, device=dev) if train else None for n in range(nnets)]
+        wb = [[torch.empty(W.shape[0], k0p[n] if l == 0 else W.shape[1], dtype=bf, device=dev)
+               for l, W in enumerate(Ws[n])] for n in range(nnets)]
+        wt = [[torch.empty(W.shape[1], _ceil8(W.shape[0]), dtype=bf, device=dev) if (train and l > 0) else None
+               for l, W in enumerate(Ws[n])] for n in range(nnets)]
+        jobs = []
+        for n in range(nnets):
+            jobs.append((xs[n], k0p[n], xb[n], xt[n]))
+            for l, W in enumerate(Ws[n]):
+                Wd = W.detach()
+                jobs.append((Wd, wb[n][l].shape[1], wb[n][l], None))
+                if wt[n][l] is not None:  # W^T [K, N8] for the input-gradient GEMM
+                    jobs.append((Wd, W.shape[1], None, wt[n][l]))
+        _convert(jobs)
+        acts = [[xb[n]] for n in range(nnets)]
+        acts_t = [[xt[n]] for n in range(nnets)]
+        outs = [None] * nnets
+        for l in range(L):
+            last = l == L - 1
+            gj = []
+            for n in range(nnets):
+                N, K = Ws[n][l].shape
+                kp = k0p[n] if l == 0 else K
+                if last:
+                    outs[n] = torch.empty(M, N, dtype=torch.float32, device=dev)
+                    gj.append(dict(A=acts[n][-1], B=wb[n][l], M=M, N=N, K=kp, bias=bs[n][l].detach(), cf=outs[n]))
+                else:
+                    y = torch.empty(M, N, dtype=bf, device=dev)
+                    yt = torch.empty(N, M, dtype=bf, device=dev) if train else None
+                    gj.append(dict(A=acts[n][-1], B=wb[n][l], M=M, N=N, K=kp, bias=bs[n][l].detach(), cb=y, ct=yt))
+                    acts[n].append(y)
+                    acts_t[n].append(yt)
+            _gemm(EPI_FWD_OUT if last else EPI_FWD_HIDDEN, gj)
+        if train:
+            ctx.acts, ctx.acts_t, ctx.wt = acts, acts_t, wt
+            ctx.shapes = [[tuple(W.shape) for W in Ws[n]] for n in range(nnets)]
+            ctx.k0p, ctx.nnets = k0p, nnets
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        nnets, shapes, acts, acts_t, wt, k0p = ctx.nnets, ctx.shapes, ctx.acts, ctx.acts_t, ctx.wt, ctx.k0p
+        L = len(shapes[0])
+        M = acts[0][0].shape[0]
+        dev, bf = acts[0][0].device, torch.bfloat16
+        dz, dzt, jobs = [], [], []
+        for n in range(nnets):
+            n_out = shapes[n][-1][0]
+            d = douts[n]
+            d = torch.zeros(M, n_out, device=dev) if d is None else d.contiguous().float()
+            npad = _ceil8(n_out)
+            dz.append(torch.empty(M, npad, dtype=bf, device=dev))
+            dzt.append(torch.empty(npad, M, dtype=bf, device=dev))
+            jobs.append((d, npad, dz[n], dzt[n]))
+        _convert(jobs)
+        grads = [[None] * (2 * L) for _ in range(nnets)]
+        red, rsum = [], []
         for l in range(L - 1, -1, -1):
-            N, K = shapes[l]
-            kp = ctx.k0p if l == 0 else K
-            # weight gradient: dW = dz^T x  (A = dz^T [N, M], B = x^T [kp, M]), split over the batch
-            ks = _ksplit(M, _tiles(N, kp))
+            # weight gradients dW = dz^T x (split over the batch) for every net in one launch
+            kps = [k0p[n] if l == 0 else shapes[n][l][1] for n in range(nnets)]
+            ks = _ksplit(M, max(_tiles(shapes[n][l][0], kps[n]) for n in range(nnets)))
             slabs = (M + ks - 1) // ks
-            slab = torch.empty(slabs, N, kp, dtype=torch.float32, device=dev)
-            _gemm(EPI_PARTIAL, dzt, acts_t[l], N, kp, M, cf=slab, ksplit=ks)
-            dw = torch.empty(N, kp, dtype=torch.float32, device=dev)
-            _ok(load().pmlp_reduce_slabs(_p(slab), slabs, N * kp, N * kp, _p(dw), _stream()), "pmlp_reduce_slabs")
-            db = torch.empty(N, dtype=torch.float32, device=dev)
-            _ok(load().pmlp_rowsum(_p(dzt), N, M, dzt.stride(0), _p(db), _stream()), "pmlp_rowsum")
-            grads[2 * l] = dw if kp == K else dw[:, :K].contiguous()
-            grads[2 * l + 1] = db
-            if l > 0:  # input gradient through the ELU below: dz_prev = (dz W) * ELU'(y_prev)
-                dzp = torch.empty(M, K, dtype=bf, device=dev)
-                dztp = torch.empty(K, M, dtype=bf, device=dev)
-                _gemm(EPI_BWD_DX, dz, wts[l], M, K, dz.shape[1], yprev=acts[l], cb=dzp, ct=dztp)
-                dz, dzt = dzp, dztp
-        ctx.acts = ctx.acts_t = ctx.wts = None
-        return (None, None, *grads)
+            gj = []
+            for n in range(nnets):
+                N = shapes[n][l][0]
+                slab = torch.empty(slabs, N, kps[n], dtype=torch.float32, device=dev)
+                dw = torch.empty(N, kps[n], dtype=torch.float32, device=dev)
+                db = torch.empty(N, dtype=torch.float32, device=dev)
+                gj.append(dict(A=dzt[n], B=acts_t[n][l], M=N, N=kps[n], K=M, cf=slab))
+                red.append((slab, dw, N * kps[n], slabs))
+                rsum.append((dzt[n], db, N))
+                K = shapes[n][l][1]
+                grads[n][2 * l] = dw if kps[n] == K else dw[:, :K]
+                grads[n][2 * l + 1] = db
+            _gemm(EPI_PARTIAL, gj, ksplit=ks)
+            if l > 0:  # input gradients through the ELU below, every net in one launch
+                gj, nxt = [], []
+                for n in range(nnets):
+                    K = shapes[n][l][1]
+                    dzp = torch.empty(M, K, dtype=bf, device=dev)
+                    dztp = torch.empty(K, M, dtype=bf, device=dev)
+                    gj.append(dict(A=dz[n], B=wt[n][l], M=M, N=K, K=dz[n].shape[1], yprev=acts[n][l], cb=dzp,
+                                   ct=dztp))
+                    nxt.append((dzp, dztp))
+                _gemm(EPI_BWD_DX, gj)
+                dz, dzt = [a for a, _ in nxt], [b for _, b in nxt]
+        _reduce(red)
+        _rowsum(rsum)
+        for n in range(nnets):
+            for l in range(L):
+                K = shapes[n][l][1]
+                if grads[n][2 * l].shape[1] != K or not grads[n][2 * l].is_contiguous():
+                    grads[n][2 * l] = grads[n][2 * l].contiguous()
+        ctx.acts = ctx.acts_t = ctx.wt = None
+        flat = [g for n in range(nnets) for g in grads[n]]
+        return (None, None) + (None,) * nnets + tuple(flat)
 
 
 def usable(seq, x):
@@ -212,14 +285,25 @@ def usable(seq, x):
     return x.is_cuda and x.dim() == 2 and x.shape[0] % 8 == 0 and supported(seq)
 
 
-def mlp_apply(seq, x):
-    """Run nn.Sequential `seq` on x [M, in] through the MFMA kernels (autograd-aware)."""
-    params = []
+def _params(seq):
+    ps = []
     for m in seq:
         if isinstance(m, nn.Linear):
-            params += [m.weight, m.bias]
+            ps += [m.weight, m.bias]
+    return ps
+
+
+def mlps_apply(seqs, xs):
+    """Run nn.Sequentials `seqs` on inputs `xs` (same batch size) through the MFMA kernels,
+    every stage of all nets in one launch.  Returns a tuple of outputs (autograd-aware)."""
+    params = [p for s in seqs for p in _params(s)]
     train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-    return _MfmaMLPFn.apply(x, train, *params)
+    return _MfmaMLPsFn.apply(len(seqs), train, *xs, *params)
+
+
+def mlp_apply(seq, x):
+    """Run nn.Sequential `seq` on x [M, in] through the MFMA kernels (autograd-aware)."""
+    return mlps_apply([seq], [x])[0]
 
 
 class _PPOLossFn(torch.autograd.Function):
