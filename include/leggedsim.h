@@ -171,6 +171,9 @@ typedef struct lgs_task_params {
     /* humanoid gait phase (h1_env.py:55-65) */
     float phase_period, phase_offset, stance_threshold, swing_height_target;
     uint64_t seed;
+    /* 1: refresh rigid_body_states [N,B,13] every control step (the humanoid envs
+     * read it, h1_env.py:37,49); 0: leave it untouched (LeggedRobot never reads it) */
+    int32_t write_body_states;
 } lgs_task_params;
 
 /* ---- per-env buffers of the VecEnv (device pointers; torch owns them) ---- */

@@ -911,8 +911,8 @@ void orc_step(const lgs_model_desc* md, const lgs_sim_params* sp, const lgs_task
             orc_substep_env(md, sp, root + 13 * e, dofs + 2 * D * e, E->torques + D * e, cforce + 3 * B * e,
                             added_mass ? added_mass[e] : 0.f, friction ? friction[e] : 1.f);
         }
-        if (rbs) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
-        ostate st = {root, dofs, cforce, rbs};
+        if (rbs && T->write_body_states) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
+        ostate st = {root, dofs, cforce, T->write_body_states ? rbs : NULL};
         orc_post_physics_env(md, T, N, e, &st, E, step_counter);
     }
 }

@@ -56,6 +56,11 @@ __device__ unsigned long long* g_phase_buf;
 #define STAMP_FLUSH(e) do {} while (0)
 #define STAMP_INIT() do {} while (0)
 #endif
+// occupancy target of the 32-row (Go2) k_step: 4 waves/SIMD puts all 4096 envs in
+// flight at once but caps VGPRs at 128 (spills); 2 keeps every value in registers
+#ifndef LGS_WAVES_PER_EU
+#define LGS_WAVES_PER_EU 4
+#endif
 #define MAXB LGS_MAX_BODIES
 #define MAXD LGS_MAX_DEPTH
 #define WAVE 64
@@ -303,7 +308,11 @@ template <int D, int B, int ROWS>
 __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& sp, float added_mass, float shape_mu) {
     constexpr int n = 6 + D;
     const ModelCache<D, B>& mc = s.mc;
-    const int lane = threadIdx.x;
+    // Opaque lane id: lane-derived addresses are recomputed each substep (a few VALU
+    // ops) instead of being hoisted out of the decimation loop and held live across
+    // every substep, which pushed the 4-waves/SIMD build into scratch.
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
     const float dt = sp.dt;
 
     STAMP(0);
@@ -528,6 +537,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             const float ljk = rl(m[k], j);
             if (lane >= j) m[j] -= m[k] * ljk;
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
     // rows of L to LDS; lane j then holds column j (c[k] = L[k][j], k >= j)
     if (lane < n) {
@@ -674,6 +684,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
             for (int k = 0; k < i; ++k) t -= rl(m[k], i) * y[k];
             y[i] = t / rl(m[i], i);
+            // keep row i's L broadcasts next to their use: hoisting all 171 of them
+            // exhausts the SGPRs and spills the kernel to scratch
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (lane < ROWS) {
 #pragma unroll
@@ -742,29 +755,33 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acol[r] = (lane < ROWS) ? s.u.con.A[r][lane < ROWS ? lane : 0] : 0.f;
     }
-    float lamv[ROWS];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) lamv[r] = 0.f;
+    float lam = 0.f;  // lane r holds lambda_r (one VGPR; read by v_readlane)
     {
         const float mu = 0.5f * (sp.ground_friction + shape_mu);
-        const float tg = used ? s.tgt[lane] : 0.f;
+        float tg = used ? s.tgt[lane] : 0.f;
         float dg = 0.f;
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) dg = (lane == r) ? acol[r] : dg;
-        const float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
+        float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
         for (int it = 0; it < sp.iters; ++it) {
+            // Opaque per sweep: otherwise LICM hoists ~64 loop-invariant readlanes
+            // (targets, 1/A_rr, normal-friction couplings) out of the sweep loop; with
+            // the SGPRs full they occupy VGPRs and the kernel spills to scratch.
+            asm volatile("" : "+v"(tg), "+v"(inv));
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) asm volatile("" : "+v"(acol[r]));
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
                 if (c < nc) {
                     const int r = 3 * c;
+                    const float lno = rl(lam, r), l1o = rl(lam, r + 1), l2o = rl(lam, r + 2);
                     const float vn = rl(v, r), v1 = rl(v, r + 1), v2 = rl(v, r + 2);
-                    const float ln = fmaxf(0.f, lamv[r] + (rl(tg, r) - vn) * rl(inv, r));
-                    const float dn = ln - lamv[r];
+                    const float ln = fmaxf(0.f, lno + (rl(tg, r) - vn) * rl(inv, r));
+                    const float dn = ln - lno;
                     v = fmaf(acol[r], dn, v);
                     const float v1n = fmaf(rl(acol[r], r + 1), dn, v1);
                     const float v2n = fmaf(rl(acol[r], r + 2), dn, v2);
                     const float lim = mu * ln;
-                    const float l1o = lamv[r + 1], l2o = lamv[r + 2];
                     float l1 = l1o - v1n * rl(inv, r + 1);
                     float l2 = l2o - v2n * rl(inv, r + 2);
                     const float nrm = sqrtf(l1 * l1 + l2 * l2);
@@ -774,19 +791,17 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                     }
                     const float d1 = l1 - l1o, d2 = l2 - l2o;
                     v += acol[r + 1] * d1 + acol[r + 2] * d2;
-                    lamv[r] = rfl(ln);
-                    lamv[r + 1] = rfl(l1);
-                    lamv[r + 2] = rfl(l2);
+                    lam = lane == r ? ln : (lane == r + 1 ? l1 : (lane == r + 2 ? l2 : lam));
                 }
             }
 #pragma unroll
             for (int l = 0; l < LM; ++l) {
                 if (l < nlimit) {
                     const int r = 3 * CM + l;
-                    const float ln = fmaxf(0.f, lamv[r] + (rl(tg, r) - rl(v, r)) * rl(inv, r));
-                    const float dl = ln - lamv[r];
-                    v = fmaf(acol[r], dl, v);
-                    lamv[r] = rfl(ln);
+                    const float lo = rl(lam, r);
+                    const float ln = fmaxf(0.f, lo + (rl(tg, r) - rl(v, r)) * rl(inv, r));
+                    v = fmaf(acol[r], ln - lo, v);
+                    lam = lane == r ? ln : lam;
                 }
             }
         }
@@ -798,13 +813,13 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
-                z += s.u.con.Y[3 * c][lane] * lamv[3 * c];
-                z += s.u.con.Y[3 * c + 1][lane] * lamv[3 * c + 1];
-                z += s.u.con.Y[3 * c + 2][lane] * lamv[3 * c + 2];
+                z += s.u.con.Y[3 * c][lane] * rl(lam, 3 * c);
+                z += s.u.con.Y[3 * c + 1][lane] * rl(lam, 3 * c + 1);
+                z += s.u.con.Y[3 * c + 2][lane] * rl(lam, 3 * c + 2);
             }
 #pragma unroll
         for (int l = 0; l < LM; ++l)
-            if (l < nlimit) z += s.u.con.Y[3 * CM + l][lane] * lamv[3 * CM + l];
+            if (l < nlimit) z += s.u.con.Y[3 * CM + l][lane] * rl(lam, 3 * CM + l);
     }
     {
         float lc[n];
@@ -827,8 +842,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         float F[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < CM; ++c)
-            if (c < nc && s.c_body[c] == lane) {
-                F[0] += lamv[3 * c + 1] / dt; F[1] += lamv[3 * c + 2] / dt; F[2] += lamv[3 * c] / dt;
+            if (c < nc) {
+                const float ln = rl(lam, 3 * c), l1 = rl(lam, 3 * c + 1), l2 = rl(lam, 3 * c + 2);
+                if (s.c_body[c] == lane) { F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt; }
             }
         if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
     }
@@ -865,6 +881,16 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     __syncthreads();
     STAMP(14);
+}
+
+// Workgroups are dealt round-robin over the 8 XCDs (each with its own L2).  Map
+// them so every XCD owns one contiguous env range: small per-env fields (reward,
+// reset byte, commands, counters) then share cache lines within one L2 instead
+// of being dirtied and written back by up to 8 (bijective for any grid size,
+// MI355X guide §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_env(int b, int nwg) {
+    const int xcd = b % 8, q = nwg / 8, r = nwg % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
 // rigid body states [B][13] of the block's env into global memory
@@ -931,7 +957,8 @@ __device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& 
 }
 template <int D, int B, int ROWS>
 __device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
-    const int lane = threadIdx.x;
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));  // recompute the lane indices here (no value kept live from load_state)
     if (lane < 13) st.root[13 * e + lane] = s.root[lane];
     if (lane < 2 * D) st.dofs[(size_t)2 * D * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
     for (int i = lane; i < 3 * B; i += WAVE) st.cforce[(size_t)3 * B * e + i] = (&s.cf[0][0])[i];
@@ -941,7 +968,7 @@ __device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState&
 template <int D, int B, int ROWS>
 __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
-    const int e = blockIdx.x;
+    const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(s, md);
     load_state(s, st, e);
@@ -955,7 +982,7 @@ __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevSt
 template <int D, int B, int ROWS>
 __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
-    const int e = blockIdx.x;
+    const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(s, md);
     load_state(s, st, e);
@@ -1293,10 +1320,10 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
 }
 
 template <int D, int B, int ROWS>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? 4 : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? LGS_WAVES_PER_EU : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step) {
     __shared__ Smem<D, B, ROWS> s;
-    const int e = blockIdx.x;
+    const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     const lgs_task_params& T = *Tp;
     const int lane = threadIdx.x;
@@ -1329,8 +1356,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     }
     STAMP(0);
     if (lane < D) E.torques[D * e + lane] = s.tau[lane];
-    float* rbs = st.rbs + (size_t)13 * B * e;
-    body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49)
+    float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * B * e : nullptr;
+    if (rbs) body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
     __syncthreads();
     STAMP(15);
     post_physics(s, T, E, rbs, N, e, step, false);
@@ -1345,7 +1372,7 @@ template <int D, int B, int ROWS>
 __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
                                                     lgs_env_buffers E, int N, uint32_t step) {
     __shared__ Smem<D, B, ROWS> s;
-    const int e = blockIdx.x;
+    const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(s, md);
     load_state(s, st, e);

@@ -90,6 +90,7 @@ class TaskParams(C.Structure):
         ("phase_period", C.c_float), ("phase_offset", C.c_float), ("stance_threshold", C.c_float),
         ("swing_height_target", C.c_float),
         ("seed", C.c_uint64),
+        ("write_body_states", C.c_int32),
     ]
 
 

@@ -101,4 +101,5 @@ def build_task_params(env) -> cabi.TaskParams:
     seed = int(getattr(cfg, "seed", 1))
     rank = int(os.environ.get("RANK", "0"))
     T.seed = (seed & 0xFFFFFFFF) | (rank << 32)
+    T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)))
     return T
