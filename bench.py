@@ -142,7 +142,7 @@ def main():
         ev[i][0].record(stream)
         env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
         ev[i][1].record(stream)
-        env.common_step_counter += 1
+        env.account_replayed_steps(1)
     torch.cuda.synchronize(dev)
     env_wall = time.time() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.env_steps

@@ -202,6 +202,10 @@ typedef struct lgs_env_buffers {
     float* phase;            /* [N]   humanoid, else NULL */
     float* leg_phase;        /* [N,2] humanoid, else NULL */
     float* rew_terms;        /* [num_rewards, N] per-term reward of this step (diagnostics) or NULL */
+    int64_t* step_counter;   /* [1] device copy of common_step_counter, or NULL.  When set, lgs_step and
+                                lgs_reset_all read the Philox step key from it instead of the by-value
+                                argument, and lgs_step advances it by one after the step: a captured
+                                hipGraph of K steps then draws fresh noise/commands on every replay. */
 } lgs_env_buffers;
 
 typedef struct lgs_sim lgs_sim;

@@ -384,3 +384,45 @@ def test_fused_ppo_loss_matches_reference_loss(clipped):
     for a, b in zip(g, g_ref):
         assert a.shape == b.shape
         assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-4
+
+
+def test_rollout_graph_matches_eager_rollouts(tmp_path):
+    """OnPolicyRunner's captured collection loop (_RolloutGraph) replays the same
+    rollouts as the eager loop: same env states, storage, policy and logged
+    episode statistics (rewbuffer/lenbuffer/ep_infos) after several iterations."""
+    import json
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    out = {}
+    for graph in (False, True):
+        env = make("go2", 512, env__episode_length_s=0.5)  # 25-step episodes: resets inside every rollout
+        _, train_cfg = task_registry.get_cfgs("go2")
+        cfg = class_to_dict(train_cfg)
+        cfg["runner"]["rollout_graph"] = graph
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        log_dir = tmp_path / f"graph{int(graph)}"
+        runner = OnPolicyRunner(env, cfg, log_dir=str(log_dir), device="cuda:0")
+        runner.learn(4, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+        runner.writer.flush()
+        st = runner.alg.storage
+        scal = [json.loads(line) for line in open(log_dir / "scalars.jsonl")]
+        out[graph] = dict(
+            root=env.root_states.clone(), obs=env.obs_buf.clone(), step=env.common_step_counter,
+            dev_step=int(env._d_step_counter), st_obs=st.observations.clone(), st_act=st.actions.clone(),
+            st_rew=st.rewards.clone(), st_done=st.dones.clone(),
+            params=[p.detach().clone() for p in runner.alg.actor_critic.parameters()],
+            scalars={(s["tag"], s["step"]): s["value"] for s in scal
+                     if not s["tag"].startswith("Perf") and "time" not in s["tag"]})
+        env.close()
+    e, g = out[False], out[True]
+    assert e["step"] == g["step"] == g["dev_step"] == e["dev_step"] == 4 * cfg["runner"]["num_steps_per_env"] + 1
+    for k in ("root", "obs", "st_obs", "st_act", "st_rew", "st_done"):
+        assert torch.equal(e[k], g[k]), k
+    for a, b in zip(e["params"], g["params"]):
+        assert torch.equal(a, b)
+    assert e["scalars"].keys() == g["scalars"].keys()
+    assert any(k[0] == "Train/mean_reward" for k in e["scalars"])
+    for k, v in e["scalars"].items():
+        assert v == pytest.approx(g["scalars"][k], rel=1e-6, abs=1e-7), k

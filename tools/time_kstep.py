@@ -32,7 +32,7 @@ def run_one(task, n, lib):
         ev[i][0].record(stream)
         env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
         ev[i][1].record(stream)
-        env.common_step_counter += 1
+        env.account_replayed_steps(1)
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in ev)
     print(f"{task} n={n} lib={os.path.basename(lib or 'default')}: k_step median {ms[K // 2]:.4f} ms  "

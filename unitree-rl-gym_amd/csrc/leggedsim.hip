@@ -1325,6 +1325,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
+    if (E.step_counter) step = (uint32_t)*E.step_counter;
     const lgs_task_params& T = *Tp;
     const int lane = threadIdx.x;
     load_model(s, md);
@@ -1374,6 +1375,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
+    if (E.step_counter) step = (uint32_t)*E.step_counter;
     load_model(s, md);
     load_state(s, st, e);
     if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
@@ -1383,6 +1385,9 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     store_state(s, st, e);
     if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
 }
+
+// common_step_counter += 1 on the device (the step key of graph-replayed steps)
+__global__ void k_advance_step(int64_t* counter) { *counter += 1; }
 
 __global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, int n, int width) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1633,6 +1638,10 @@ LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counte
     DevState st = state_of(s);
     LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
     HIP_TRY(hipGetLastError());
+    if (env->step_counter) {
+        hipLaunchKernelGGL(k_advance_step, dim3(1), dim3(1), 0, s->stream, env->step_counter);
+        HIP_TRY(hipGetLastError());
+    }
     return LGS_OK;
 }
 

@@ -227,6 +227,7 @@ class LeggedRobot(BaseTask):
         self.episode_sums = {name: self._episode_sums[i] for i, name in enumerate(self._sum_names)}
         self._episode_acc = torch.zeros(nsum + 1, dtype=torch.float, device=self.device)
         self._ep_means = torch.zeros(nsum, dtype=torch.float, device=self.device)
+        self._time_outs = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
 
     # ------------------------------------------------------ native task -----
     def _build_task(self):
@@ -261,7 +262,27 @@ class LeggedRobot(BaseTask):
         E.phase = p(self.phase)
         E.leg_phase = p(self.leg_phase)
         E.rew_terms = None
+        E.step_counter = p(self._d_step_counter)
         return E
+
+    @property
+    def common_step_counter(self):
+        """The reference's step counter (legged_robot.py:116).  The native step keys its
+        Philox streams on a DEVICE copy that lgs_step advances itself, so a captured
+        rollout graph draws new noise/commands on every replay; this host mirror counts
+        eagerly issued steps plus those the runner reports via `account_replayed_steps`."""
+        return self._step_mirror
+
+    @common_step_counter.setter
+    def common_step_counter(self, value):
+        self._step_mirror = int(value)
+        if getattr(self, "_d_step_counter", None) is None:
+            self._d_step_counter = torch.zeros((), dtype=torch.int64, device=self.device)
+        self._d_step_counter.fill_(self._step_mirror)
+
+    def account_replayed_steps(self, n):
+        """A graph replay of n captured steps advanced the device counter by n."""
+        self._step_mirror += int(n)
 
     def _sync_stream(self):
         s = torch.cuda.current_stream(self.device).cuda_stream
@@ -277,8 +298,8 @@ class LeggedRobot(BaseTask):
         i = self._buf_idx
         self.actions.copy_(actions)
         self._episode_acc.zero_()
-        self.sim.step(self._env_structs[i], self.common_step_counter)
-        self.common_step_counter += 1
+        self.sim.step(self._env_structs[i], self._step_mirror)
+        self._step_mirror += 1
         self.obs_buf = self._obs_bufs[i]
         self.privileged_obs_buf = self._priv_bufs[i]
         self.reset_buf = self._reset_bufs[i]
@@ -287,16 +308,22 @@ class LeggedRobot(BaseTask):
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
     def _update_extras(self):
-        """extras["episode"] / ["time_outs"] refresh only when >= 1 env reset (:742-768)."""
+        """extras["episode"] / ["time_outs"] refresh only when >= 1 env reset (:742-768).
+
+        The values carried from step to step live in persistent buffers updated in
+        place (so a captured rollout graph carries them across replays); each step's
+        extras["episode"] dict holds views of that step's own snapshot, like the
+        reference's fresh per-reset tensors."""
         nsum = len(self._sum_names)
         cnt = self._episode_acc[nsum]
         any_reset = cnt > 0
         means = self._episode_acc[:nsum] / cnt.clamp(min=1.0) / self.max_episode_length_s
-        self._ep_means = torch.where(any_reset, means, self._ep_means)
-        self.extras["episode"] = {"rew_" + k: self._ep_means[i] for i, k in enumerate(self._sum_names)}
+        snap = torch.where(any_reset, means, self._ep_means)
+        self._ep_means.copy_(snap)
+        self.extras["episode"] = {"rew_" + k: snap[i] for i, k in enumerate(self._sum_names)}
         if self.cfg.env.send_timeouts:
-            prev = self.extras.get("time_outs", self.time_out_buf)
-            self.extras["time_outs"] = torch.where(any_reset, self.time_out_buf, prev)
+            self._time_outs.copy_(torch.where(any_reset, self.time_out_buf, self._time_outs))
+            self.extras["time_outs"] = self._time_outs
 
     def reset_idx(self, env_ids):
         """Reset the given envs.  The native kernel resets every env of the batch
@@ -307,9 +334,10 @@ class LeggedRobot(BaseTask):
             raise NotImplementedError("reset_idx of a subset: resets happen inside step() from reset_buf")
         self._sync_stream()
         self.sim.reset_all(self._env_structs[self._buf_idx], self.common_step_counter)
-        self.extras["episode"] = {"rew_" + k: self._ep_means[i] for i, k in enumerate(self._sum_names)}
+        self.extras["episode"] = {"rew_" + k: self._ep_means[i].clone() for i, k in enumerate(self._sum_names)}
         if self.cfg.env.send_timeouts:
-            self.extras["time_outs"] = self.time_out_buf
+            self._time_outs.copy_(self.time_out_buf)
+            self.extras["time_outs"] = self._time_outs
 
     def post_physics_step(self):
         raise RuntimeError("post_physics_step runs inside the fused native step()")

@@ -109,8 +109,12 @@ class ActorCritic(nn.Module):
     def act_and_value(self, observations, critic_observations):
         """act() + evaluate() of one rollout step (the distribution is kept, as act() does)."""
         mean, value = self.mean_and_value(observations, critic_observations)
-        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=False)
-        return self.distribution.sample(), value
+        std = mean * 0.0 + self.std
+        self.distribution = Normal(mean, std, validate_args=False)
+        # = Normal.sample() (normal_(0, 1) * std + mean, the same draws) without its
+        # std >= 0 check, a device->host sync that hipGraph capture forbids
+        with torch.no_grad():
+            return mean + std * torch.randn_like(mean), value
 
     def act_inference(self, observations):
         return self._run(self.actor, observations)

@@ -39,6 +39,74 @@ def _make_writer(log_dir):
         return _JsonlWriter(log_dir)
 
 
+class _RolloutGraph:
+    """The collection loop of OnPolicyRunner.learn (num_steps_per_env x act -> env.step
+    -> process_env_step) captured once and replayed every iteration.
+
+    Every tensor the loop reads or writes is static: the env's parity-double-buffered
+    obs/reset buffers (num_steps_per_env is even, so the parity returns), the rollout
+    storage slots, the policy's buffers, and the env's device-side step counter, which
+    the native step advances itself so replays draw fresh noise/commands.  Episode
+    logging (the eager loop's .nonzero()/.cpu() per step) becomes per-step device
+    records read back once per iteration, in the same order."""
+
+    def __init__(self, runner, obs, critic_obs, cur_reward_sum, cur_episode_length):
+        self.runner = runner
+        T, N = runner.num_steps_per_env, runner.env.num_envs
+        if T % 2:
+            raise ValueError("rollout graph needs an even num_steps_per_env (env buffer parity)")
+        dev = runner.device
+        self.T = T
+        self.log = runner.log_dir is not None
+        with torch.inference_mode(False):  # ordinary tensors: the graph writes them in place
+            self.done = torch.zeros(T, N, dtype=torch.bool, device=dev)
+            self.done_rew = torch.zeros(T, N, device=dev)
+            self.done_len = torch.zeros(T, N, device=dev)
+        self.ep_infos = []
+        env, storage = runner.env, runner.alg.storage
+        step0, storage0 = env.common_step_counter, storage.step
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        # captured outside inference mode: the graph's RNG offset tensors must stay
+        # ordinary tensors (replays update them in place)
+        with torch.inference_mode(False), torch.no_grad(), torch.cuda.graph(self.graph):
+            for t in range(T):
+                obs, critic_obs, rewards, dones, infos = runner._collect_step(obs, critic_obs)
+                if self.log:
+                    if "episode" in infos:
+                        self.ep_infos.append(infos["episode"])
+                    cur_reward_sum += rewards
+                    cur_episode_length += 1
+                    d = dones > 0
+                    self.done[t].copy_(d)
+                    self.done_rew[t].copy_(cur_reward_sum)
+                    self.done_len[t].copy_(cur_episode_length)
+                    cur_reward_sum.masked_fill_(d, 0.0)
+                    cur_episode_length.masked_fill_(d, 0.0)
+        # capture issued nothing: restore the host-side counters the loop advanced
+        env.common_step_counter = step0
+        storage.step = storage0
+        self.obs, self.critic_obs = obs, critic_obs
+
+    def matches(self, obs, critic_obs):
+        """The loop's inputs are the buffers it was captured on (same env-buffer parity)."""
+        return obs is self.obs and critic_obs is self.critic_obs
+
+    def replay(self):
+        with torch.inference_mode(False):
+            self.graph.replay()
+        self.runner.env.account_replayed_steps(self.T)
+        self.runner.alg.storage.step = self.T
+        return self.obs, self.critic_obs
+
+    def finished_episodes(self, rewbuffer, lenbuffer):
+        """Extend the logging deques exactly as the eager loop would (step-major, env order)."""
+        done = self.done.cpu()
+        if done.any():
+            rewbuffer.extend(self.done_rew.cpu()[done].tolist())
+            lenbuffer.extend(self.done_len.cpu()[done].tolist())
+
+
 class OnPolicyRunner:
     def __init__(self, env: VecEnv, train_cfg, log_dir=None, device="cpu"):
         self.cfg = train_cfg["runner"]
@@ -62,6 +130,10 @@ class OnPolicyRunner:
         self.tot_timesteps = 0
         self.tot_time = 0
         self.current_learning_iteration = 0
+        self._cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        self._cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        self._rollout_graph = None
+        self._eager_rollouts = 0
         _, _ = self.env.reset()
 
     def learn(self, num_learning_iterations, init_at_random_ep_len=False):
@@ -79,31 +151,43 @@ class OnPolicyRunner:
         ep_infos = []
         rewbuffer = deque(maxlen=100)
         lenbuffer = deque(maxlen=100)
-        cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
-        cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        # persistent (zeroed per learn() call, as the reference's locals start at zero)
+        # so that a captured rollout graph can keep accumulating into them
+        cur_reward_sum, cur_episode_length = self._cur_reward_sum, self._cur_episode_length
+        cur_reward_sum.zero_()
+        cur_episode_length.zero_()
         sync = (lambda: torch.cuda.synchronize(self.device)) if str(self.device).startswith("cuda") else (lambda: None)
 
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
             with torch.inference_mode():
-                for _ in range(self.num_steps_per_env):
-                    actions = self.alg.act(obs, critic_obs)
-                    obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
-                    critic_obs = privileged_obs if privileged_obs is not None else obs
-                    obs, critic_obs, rewards, dones = (obs.to(self.device), critic_obs.to(self.device),
-                                                       rewards.to(self.device), dones.to(self.device))
-                    self.alg.process_env_step(rewards, dones, infos)
+                graph = self._rollout_graph
+                if graph is not None and not graph.matches(obs, critic_obs):
+                    graph = self._rollout_graph = None
+                if graph is None and self._eager_rollouts > 0 and self._rollout_graph_ok():
+                    # captured after one eager rollout has initialised everything lazily built
+                    graph = self._rollout_graph = _RolloutGraph(self, obs, critic_obs, cur_reward_sum,
+                                                                cur_episode_length)
+                if graph is not None:
+                    obs, critic_obs = graph.replay()
                     if self.log_dir is not None:
-                        if "episode" in infos:
-                            ep_infos.append(infos["episode"])
-                        cur_reward_sum += rewards
-                        cur_episode_length += 1
-                        new_ids = (dones > 0).nonzero(as_tuple=False)
-                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
-                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
-                        cur_reward_sum[new_ids] = 0
-                        cur_episode_length[new_ids] = 0
+                        ep_infos.extend(graph.ep_infos)
+                        graph.finished_episodes(rewbuffer, lenbuffer)
+                else:
+                    for _ in range(self.num_steps_per_env):
+                        obs, critic_obs, rewards, dones, infos = self._collect_step(obs, critic_obs)
+                        if self.log_dir is not None:
+                            if "episode" in infos:
+                                ep_infos.append(infos["episode"])
+                            cur_reward_sum += rewards
+                            cur_episode_length += 1
+                            new_ids = (dones > 0).nonzero(as_tuple=False)
+                            rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                            lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                            cur_reward_sum[new_ids] = 0
+                            cur_episode_length[new_ids] = 0
+                    self._eager_rollouts += 1
                 sync()
                 stop = time.time()
                 collection_time = stop - start
@@ -122,6 +206,24 @@ class OnPolicyRunner:
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))
+
+    def _collect_step(self, obs, critic_obs):
+        """One step of the reference's collection loop (on_policy_runner.py:106-114)."""
+        actions = self.alg.act(obs, critic_obs)
+        obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
+        critic_obs = privileged_obs if privileged_obs is not None else obs
+        obs, critic_obs, rewards, dones = (obs.to(self.device), critic_obs.to(self.device),
+                                           rewards.to(self.device), dones.to(self.device))
+        self.alg.process_env_step(rewards, dones, infos)
+        return obs, critic_obs, rewards, dones, infos
+
+    def _rollout_graph_ok(self):
+        """The whole collection loop replays as one HIP graph when nothing in it needs
+        the host: a CUDA device, a feed-forward policy, and an env whose step keys its
+        noise on a device-side counter (LeggedRobot.account_replayed_steps)."""
+        return (bool(self.cfg.get("rollout_graph", True)) and str(self.device).startswith("cuda")
+                and not self.alg.actor_critic.is_recurrent and hasattr(self.env, "account_replayed_steps")
+                and self.alg.storage is not None)
 
     def log(self, locs, width=80, pad=35):
         ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
