@@ -47,11 +47,14 @@ PMLP_API const char* pmlp_last_error(void);
 
 /* fp32 x[M,K] (ld ldx) -> bf16 y[M,Kp] (ld Kp; columns K..Kp-1 zero) and/or
  * y^T[Kp,ldyt] (rows K..Kp-1 and columns M..ldyt-1 zero); y or yt may be NULL.
+ * rows (optional, int64[M]): output row m is input row rows[m] (the PPO
+ * mini-batch gather of RolloutStorage.mini_batch_generator fused in).
  * Used for observations, output gradients and weights (W and W^T).          */
 typedef struct {
     const float* x;
     pmlp_bf16* y;
     pmlp_bf16* yt;
+    const int64_t* rows;
     int32_t M, K, ldx, Kp, ldyt;
 } pmlp_convert_job;
 PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream);
@@ -97,6 +100,9 @@ PMLP_API int pmlp_rowsum(int32_t njobs, const pmlp_rowsum_job* jobs, void* strea
  * (ratio, clipped surrogate, optionally clipped value loss, entropy bonus,
  * and the KL the adaptive learning rate reads).  Inputs fp32, row-major:
  * mu/actions/old_mu/old_sigma [M,A], stdv [A], value/old_logp/adv/ret/target [M].
+ * rows (optional, int64[M]): the rollout inputs actions, old_logp, old_mu,
+ * old_sigma, adv, ret and target are read at row rows[i] (flat T*N storage);
+ * mu and value are the mini-batch's own rows.
  * fwd: loss[1]; stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean};
  *      partial = scratch of 4*pmlp_ppo_loss_blocks(M) floats.
  * bwd: gout = device scalar d(total)/d(loss); dmu [M,A], dvalue [M], dstd [A];
@@ -104,13 +110,40 @@ PMLP_API int pmlp_rowsum(int32_t njobs, const pmlp_rowsum_job* jobs, void* strea
 PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M);
 PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
+                               const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                               float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
                                float* stats, void* stream);
 PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
-                               float* dvalue, float* partial_std, float* dstd, void* stream);
+                               const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                               float clip, int32_t clipped_value, float vcoef, float ecoef, const float* gout,
+                               float* dmu, float* dvalue, float* partial_std, float* dstd, void* stream);
+
+/* One optimizer step over FLAT fp32 parameter / gradient / moment buffers of n
+ * entries (nn.utils.clip_grad_norm_ then torch.optim.Adam, amsgrad off, no
+ * weight decay; rsl_rl v1.0.2 PPO.update).  grad_scale multiplies the gradient
+ * first (1/world_size after an all-reduce sum).
+ * pmlp_opt_prepare: partial[pmlp_opt_parts()] = squared-norm partials; step[0] += 1;
+ *   with stats = [surrogate, value, kl, entropy] (scaled by grad_scale too):
+ *   acc[0] += value loss, acc[1] += surrogate loss (acc may be NULL), and when
+ *   adaptive != 0 the KL rule of rsl_rl's adaptive schedule updates lr[0].
+ * pmlp_adam: clip coefficient min(1, max_norm/(|g|+1e-6)) (max_norm <= 0: no
+ *   clipping), then Adam with bias corrections from step[0] and lr[0].        */
+PMLP_API int32_t pmlp_opt_parts(void);
+PMLP_API int pmlp_opt_prepare(const float* grad, int64_t n, float grad_scale, float* partial, float* step,
+                              const float* stats, float* lr, float* acc, float desired_kl, int32_t adaptive,
+                              void* stream);
+PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float grad_scale, const float* partial, const float* step, const float* lr, float max_norm,
+                       float beta1, float beta2, float eps, void* stream);
+
+/* RolloutStorage.compute_returns (rsl_rl v1.0.2): GAE(gamma, lam) over [T,N]
+ * rewards/dones(bool bytes)/values with last_values[N], writing returns and
+ * advantages, then advantages normalised by their mean and unbiased std.
+ * partial: 2 * pmlp_gae_parts(N) doubles of scratch.                        */
+PMLP_API int32_t pmlp_gae_parts(int32_t num_envs);
+PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                      float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
+                      double* partial, void* stream);
 
 #endif

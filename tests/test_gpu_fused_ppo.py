@@ -1,0 +1,173 @@
+"""The fused PPO optimizer step (rsl_rl/algorithms/fused_step.py: gathered bf16
+MFMA forward/backward, fused loss, flat clip_grad_norm_ + Adam, GAE kernel)
+against the reference's torch statement of the same update (fp32 autograd,
+nn.utils.clip_grad_norm_, torch.optim.Adam, RolloutStorage.compute_returns)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from rsl_rl.algorithms import PPO  # noqa: E402
+from rsl_rl.algorithms import fused_step  # noqa: E402
+from rsl_rl.modules import ActorCritic, mfma_mlp  # noqa: E402
+from rsl_rl.storage import RolloutStorage  # noqa: E402
+
+
+def _fill_storage(alg, T, N, O, A, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    st = alg.storage
+    with torch.inference_mode():
+        for _ in range(T):
+            obs = torch.randn(N, O, device="cuda", generator=g)
+            alg.act(obs, obs)
+            alg.transition.actions = alg.transition.action_mean + 0.3 * torch.randn(N, A, device="cuda", generator=g)
+            alg.transition.actions_log_prob = alg.actor_critic.get_actions_log_prob(alg.transition.actions).detach()
+            rew = 0.2 * torch.randn(N, device="cuda", generator=g)
+            done = torch.rand(N, device="cuda", generator=g) < 0.05
+            alg.process_env_step(rew, done, {"time_outs": done & (torch.rand(N, device="cuda", generator=g) < 0.5)})
+        alg.compute_returns(torch.randn(N, O, device="cuda", generator=g))
+    return {k: v.clone() for k, v in st.__dict__.items() if torch.is_tensor(v) and not k.startswith("_")}
+
+
+@pytest.mark.parametrize("schedule", ["fixed", "adaptive"])
+def test_fused_step_matches_fp32_autograd_update(schedule):
+    """One update (1 epoch x 2 mini-batches) from identical weights and rollout:
+    losses, learning rate and every parameter after the two Adam steps agree with
+    the fp32 torch update within bf16 GEMM rounding."""
+    torch.manual_seed(0)
+    N, T, O, A = 1024, 8, 48, 12
+    ac32 = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128], mixed_precision=False).cuda()
+    acbf = copy.deepcopy(ac32)
+    acbf.mixed_precision = True
+    kw = dict(num_learning_epochs=1, num_mini_batches=2, learning_rate=1e-3, schedule=schedule, device="cuda")
+    ref = PPO(ac32, fused_loss=False, **kw)
+    ref.use_graph = False
+    fus = PPO(acbf, **kw)
+    for alg in (ref, fus):
+        alg.init_storage(N, T, [O], [None], [A])
+    assert fus._fused is not None and ref._fused is None
+    data = _fill_storage(ref, T, N, O, A, seed=1)
+    for k, v in data.items():  # identical rollout for both
+        getattr(fus.storage, k).copy_(v)
+    fus.storage.step = T
+    p0 = [p.detach().clone() for p in ref.actor_critic.parameters()]
+    torch.manual_seed(7)
+    l_ref = ref.update()
+    torch.manual_seed(7)
+    l_fus = fus.update()
+    np.testing.assert_allclose(l_fus, l_ref, rtol=2e-2, atol=2e-3)
+    assert fus.learning_rate == pytest.approx(ref.learning_rate, rel=1e-6)
+    lr = 1e-3
+    for a, b, c in zip(ref.actor_critic.parameters(), fus.actor_critic.parameters(), p0):
+        da, db = (a.detach() - c), (b.detach() - c)
+        assert da.abs().max() > 0
+        # Adam steps are ~lr per entry: a flipped near-zero gradient moves an entry by up to 2 lr per step
+        bad = ((da - db).abs() > 0.2 * lr).float().mean().item()
+        assert bad < 0.02, bad
+        assert (da - db).abs().max() <= 4 * 3 * lr
+
+
+def test_adam_kernel_matches_torch_adam_with_clipping():
+    """pmlp_opt_prepare + pmlp_adam == nn.utils.clip_grad_norm_ + torch.optim.Adam (fp32)
+    over several steps with changing gradients, on flat buffers."""
+    lib = mfma_mlp.load()
+    torch.manual_seed(0)
+    n = 100_003
+    p_ref = torch.nn.Parameter(torch.randn(n, device="cuda"))
+    lr = torch.tensor(3e-3, device="cuda")
+    opt = torch.optim.Adam([p_ref], lr=3e-3)
+    p = p_ref.detach().clone()
+    m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    step = torch.zeros((), device="cuda")
+    part = torch.empty(lib.pmlp_opt_parts(), device="cuda")
+    for it in range(5):
+        g = torch.randn(n, device="cuda") * (0.5 if it % 2 else 0.002)  # clipped and unclipped steps
+        p_ref.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_([p_ref], 1.0)
+        opt.step()
+        s = mfma_mlp._stream()
+        P = mfma_mlp._p
+        mfma_mlp._ok(lib.pmlp_opt_prepare(P(g), n, 1.0, P(part), P(step), None, P(lr), None, 0.0, 0, s), "prep")
+        mfma_mlp._ok(lib.pmlp_adam(P(p), P(g), P(m), P(v), n, 1.0, P(part), P(step), P(lr), 1.0, 0.9, 0.999, 1e-8, s),
+                     "adam")
+        torch.testing.assert_close(p, p_ref.detach(), rtol=1e-5, atol=1e-6)
+        st = opt.state[p_ref]
+        torch.testing.assert_close(m, st["exp_avg"], rtol=1e-5, atol=1e-8)
+        torch.testing.assert_close(v, st["exp_avg_sq"], rtol=1e-5, atol=1e-10)
+    assert float(step) == 5.0
+
+
+@pytest.mark.parametrize("T,N", [(24, 4096), (7, 333)])
+def test_gae_kernel_matches_storage_compute_returns(T, N):
+    torch.manual_seed(0)
+    sts = [RolloutStorage(N, T, [3], [None], [2], "cuda") for _ in range(2)]
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rew = torch.randn(T, N, 1, device="cuda", generator=g)
+    done = torch.rand(T, N, 1, device="cuda", generator=g) < 0.1
+    val = torch.randn(T, N, 1, device="cuda", generator=g)
+    last = torch.randn(N, 1, device="cuda", generator=g)
+    for st in sts:
+        st.rewards.copy_(rew)
+        st.dones.copy_(done)
+        st.values.copy_(val)
+    sts[0].compute_returns(last, 0.99, 0.95)
+    fused_step.gae(sts[1], last, 0.99, 0.95)
+    torch.testing.assert_close(sts[1].returns, sts[0].returns, rtol=0, atol=1e-5)
+    torch.testing.assert_close(sts[1].advantages, sts[0].advantages, rtol=0, atol=1e-4)
+
+
+def test_fused_update_graph_is_bitwise_eager():
+    """Replaying the captured fused update == running the same fused steps eagerly."""
+    torch.manual_seed(0)
+    N, T, O, A = 2048, 8, 48, 12
+    ac = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda()
+    algs = []
+    for graph in (True, False):
+        alg = PPO(copy.deepcopy(ac), num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3,
+                  schedule="adaptive", device="cuda")
+        alg.use_graph = graph
+        alg.init_storage(N, T, [O], [None], [A])
+        algs.append(alg)
+    for u in range(4):
+        data = _fill_storage(algs[1], T, N, O, A, seed=10 + u)
+        for k, v in data.items():
+            getattr(algs[0].storage, k).copy_(v)
+        algs[0].storage.step = T
+        torch.manual_seed(100 + u)
+        lg = algs[0].update()
+        torch.manual_seed(100 + u)
+        le = algs[1].update()
+        assert lg == le
+        for a, b in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
+            assert torch.equal(a, b)
+    assert algs[0]._fgraph is not None and algs[1]._fgraph is None
+
+
+def test_fused_checkpoint_roundtrip(tmp_path):
+    """state_dicts keep the reference structure and a reload lands in the flat buffers."""
+    torch.manual_seed(0)
+    N, T, O, A = 512, 8, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [128, 64], [128, 64]).cuda(), num_learning_epochs=1, num_mini_batches=2,
+              device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    _fill_storage(alg, T, N, O, A, seed=2)
+    alg.update()
+    path = tmp_path / "ck.pt"
+    torch.save({"model_state_dict": alg.actor_critic.state_dict(),
+                "optimizer_state_dict": alg.optimizer.state_dict()}, path)
+    ck = torch.load(path, map_location="cuda", weights_only=True)
+    assert set(ck["model_state_dict"]) == set(alg.actor_critic.state_dict())
+    alg2 = PPO(ActorCritic(O, O, A, [128, 64], [128, 64]).cuda(), num_learning_epochs=1, num_mini_batches=2,
+               device="cuda")
+    alg2.init_storage(N, T, [O], [None], [A])
+    alg2.actor_critic.load_state_dict(ck["model_state_dict"])
+    alg2.optimizer.load_state_dict(ck["optimizer_state_dict"])
+    alg2._fused.sync_optimizer_state(alg2.optimizer)
+    for a, b in zip(alg.actor_critic.parameters(), alg2.actor_critic.parameters()):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(alg2._fused.exp_avg, alg._fused.exp_avg)
+    torch.testing.assert_close(alg2._fused.exp_avg_sq, alg._fused.exp_avg_sq)
+    assert float(alg2._fused.step_t) == float(alg._fused.step_t) == 2.0

@@ -235,6 +235,7 @@ struct CvtJob {
     const float* x;
     bf16* y;
     bf16* yt;
+    const int64_t* rows;  // optional gather: row m of the output is row rows[m] of x
     int M, K, ldx, Kp, ldyt;
 };
 struct CvtJobs {
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
     for (int r = ty; r < 64; r += 4) {
         const int m = m0 + r, k = k0 + tx;
         float v = 0.f;
-        if (m < J.M && k < J.K) v = J.x[(size_t)m * J.ldx + k];
+        if (m < J.M && k < J.K) v = J.x[(size_t)(J.rows ? J.rows[m] : m) * J.ldx + k];
         tile[r][tx] = v;
         if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v;
     }
@@ -318,8 +319,10 @@ __global__ __launch_bounds__(256) void k_rowsum_jobs(SumJobs jobs) {
 #define PMLP_LOSS_THREADS 256
 struct LossArgs {
     const float *mu, *stdv, *value, *actions, *old_logp, *old_mu, *old_sigma, *adv, *ret, *target;
+    const int64_t* rows;  // optional: rollout inputs (actions .. target) are read at row rows[i]
     int M, A, clipped_value;
     float clip, vcoef, ecoef;
+    __device__ size_t src(int i) const { return rows ? (size_t)rows[i] : (size_t)i; }
 };
 static constexpr float kHalfLog2Pi = 0.91893853320467274f;  // log(sqrt(2 pi))
 
@@ -338,21 +341,22 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_fwd(LossArgs a, 
     const int i = blockIdx.x * PMLP_LOSS_THREADS + threadIdx.x;
     float surr = 0.f, vl = 0.f, kl = 0.f;
     if (i < a.M) {
+        const size_t si = a.src(i);
         float logp = 0.f;
         for (int k = 0; k < a.A; ++k) {
             const float sg = a.stdv[k], mu = a.mu[(size_t)i * a.A + k];
-            const float d = a.actions[(size_t)i * a.A + k] - mu;
+            const float d = a.actions[si * a.A + k] - mu;
             logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
-            const float os = a.old_sigma[(size_t)i * a.A + k], om = a.old_mu[(size_t)i * a.A + k] - mu;
+            const float os = a.old_sigma[si * a.A + k], om = a.old_mu[si * a.A + k] - mu;
             kl += logf(sg / os + 1.0e-5f) + (os * os + om * om) / (2.f * sg * sg) - 0.5f;
         }
-        const float ratio = expf(logp - a.old_logp[i]);
-        const float adv = a.adv[i];
+        const float ratio = expf(logp - a.old_logp[si]);
+        const float adv = a.adv[si];
         const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip);
         surr = fmaxf(s1, s2);
-        const float v = a.value[i], r = a.ret[i];
+        const float v = a.value[i], r = a.ret[si];
         if (a.clipped_value) {
-            const float t = a.target[i];
+            const float t = a.target[si];
             const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
             vl = fmaxf((v - r) * (v - r), (vc - r) * (vc - r));
         } else {
@@ -405,15 +409,16 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_bwd(LossArgs a, 
     const float g = gout[0];
     const float gs = g / (float)a.M, gv = g * a.vcoef / (float)a.M;
     float dlogp = 0.f;
+    const size_t si = i < a.M ? a.src(i) : 0;
     if (i < a.M) {
         float logp = 0.f;
         for (int k = 0; k < a.A; ++k) {
             const float sg = a.stdv[k];
-            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
             logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
         }
-        const float ratio = expf(logp - a.old_logp[i]);
-        const float adv = a.adv[i];
+        const float ratio = expf(logp - a.old_logp[si]);
+        const float adv = a.adv[si];
         const float lo = 1.f - a.clip, hi = 1.f + a.clip;
         const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, lo), hi);
         float w1, w2;
@@ -422,13 +427,13 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_bwd(LossArgs a, 
         dlogp = gs * (-adv) * (w1 + w2 * dclamp) * ratio;
         for (int k = 0; k < a.A; ++k) {
             const float sg = a.stdv[k];
-            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
             dmu[(size_t)i * a.A + k] = dlogp * d / (sg * sg);
         }
-        const float v = a.value[i], r = a.ret[i];
+        const float v = a.value[i], r = a.ret[si];
         float dv;
         if (a.clipped_value) {
-            const float t = a.target[i];
+            const float t = a.target[si];
             const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
             float u1, u2;
             max_weights((v - r) * (v - r), (vc - r) * (vc - r), u1, u2);
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_bwd(LossArgs a, 
         float c = 0.f;
         if (i < a.M) {
             const float sg = a.stdv[k];
-            const float d = a.actions[(size_t)i * a.A + k] - a.mu[(size_t)i * a.A + k];
+            const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
             c = dlogp * (d * d / (sg * sg * sg) - 1.f / sg);
         }
         c = block_sum(c, sh);
@@ -462,6 +467,139 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_std(LossArgs a, 
         c = block_sum(c, sh);
         if (threadIdx.x == 0) dstd[k] = c - a.ecoef * gout[0] / a.stdv[k];  // + entropy term
     }
+}
+
+// ------------------------------------------------------------ optimizer --
+// One PPO optimizer step over the FLAT parameter/gradient buffers (every
+// actor/critic parameter is a view of one fp32 buffer): clip_grad_norm_ +
+// torch.optim.Adam (amsgrad off, no weight decay) in two launches.
+#define PMLP_OPT_THREADS 256
+#define PMLP_OPT_PARTS 256
+
+// partial[b] = sum of (scale*g)^2 over block b's grid-stride share; block 0 also
+// advances Adam's step and, from stats = [surrogate, value, kl, entropy] (sums over
+// ranks when scale = 1/world), accumulates the logged losses and adapts the LR.
+__global__ __launch_bounds__(PMLP_OPT_THREADS) void k_opt_prepare(const float* __restrict__ g, int64_t n, float scale,
+                                                                  float* __restrict__ partial, float* step,
+                                                                  const float* stats, float* lr, float* acc,
+                                                                  float desired_kl, int adaptive) {
+    __shared__ float sh[4];
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * PMLP_OPT_THREADS) {
+        const float v = g[i] * scale;
+        s += v * v;
+    }
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        step[0] += 1.f;
+        if (stats) {
+            if (acc) {
+                acc[0] += stats[1] * scale;
+                acc[1] += stats[0] * scale;
+            }
+            if (adaptive) {  // rsl_rl v1.0.2 PPO.update: KL-adaptive learning rate
+                const float kl = stats[2] * scale;
+                float l = lr[0];
+                if (kl > desired_kl * 2.f) l = fmaxf(l / 1.5f, 1e-5f);
+                else if (kl < desired_kl / 2.f && kl > 0.f) l = fminf(l * 1.5f, 1e-2f);
+                lr[0] = l;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                           float scale, const float* __restrict__ partial, int nparts,
+                                                           const float* step, const float* lr, float max_norm,
+                                                           float b1, float b2, float eps) {
+    __shared__ float sh[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += PMLP_OPT_THREADS) s += partial[i];
+    s = block_sum(s, sh);
+    float coef = scale;
+    if (max_norm > 0.f) coef = scale * fminf(max_norm / (sqrtf(s) + 1e-6f), 1.f);  // clip_grad_norm_
+    const float t = step[0];
+    const float bc1 = 1.f - powf(b1, t), bc2s = sqrtf(1.f - powf(b2, t));
+    const float step_size = lr[0] / bc1;
+    for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * PMLP_OPT_THREADS) {
+        const float gi = g[i] * coef;
+        const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] -= step_size * (mi / (sqrtf(vi) / bc2s + eps));
+    }
+}
+
+// ----------------------------------------------------------------- GAE --
+// RolloutStorage.compute_returns: one thread per env walks t backwards; the
+// advantage sums for the normalisation go to per-block fp64 partials.
+__global__ __launch_bounds__(PMLP_OPT_THREADS) void k_gae(const float* __restrict__ rew,
+                                                          const uint8_t* __restrict__ dones,
+                                                          const float* __restrict__ values,
+                                                          const float* __restrict__ last_values,
+                                                          float* __restrict__ ret, float* __restrict__ adv, int T,
+                                                          int N, float gamma, float lam, double* __restrict__ partial) {
+#pragma clang fp contract(off)
+    __shared__ double shd[2][4];
+    const int e = blockIdx.x * PMLP_OPT_THREADS + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    if (e < N) {
+        float a = 0.f;
+        for (int t = T - 1; t >= 0; --t) {
+            const size_t i = (size_t)t * N + e;
+            const float next = t == T - 1 ? last_values[e] : values[i + N];
+            const float nt = 1.f - (dones[i] ? 1.f : 0.f);
+            const float delta = (rew[i] + (nt * gamma) * next) - values[i];
+            a = delta + ((nt * gamma) * lam) * a;
+            const float r = a + values[i];
+            ret[i] = r;
+            const float ad = r - values[i];
+            adv[i] = ad;
+            s1 += ad;
+            s2 += (double)ad * ad;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off);
+        s2 += __shfl_xor(s2, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        shd[0][threadIdx.x >> 6] = s1;
+        shd[1][threadIdx.x >> 6] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = (shd[0][0] + shd[0][1]) + (shd[0][2] + shd[0][3]);
+        partial[2 * blockIdx.x + 1] = (shd[1][0] + shd[1][1]) + (shd[1][2] + shd[1][3]);
+    }
+}
+
+// adv = (adv - mean) / (std + 1e-8), unbiased std over all T*N advantages
+__global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adv_norm(float* __restrict__ adv, int64_t n,
+                                                               const double* __restrict__ partial, int nparts) {
+    __shared__ double sh[2];
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int i = 0; i < nparts; ++i) {
+            a += partial[2 * i];
+            b += partial[2 * i + 1];
+        }
+        sh[0] = a;
+        sh[1] = b;
+    }
+    __syncthreads();
+    const double mean = sh[0] / (double)n;
+    const double var = (sh[1] - (double)n * mean * mean) / (double)(n - 1);
+    const float meanf = (float)mean, den = (float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f;
+    for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * PMLP_OPT_THREADS)
+        adv[i] = (adv[i] - meanf) / den;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -489,7 +627,7 @@ PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* str
         const pmlp_convert_job& J = jobs[i];
         if (!J.x || J.M <= 0 || J.K <= 0 || J.Kp < J.K || J.ldx < J.K || (!J.y && !J.yt) || (J.yt && J.ldyt < J.M))
             return fail(-1, "pmlp_convert: bad job " + std::to_string(i));
-        cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0};
+        cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.rows, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0};
         maxm = std::max(maxm, std::max(J.M, J.yt ? J.ldyt : 0));
         maxk = std::max(maxk, J.Kp);
     }
@@ -577,12 +715,12 @@ PMLP_API int pmlp_rowsum(int32_t njobs, const pmlp_rowsum_job* jobs, void* strea
 
 static int loss_args(LossArgs& a, const float* mu, const float* stdv, const float* value, const float* actions,
                      const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                     const float* ret, const float* target, int32_t M, int32_t A, float clip, int32_t clipped_value,
-                     float vcoef, float ecoef) {
+                     const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A, float clip,
+                     int32_t clipped_value, float vcoef, float ecoef) {
     if (!mu || !stdv || !value || !actions || !old_logp || !old_mu || !old_sigma || !adv || !ret ||
         (clipped_value && !target) || M <= 0 || A <= 0)
         return fail(-1, "pmlp_ppo_loss: null input or empty batch");
-    a = LossArgs{mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clipped_value,
+    a = LossArgs{mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clipped_value,
                  clip, vcoef, ecoef};
     return 0;
 }
@@ -591,11 +729,11 @@ PMLP_API int32_t pmlp_ppo_loss_blocks(int32_t M) { return (M + PMLP_LOSS_THREADS
 
 PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* value, const float* actions,
                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
+                               const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                               float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial, float* loss,
                                float* stats, void* stream) {
     LossArgs a;
-    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clip,
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
                           clipped_value, vcoef, ecoef))
         return e;
     if (!partial || !loss || !stats) return fail(-1, "pmlp_ppo_loss_fwd: null output");
@@ -609,11 +747,11 @@ PMLP_API int pmlp_ppo_loss_fwd(const float* mu, const float* stdv, const float* 
 
 PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* value, const float* actions,
                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                               const float* ret, const float* target, int32_t M, int32_t A, float clip,
-                               int32_t clipped_value, float vcoef, float ecoef, const float* gout, float* dmu,
-                               float* dvalue, float* partial_std, float* dstd, void* stream) {
+                               const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                               float clip, int32_t clipped_value, float vcoef, float ecoef, const float* gout,
+                               float* dmu, float* dvalue, float* partial_std, float* dstd, void* stream) {
     LossArgs a;
-    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, M, A, clip,
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
                           clipped_value, vcoef, ecoef))
         return e;
     if (!gout || !dmu || !dvalue || !partial_std || !dstd) return fail(-1, "pmlp_ppo_loss_bwd: null output");
@@ -623,6 +761,50 @@ PMLP_API int pmlp_ppo_loss_bwd(const float* mu, const float* stdv, const float* 
     hipLaunchKernelGGL(k_ppo_loss_std, dim3(1), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, gout,
                        partial_std, nb, dstd);
     PMLP_CHECK_LAUNCH("pmlp_ppo_loss_bwd");
+    return 0;
+}
+
+PMLP_API int32_t pmlp_opt_parts(void) { return PMLP_OPT_PARTS; }
+
+PMLP_API int pmlp_opt_prepare(const float* grad, int64_t n, float grad_scale, float* partial, float* step,
+                              const float* stats, float* lr, float* acc, float desired_kl, int32_t adaptive,
+                              void* stream) {
+    if (!grad || n <= 0 || !partial || !step || (adaptive && (!stats || !lr)))
+        return fail(-1, "pmlp_opt_prepare: null buffer or empty parameter set");
+    hipLaunchKernelGGL(k_opt_prepare, dim3(PMLP_OPT_PARTS), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, grad, n,
+                       grad_scale, partial, step, stats, lr, acc, desired_kl, adaptive);
+    PMLP_CHECK_LAUNCH("pmlp_opt_prepare");
+    return 0;
+}
+
+PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float grad_scale, const float* partial, const float* step, const float* lr, float max_norm,
+                       float beta1, float beta2, float eps, void* stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !partial || !step || !lr)
+        return fail(-1, "pmlp_adam: null buffer or empty parameter set");
+    const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
+                       exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps);
+    PMLP_CHECK_LAUNCH("pmlp_adam");
+    return 0;
+}
+
+PMLP_API int32_t pmlp_gae_parts(int32_t num_envs) { return (num_envs + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS; }
+
+PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                      float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
+                      double* partial, void* stream) {
+    if (!rewards || !dones || !values || !last_values || !returns || !advantages || !partial || T <= 0 || N <= 0 ||
+        (int64_t)T * N < 2)
+        return fail(-1, "pmlp_gae: null buffer or empty rollout");
+    const int nb = pmlp_gae_parts(N);
+    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, rewards, dones, values,
+                       last_values, returns, advantages, T, N, gamma, lam, partial);
+    const int64_t n = (int64_t)T * N;
+    const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    hipLaunchKernelGGL(k_adv_norm, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, advantages, n,
+                       partial, nb);
+    PMLP_CHECK_LAUNCH("pmlp_gae");
     return 0;
 }
 

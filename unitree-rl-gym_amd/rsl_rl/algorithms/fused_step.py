@@ -1,0 +1,257 @@
+"""One PPO mini-batch optimizer step of the Gaussian MLP actor-critic as ~20
+kernel launches, with no autograd and no torch glue (rsl_rl v1.0.2
+PPO.update body).
+
+What the reference does per mini-batch:
+    gather the rollout rows -> actor/critic forward -> loss -> backward ->
+    clip_grad_norm_ -> Adam
+What runs here (csrc/ppo_mlp.hip through include/ppo_mlp.h):
+    1 convert   observations gathered by the mini-batch index (fused gather)
+                + every weight and weight^T to bf16
+    L GEMMs     forward, actor and critic sharing every launch
+    2 + 2       loss forward (+ final) / backward (+ std gradient); the loss
+                reads actions, old log-probs, advantages, ... through the index
+    1 convert   output gradients to bf16
+    2L-1 GEMMs  weight-gradient slabs and input gradients
+    2           slab combine + bias sums, written into the flat gradient
+    2           grad-norm partials (+ step/LR/loss bookkeeping) and Adam
+
+Every parameter is a view of ONE flat fp32 buffer (`flat`), every gradient a view
+of another (`grad`, whose 4-float tail holds the loss statistics), and Adam's
+moments are flat too.  The module's parameters, state_dict and the optimizer's
+state_dict keep their reference structure: the Parameters are the same objects
+(`.data` re-pointed) and the torch Adam's per-parameter state entries are views
+of the flat moments.  With torch.distributed the gradient (and the statistics
+tail) is all-reduced as one bucket and averaged inside the kernels.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from rsl_rl.modules import mfma_mlp as mm
+
+
+def _ceil8(n):
+    return (n + 7) // 8 * 8
+
+
+class FusedPPOStep:
+    def __init__(self, alg, mini_batch_size):
+        ac = alg.actor_critic
+        seqs = [ac.actor, ac.critic]
+        if not all(mm.supported(s) for s in seqs):
+            raise ValueError("fused PPO step: actor/critic must be Linear/ELU MLPs")
+        self.lins = [[m for m in s if isinstance(m, nn.Linear)] for s in seqs]
+        if len(self.lins[0]) != len(self.lins[1]):
+            raise ValueError("fused PPO step: actor and critic must have the same depth")
+        params = [p for ls in self.lins for lin in ls for p in (lin.weight, lin.bias)] + [ac.std]
+        if sorted(map(id, params)) != sorted(map(id, ac.parameters())):
+            raise ValueError("fused PPO step: unexpected parameter set")
+        self.alg, self.ac, self.M = alg, ac, int(mini_batch_size)
+        if self.M % 8:
+            raise ValueError("fused PPO step: mini-batch size must be a multiple of 8")
+        dev = ac.std.device
+        self.dev = dev
+        n = sum(p.numel() for p in params)
+        self.n = n
+        self.flat = torch.empty(n, device=dev)
+        self.grad = torch.zeros(n + 4, device=dev)  # tail: [surrogate, value, kl, entropy]
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        self.step_t = torch.zeros((), device=dev)
+        self.params = params
+        self._gview, self._mview, self._vview = {}, {}, {}
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                v = self.flat[off:off + k].view_as(p)
+                v.copy_(p.data)
+                p.data = v
+                p.grad = self.grad[off:off + k].view_as(p)
+                self._gview[id(p)] = p.grad
+                self._mview[id(p)] = self.exp_avg[off:off + k].view_as(p)
+                self._vview[id(p)] = self.exp_avg_sq[off:off + k].view_as(p)
+                off += k
+        self.stats = self.grad[n:n + 4]
+        self.sync_optimizer_state(alg.optimizer)
+        self._alloc()
+
+    # ------------------------------------------------------------ buffers --
+    def _alloc(self):
+        M, dev, bf = self.M, self.dev, torch.bfloat16
+        L = len(self.lins[0])
+        self.L = L
+        self.k0p = [_ceil8(ls[0].in_features) for ls in self.lins]
+        self.xb = [torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
+        self.xt = [torch.empty(k, M, dtype=bf, device=dev) for k in self.k0p]
+        self.wb = [[torch.empty(lin.out_features, self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
+                    for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
+        self.wt = [[torch.empty(lin.in_features, _ceil8(lin.out_features), dtype=bf, device=dev) if l > 0 else None
+                    for l, lin in enumerate(ls)] for ls in self.lins]
+        self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
+        self.yt = [[torch.empty(lin.out_features, M, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
+        self.out = [torch.empty(M, ls[-1].out_features, device=dev) for ls in self.lins]
+        A = self.lins[0][-1].out_features
+        if self.lins[1][-1].out_features != 1:
+            raise ValueError("fused PPO step: the critic must output one value")
+        nb = mm.load().pmlp_ppo_loss_blocks(M)
+        self.loss_partial = torch.empty(4 * nb, device=dev)
+        self.loss = torch.empty((), device=dev)
+        self.one = torch.ones((), device=dev)
+        self.dmu = torch.empty(M, A, device=dev)
+        self.dvalue = torch.empty(M, 1, device=dev)
+        self.std_partial = torch.empty(A * nb, device=dev)
+        # output gradients (bf16, both layouts) and the hidden-layer input gradients
+        self.dz_out = [torch.empty(M, _ceil8(ls[-1].out_features), dtype=bf, device=dev) for ls in self.lins]
+        self.dzt_out = [torch.empty(_ceil8(ls[-1].out_features), M, dtype=bf, device=dev) for ls in self.lins]
+        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 0 else None
+                    for l, lin in enumerate(ls)] for ls in self.lins]
+        self.dzt = [[torch.empty(lin.in_features, M, dtype=bf, device=dev) if l > 0 else None
+                     for l, lin in enumerate(ls)] for ls in self.lins]
+        # split-K weight-gradient slabs; layers whose padded width differs from the
+        # parameter's get a staging buffer (copied into the flat gradient)
+        self.ks, self.slab, self.dw_stage = [], [], []
+        for l in range(L):
+            kps = [self.k0p[n] if l == 0 else self.lins[n][l].in_features for n in range(2)]
+            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n]) for n in range(2)))
+            nsl = (M + ks - 1) // ks
+            self.ks.append(ks)
+            self.slab.append([torch.empty(nsl, self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
+            self.dw_stage.append([None if kps[n] == self.lins[n][l].in_features else
+                                  torch.empty(self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
+        self.opt_partial = torch.empty(mm.load().pmlp_opt_parts(), device=dev)
+
+    # -------------------------------------------------------- optimizer state --
+    def sync_optimizer_state(self, opt):
+        """Point the torch Adam's per-parameter state at the flat moments (after
+        construction or an optimizer.load_state_dict, copying loaded values in)."""
+        with torch.no_grad():
+            for p in self.params:
+                st = opt.state.get(p)
+                m, v = self._mview[id(p)], self._vview[id(p)]
+                if st and st.get("exp_avg") is not None and st["exp_avg"].data_ptr() == m.data_ptr():
+                    continue
+                if st and "exp_avg" in st:
+                    m.copy_(st["exp_avg"])
+                    v.copy_(st["exp_avg_sq"])
+                    self.step_t.fill_(float(st["step"]))
+                opt.state[p] = {"step": self.step_t, "exp_avg": m, "exp_avg_sq": v}
+            for p in self.params:  # gradients must alias the flat buffer
+                if p.grad is None or p.grad.data_ptr() != self._gview[id(p)].data_ptr():
+                    p.grad = self._gview[id(p)]
+
+    # -------------------------------------------------------------- step ----
+    def run(self, rows, src, acc):
+        """One optimizer step on mini-batch rows `rows` (int64 [M]) of the flat rollout
+        `src` = (obs, critic_obs, actions, values, advantages, returns, log_prob, mu, sigma),
+        each [T*N, ...] fp32.  acc[0] += value loss, acc[1] += surrogate loss."""
+        alg, ac, M, L = self.alg, self.ac, self.M, self.L
+        obs, cobs, actions, values, adv, ret, logp, mu_old, sigma_old = src
+        shared = cobs is obs and self.k0p[0] == self.k0p[1]
+        lib = mm.load()
+        # 1. gathered observations + weights -> bf16
+        jobs = [(obs, self.k0p[0], self.xb[0], self.xt[0], rows)]
+        if not shared:
+            jobs.append((cobs, self.k0p[1], self.xb[1], self.xt[1], rows))
+        for n in range(2):
+            for l, lin in enumerate(self.lins[n]):
+                W = lin.weight.detach()
+                jobs.append((W, self.wb[n][l].shape[1], self.wb[n][l], None))
+                if l > 0:
+                    jobs.append((W, W.shape[1], None, self.wt[n][l]))
+        mm._convert(jobs)
+        xb = [self.xb[0], self.xb[0] if shared else self.xb[1]]
+        xt = [self.xt[0], self.xt[0] if shared else self.xt[1]]
+        # 2. forward
+        for l in range(L):
+            last = l == L - 1
+            gj = []
+            for n in range(2):
+                lin = self.lins[n][l]
+                a_in = xb[n] if l == 0 else self.y[n][l - 1]
+                K = self.k0p[n] if l == 0 else lin.in_features
+                if last:
+                    gj.append(dict(A=a_in, B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cf=self.out[n]))
+                else:
+                    gj.append(dict(A=a_in, B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cb=self.y[n][l], ct=self.yt[n][l]))
+            mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
+        # 3. loss forward / backward (rollout inputs read through `rows`)
+        A = self.out[0].shape[1]
+        std = ac.std.detach()
+        common = [mm._p(t) for t in (self.out[0], std, self.out[1], actions, logp, mu_old, sigma_old, adv, ret,
+                                     values)] + [mm._p(rows), M, A, float(alg.clip_param),
+                                                 int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
+                                                 float(alg.entropy_coef)]
+        st = mm._stream()
+        mm._ok(lib.pmlp_ppo_loss_fwd(*common, mm._p(self.loss_partial), mm._p(self.loss), mm._p(self.stats), st),
+               "pmlp_ppo_loss_fwd")
+        mm._ok(lib.pmlp_ppo_loss_bwd(*common, mm._p(self.one), mm._p(self.dmu), mm._p(self.dvalue),
+                                     mm._p(self.std_partial), mm._p(self._gview[id(ac.std)]), st), "pmlp_ppo_loss_bwd")
+        # 4. backward through both MLPs
+        mm._convert([(self.dmu, self.dz_out[0].shape[1], self.dz_out[0], self.dzt_out[0]),
+                     (self.dvalue, self.dz_out[1].shape[1], self.dz_out[1], self.dzt_out[1])])
+        dz, dzt = list(self.dz_out), list(self.dzt_out)
+        red, rsum, copies = [], [], []
+        for l in range(L - 1, -1, -1):
+            gj = []
+            for n in range(2):
+                lin = self.lins[n][l]
+                B = xt[n] if l == 0 else self.yt[n][l - 1]
+                kp = self.k0p[n] if l == 0 else lin.in_features
+                slab = self.slab[l][n]
+                gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab))
+                dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
+                red.append((slab, dw, lin.out_features * kp, slab.shape[0]))
+                rsum.append((dzt[n], self._gview[id(lin.bias)], lin.out_features))
+                if self.dw_stage[l][n] is not None:
+                    copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
+            mm._gemm(mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
+            if l > 0:
+                gj = []
+                for n in range(2):
+                    lin = self.lins[n][l]
+                    gj.append(dict(A=dz[n], B=self.wt[n][l], M=M, N=lin.in_features, K=dz[n].shape[1],
+                                   yprev=self.y[n][l - 1], cb=self.dz[n][l], ct=self.dzt[n][l]))
+                mm._gemm(mm.EPI_BWD_DX, gj)
+                dz = [self.dz[n][l] for n in range(2)]
+                dzt = [self.dzt[n][l] for n in range(2)]
+        mm._reduce(red)
+        mm._rowsum(rsum)
+        for dst, srcv in copies:
+            dst.copy_(srcv)
+        # 5. data-parallel: one bucket (gradient + loss statistics)
+        scale = 1.0
+        if alg.world_size > 1:
+            dist.all_reduce(self.grad)
+            scale = 1.0 / alg.world_size
+        # 6. clip_grad_norm_ + Adam
+        grp = alg.optimizer.param_groups[0]
+        b1, b2 = grp.get("betas", (0.9, 0.999))
+        eps = grp.get("eps", 1e-8)
+        adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
+        mm._ok(lib.pmlp_opt_prepare(mm._p(self.grad), self.n, scale, mm._p(self.opt_partial), mm._p(self.step_t),
+                                    mm._p(self.stats), mm._p(alg._lr), mm._p(acc),
+                                    float(alg.desired_kl if alg.desired_kl is not None else 0.0), adaptive, st),
+               "pmlp_opt_prepare")
+        max_norm = float(alg.max_grad_norm) if alg.max_grad_norm is not None else 0.0
+        mm._ok(lib.pmlp_adam(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg), mm._p(self.exp_avg_sq), self.n,
+                             scale, mm._p(self.opt_partial), mm._p(self.step_t), mm._p(alg._lr), max_norm, float(b1),
+                             float(b2), float(eps), st), "pmlp_adam")
+
+
+def gae(storage, last_values, gamma, lam):
+    """RolloutStorage.compute_returns on the GPU in two launches (pmlp_gae): GAE
+    backwards over T per env, then advantage normalisation."""
+    lib = mm.load()
+    T, N = storage.num_transitions_per_env, storage.num_envs
+    key = (T, N)
+    if getattr(storage, "_gae_partial_key", None) != key:
+        storage._gae_partial = torch.empty(2 * lib.pmlp_gae_parts(N), dtype=torch.float64, device=storage.device)
+        storage._gae_partial_key = key
+    lv = last_values.reshape(N).contiguous()
+    mm._ok(lib.pmlp_gae(mm._p(storage.rewards), mm._p(storage.dones), mm._p(storage.values), mm._p(lv),
+                        mm._p(storage.returns), mm._p(storage.advantages), T, N, float(gamma), float(lam),
+                        mm._p(storage._gae_partial), mm._stream()), "pmlp_gae")

@@ -16,6 +16,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.optim as optim
 
+from rsl_rl.algorithms import fused_step
 from rsl_rl.modules import ActorCritic
 from rsl_rl.modules import mfma_mlp
 from rsl_rl.storage import RolloutStorage
@@ -74,6 +75,8 @@ class PPO:
         # fused PPO-loss kernels for the Gaussian MLP policy on a GPU (fused_loss=False:
         # the torch statement of the loss, _reference_loss)
         self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "mean_and_value")
+        self._fused = None  # FusedPPOStep, built with the storage (init_storage)
+        self._fgraph = None
         self._diag, self._diag_i = None, 0
         self._graph_calls = 0
         self._capturing = False
@@ -96,6 +99,13 @@ class PPO:
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
                                       action_shape, self.device)
+        batch = num_envs * num_transitions_per_env
+        if self._fused_loss and not self.actor_critic.is_recurrent and self._fused is None and \
+                getattr(self.actor_critic, "mixed_precision", False) and batch % self.num_mini_batches == 0:
+            try:  # whole optimizer step in ~20 launches (algorithms/fused_step.py)
+                self._fused = fused_step.FusedPPOStep(self, batch // self.num_mini_batches)
+            except ValueError:
+                self._fused = None
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -139,6 +149,9 @@ class PPO:
 
     def compute_returns(self, last_critic_obs):
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        if self._fused is not None and self.world_size == 1:  # GAE + normalisation: two launches
+            fused_step.gae(self.storage, last_values, self.gamma, self.lam)
+            return
         stats = self._global_adv_stats if self.world_size > 1 else None
         self.storage.compute_returns(last_values, self.gamma, self.lam, adv_stats=stats)
 
@@ -249,7 +262,9 @@ class PPO:
     def update(self):
         num_updates = self.num_learning_epochs * self.num_mini_batches
         self._graph_calls += 1
-        if self.use_graph and self._graph_calls >= 2:  # first call runs eagerly (warm-up)
+        if self._fused is not None:
+            acc = self._update_fused()
+        elif self.use_graph and self._graph_calls >= 2:  # first call runs eagerly (warm-up)
             acc = self._update_graphed()
         else:
             acc = torch.zeros(2, device=self.device)
@@ -262,6 +277,48 @@ class PPO:
         means = (acc / num_updates).tolist()
         self.storage.clear()
         return means[0], means[1]
+
+    def _update_fused(self):
+        """num_epochs x num_mini_batches fused optimizer steps (FusedPPOStep.run), replayed
+        as one HIP graph from the second call on.  Same permutation rule as
+        RolloutStorage.mini_batch_generator: one randperm per update, reused every epoch."""
+        f, st = self._fused, self.storage
+        f.sync_optimizer_state(self.optimizer)
+        mb = f.M
+        if self._fgraph is None and not hasattr(self, "_fperm"):
+            self._fperm = torch.empty(self.num_mini_batches * mb, dtype=torch.int64, device=self.device)
+            self._facc = torch.zeros(2, device=self.device)
+            cobs = st.privileged_observations if st.privileged_observations is not None else st.observations
+            self._fsrc = (st.observations.flatten(0, 1), cobs.flatten(0, 1) if cobs is not st.observations
+                          else st.observations.flatten(0, 1), st.actions.flatten(0, 1), st.values.flatten(0, 1),
+                          st.advantages.flatten(0, 1), st.returns.flatten(0, 1), st.actions_log_prob.flatten(0, 1),
+                          st.mu.flatten(0, 1), st.sigma.flatten(0, 1))
+            if st.privileged_observations is None:  # the critic reads the actor's observations
+                self._fsrc = (self._fsrc[0], self._fsrc[0]) + self._fsrc[2:]
+            self._fadv = st.advantages
+        if st.advantages.data_ptr() != self._fadv.data_ptr():
+            self._fadv.copy_(st.advantages)
+            st.advantages = self._fadv
+        self._fperm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
+
+        def body():
+            self._facc.zero_()
+            for _ in range(self.num_learning_epochs):
+                for i in range(self.num_mini_batches):
+                    f.run(self._fperm[i * mb:(i + 1) * mb], self._fsrc, self._facc)
+
+        if not (self.use_graph and self._graph_calls >= 2):
+            body()
+            return self._facc
+        if self._fgraph is None:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            self._fgraph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._fgraph, stream=side):
+                body()
+            torch.cuda.current_stream(self.device).wait_stream(side)
+        self._fgraph.replay()
+        return self._facc
 
     def _update_graphed(self):
         """All num_epochs x num_mini_batches optimizer steps replayed as ONE HIP graph.

@@ -30,8 +30,8 @@ def lib_path():
 
 
 class ConvertJob(C.Structure):
-    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("yt", C.c_void_p), ("M", C.c_int32), ("K", C.c_int32),
-                ("ldx", C.c_int32), ("Kp", C.c_int32), ("ldyt", C.c_int32)]
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("yt", C.c_void_p), ("rows", C.c_void_p), ("M", C.c_int32),
+                ("K", C.c_int32), ("ldx", C.c_int32), ("Kp", C.c_int32), ("ldyt", C.c_int32)]
 
 
 class GemmJob(C.Structure):
@@ -70,8 +70,15 @@ def load():
         f32 = C.c_float
         L.pmlp_ppo_loss_blocks.argtypes = [i32]
         L.pmlp_ppo_loss_blocks.restype = i32
-        L.pmlp_ppo_loss_fwd.argtypes = [vp] * 10 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp]
-        L.pmlp_ppo_loss_bwd.argtypes = [vp] * 10 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
+        L.pmlp_ppo_loss_fwd.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp]
+        L.pmlp_ppo_loss_bwd.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
+        i64 = C.c_int64
+        L.pmlp_opt_parts.restype = i32
+        L.pmlp_opt_prepare.argtypes = [vp, i64, f32, vp, vp, vp, vp, vp, f32, i32, vp]
+        L.pmlp_adam.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, vp]
+        L.pmlp_gae_parts.argtypes = [i32]
+        L.pmlp_gae_parts.restype = i32
+        L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
         _lib = L
     return _lib
 
@@ -109,12 +116,17 @@ def supported(seq):
 
 
 def _convert(jobs):
-    """jobs: (x fp32 [M,K], Kp, y bf16 [M,Kp] | None, yt bf16 [Kp,ld] | None)"""
+    """jobs: (x fp32 [*,K], Kp, y bf16 [M,Kp] | None, yt bf16 [Kp,ld] | None[, rows int64 [M]]);
+    without rows M = x.shape[0], with rows output row m is x[rows[m]]."""
+    def mk(j):
+        x, kp, y, yt = j[:4]
+        rows = j[4] if len(j) > 4 else None
+        M = x.shape[0] if rows is None else rows.shape[0]
+        return ConvertJob(_p(x), _p(y), _p(yt), _p(rows), M, x.shape[1], x.stride(0), kp,
+                          0 if yt is None else yt.shape[1])
     for i in range(0, len(jobs), MAX_JOBS):
         chunk = jobs[i:i + MAX_JOBS]
-        arr = (ConvertJob * len(chunk))(*[
-            ConvertJob(_p(x), _p(y), _p(yt), x.shape[0], x.shape[1], x.stride(0), kp, 0 if yt is None else yt.shape[1])
-            for x, kp, y, yt in chunk])
+        arr = (ConvertJob * len(chunk))(*[mk(j) for j in chunk])
         _ok(load().pmlp_convert(len(chunk), arr, _stream()), "pmlp_convert")
 
 
@@ -321,7 +333,7 @@ class _PPOLossFn(torch.autograd.Function):
         partial = torch.empty(4 * nb, device=mu.device)
         loss = torch.empty((), device=mu.device)
         stats = torch.empty(4, device=mu.device)
-        _ok(load().pmlp_ppo_loss_fwd(*[_p(t) for t in ins], M, A, float(clip), int(bool(clipped)), float(vcoef),
+        _ok(load().pmlp_ppo_loss_fwd(*[_p(t) for t in ins], None, M, A, float(clip), int(bool(clipped)), float(vcoef),
                                      float(ecoef), _p(partial), _p(loss), _p(stats), _stream()), "pmlp_ppo_loss_fwd")
         ctx.save_for_backward(*ins)
         ctx.cfg = (M, A, float(clip), int(bool(clipped)), float(vcoef), float(ecoef), tuple(value.shape))
@@ -339,7 +351,7 @@ class _PPOLossFn(torch.autograd.Function):
         dvalue = torch.empty(M, device=dev)
         dstd = torch.empty(A, device=dev)
         partial = torch.empty(A * nb, device=dev)
-        _ok(load().pmlp_ppo_loss_bwd(*[_p(t) for t in ins], M, A, clip, clipped, vcoef, ecoef, _p(g), _p(dmu),
+        _ok(load().pmlp_ppo_loss_bwd(*[_p(t) for t in ins], None, M, A, clip, clipped, vcoef, ecoef, _p(g), _p(dmu),
                                      _p(dvalue), _p(partial), _p(dstd), _stream()), "pmlp_ppo_loss_bwd")
         return (dmu, dstd, dvalue.view(vshape)) + (None,) * 11
 
