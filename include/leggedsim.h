@@ -206,6 +206,11 @@ typedef struct lgs_env_buffers {
                                 lgs_reset_all read the Philox step key from it instead of the by-value
                                 argument, and lgs_step advances it by one after the step: a captured
                                 hipGraph of K steps then draws fresh noise/commands on every replay. */
+    /* extras (legged_robot.py:742-768), refreshed by lgs_step after the step when >= 1 env reset;
+       each may be NULL.  lgs_step also zeroes episode_acc for the next step.                      */
+    float* ep_means;         /* [num_sums] carried extras["episode"] values (rew_* / max_episode_length_s) */
+    float* ep_snapshot;      /* [num_sums] this step's copy of ep_means (the step's extras["episode"]) */
+    uint8_t* time_outs_carry;/* [N] extras["time_outs"]: time_out of the last step with a reset */
 } lgs_env_buffers;
 
 typedef struct lgs_sim lgs_sim;

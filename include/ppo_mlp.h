@@ -146,4 +146,22 @@ PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* v
                       float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
                       double* partial, void* stream);
 
+/* Rollout step of PPO (rsl_rl v1.0.2 PPO.act + RolloutStorage.add_transitions):
+ * from the policy mean mu[N,A], std[A] and value[N] (the MLP outputs) draw
+ * actions = mu + std * n, n ~ N(0,1) from Philox4x32-10 keyed (seed; draw[0],
+ * row, pair) with Box-Muller; write actions_out[N,A] and storage row t:
+ * actions, log_prob[N] (sum over A of the Gaussian log-density), mu, sigma
+ * (std broadcast), value, observations obs[N,O] (and critic observations
+ * cobs[N,CO] when st_cobs != NULL).
+ * pmlp_store_step (PPO.process_env_step): st_rewards = rewards + gamma *
+ * (st_value * time_outs) (time_outs may be NULL: no bootstrap), st_dones =
+ * dones (bool bytes), then draw[0] += 1.                                     */
+PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, const float* obs, const float* cobs,
+                      int32_t N, int32_t A, int32_t O, int32_t CO, const int64_t* draw, uint64_t seed,
+                      float* actions_out, float* st_actions, float* st_logp, float* st_mu, float* st_sigma,
+                      float* st_value, float* st_obs, float* st_cobs, void* stream);
+PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                             const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                             int64_t* draw, void* stream);
+
 #endif

@@ -829,10 +829,12 @@ void orc_post_physics_env(const lgs_model_desc* md, const lgs_task_params* T, in
         for (int f = 0; f < T->num_feet; ++f) air[f] = 0.f;
         *ep = 0;
         int nsum = T->num_rewards + (T->has_termination_reward ? 1 : 0);
-        for (int k = 0; k < nsum; ++k) {
+        for (int k = 0; k < nsum; ++k) {  /* shared across the OpenMP env loop */
+#pragma omp atomic
             E->episode_acc[k] += E->episode_sums[(size_t)k * N + e];
             E->episode_sums[(size_t)k * N + e] = 0.f;
         }
+#pragma omp atomic
         E->episode_acc[nsum] += 1.f;
     }
     /* _push_robots (:540-555): envs with ep_len % interval == 0, incl. just-reset ones */

@@ -103,6 +103,14 @@ def test_timeouts_reset_push_match_oracle_exactly(task):
     ep = env.extras["episode"]
     assert set(ep) == {"rew_" + k for k in env._sum_names}
     assert env.extras["time_outs"].all()
+    # extras["episode"] = sums over the reset envs / count / episode_length_s (:742-768)
+    nsum = len(env._sum_names)
+    acc = ref["episode_acc"]
+    means = acc[:nsum] / max(float(acc[nsum]), 1.0) / env.max_episode_length_s
+    got = torch.stack([ep["rew_" + k] for k in env._sum_names]).cpu().numpy()
+    # the step's reward terms inherit the physics tolerance (dof_acc/torque terms)
+    np.testing.assert_allclose(got, means, rtol=2e-2, atol=1e-5)
+    assert float(env._episode_acc.abs().sum()) == 0.0  # zeroed for the next step
 
 
 def test_drop_in_semantics():
@@ -263,6 +271,7 @@ def test_ppo_graph_tracks_eager_over_many_updates():
                   schedule="fixed", device="cuda")
         alg.use_graph = graph
         alg.init_storage(N, T, [O], [None], [A])
+        alg._rollout = None  # the reference act()/process_env_step: the test sets the actions itself
         algs.append(alg)
     g = torch.Generator(device="cuda").manual_seed(1)
     losses = {True: [], False: []}

@@ -19,6 +19,7 @@ from rsl_rl.storage import RolloutStorage  # noqa: E402
 def _fill_storage(alg, T, N, O, A, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     st = alg.storage
+    ro, alg._rollout = alg._rollout, None  # the reference act()/process_env_step path (custom actions)
     with torch.inference_mode():
         for _ in range(T):
             obs = torch.randn(N, O, device="cuda", generator=g)
@@ -29,6 +30,7 @@ def _fill_storage(alg, T, N, O, A, seed):
             done = torch.rand(N, device="cuda", generator=g) < 0.05
             alg.process_env_step(rew, done, {"time_outs": done & (torch.rand(N, device="cuda", generator=g) < 0.5)})
         alg.compute_returns(torch.randn(N, O, device="cuda", generator=g))
+    alg._rollout = ro
     return {k: v.clone() for k, v in st.__dict__.items() if torch.is_tensor(v) and not k.startswith("_")}
 
 
@@ -171,3 +173,48 @@ def test_fused_checkpoint_roundtrip(tmp_path):
     torch.testing.assert_close(alg2._fused.exp_avg, alg._fused.exp_avg)
     torch.testing.assert_close(alg2._fused.exp_avg_sq, alg._fused.exp_avg_sq)
     assert float(alg2._fused.step_t) == float(alg._fused.step_t) == 2.0
+
+
+def test_fused_rollout_act_and_store_match_reference_semantics():
+    """PPO.act / process_env_step through FusedRollout: actions ~ N(mu, std) (sample
+    moments), log-prob, mean, sigma, value and observations in the storage row exactly
+    as the reference computes them from the same policy outputs; the time-out bootstrap
+    bitwise as the torch statement; fresh noise every step."""
+    from torch.distributions import Normal
+    torch.manual_seed(0)
+    N, T, O, A = 4096, 4, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    assert alg._rollout is not None
+    ac, st = alg.actor_critic, alg.storage
+    g = torch.Generator(device="cuda").manual_seed(4)
+    prev = None
+    with torch.inference_mode():
+        for t in range(T):
+            obs = torch.randn(N, O, device="cuda", generator=g)
+            actions = alg.act(obs, obs).clone()
+            mu, value = ac.mean_and_value(obs, obs)  # same bf16 MFMA forward
+            torch.testing.assert_close(st.mu[t], mu, rtol=0, atol=0)
+            torch.testing.assert_close(st.values[t], value, rtol=0, atol=0)
+            torch.testing.assert_close(st.observations[t], obs, rtol=0, atol=0)
+            sig = (mu * 0.0 + ac.std).detach()
+            torch.testing.assert_close(st.sigma[t], sig, rtol=0, atol=0)
+            assert torch.equal(st.actions[t], actions)
+            z = (actions - mu) / sig
+            assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
+            lp = Normal(mu, sig).log_prob(actions).sum(dim=-1)
+            torch.testing.assert_close(st.actions_log_prob[t].squeeze(1), lp, rtol=1e-5, atol=1e-4)
+            if prev is not None:
+                assert not torch.equal(z, prev)
+            prev = z
+            rew = torch.randn(N, device="cuda", generator=g)
+            done = torch.rand(N, device="cuda", generator=g) < 0.1
+            tout = done & (torch.rand(N, device="cuda", generator=g) < 0.5)
+            alg.process_env_step(rew, done, {"time_outs": tout})
+            ref = rew.clone()
+            ref += alg.gamma * torch.squeeze(value * tout.unsqueeze(1), 1)
+            assert torch.equal(st.rewards[t].squeeze(1), ref)
+            assert torch.equal(st.dones[t].squeeze(1), done)
+    assert st.step == T
+    with pytest.raises(AssertionError):
+        alg.act(obs, obs)

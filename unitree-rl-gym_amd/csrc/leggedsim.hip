@@ -1386,8 +1386,29 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
 }
 
-// common_step_counter += 1 on the device (the step key of graph-replayed steps)
-__global__ void k_advance_step(int64_t* counter) { *counter += 1; }
+// After k_step (one block): the extras of reset_idx (legged_robot.py:742-768) —
+// episode means over the envs reset this step, carried when none reset, and the
+// carried time-out flags — then episode_acc zeroed for the next step and the
+// device step counter advanced (the Philox key of graph-replayed steps).
+__global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
+                                                      int N) {
+    const lgs_task_params& T = *Tp;
+    const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+    const float cnt = E.episode_acc[nsum];
+    const bool any = cnt > 0.f;
+    const int t = threadIdx.x;
+    if (E.ep_means && t < nsum) {
+        float m = E.ep_means[t];
+        if (any) m = E.episode_acc[t] / fmaxf(cnt, 1.f) / T.max_episode_length_s;
+        E.ep_means[t] = m;
+        if (E.ep_snapshot) E.ep_snapshot[t] = m;
+    }
+    if (E.time_outs_carry && any)
+        for (int e = t; e < N; e += blockDim.x) E.time_outs_carry[e] = E.time_out[e];
+    __syncthreads();
+    if (t <= nsum) E.episode_acc[t] = 0.f;
+    if (t == 0 && E.step_counter) *E.step_counter += 1;
+}
 
 __global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, int n, int width) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1638,10 +1659,8 @@ LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counte
     DevState st = state_of(s);
     LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
     HIP_TRY(hipGetLastError());
-    if (env->step_counter) {
-        hipLaunchKernelGGL(k_advance_step, dim3(1), dim3(1), 0, s->stream, env->step_counter);
-        HIP_TRY(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N);
+    HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
 

@@ -602,6 +602,93 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adv_norm(float* __restrict
         adv[i] = (adv[i] - meanf) / den;
 }
 
+// ------------------------------------------------------------- rollout --
+// PPO.act tail + RolloutStorage.add_transitions (rsl_rl v1.0.2) for the
+// Gaussian MLP policy, and PPO.process_env_step's reward bootstrap + store.
+// Policy noise: Philox4x32-10 keyed (seed; draw, row, pair) -> Box-Muller.
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)x + 0.5f) * 2.3283064365386963e-10f; }
+
+struct ActArgs {
+    const float *mu, *stdv, *value, *obs, *cobs;
+    float *actions_out, *st_actions, *st_logp, *st_mu, *st_sigma, *st_value, *st_obs, *st_cobs;
+    const int64_t* draw;
+    uint64_t seed;
+    int N, A, O, CO;
+};
+
+__global__ __launch_bounds__(256) void k_act(ActArgs a) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+    const uint32_t draw = (uint32_t)*a.draw;
+    const uint2 key = make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    for (int64_t i = tid; i < a.N; i += nth) {
+        float logp = 0.f;
+        for (int k0 = 0; k0 < a.A; k0 += 4) {
+            const uint4 r = philox4x32(make_uint4(draw, (uint32_t)i, (uint32_t)(k0 >> 2), 0x5050u), key);
+            const float rad0 = sqrtf(-2.f * logf(u01(r.x))), rad1 = sqrtf(-2.f * logf(u01(r.z)));
+            float z[4];
+            sincospif(2.f * u01(r.y), &z[1], &z[0]);
+            sincospif(2.f * u01(r.w), &z[3], &z[2]);
+            z[0] *= rad0; z[1] *= rad0; z[2] *= rad1; z[3] *= rad1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u;
+                if (k >= a.A) break;
+                const size_t o = (size_t)i * a.A + k;
+                const float sg = a.stdv[k], mu = a.mu[o];
+                const float act = mu + sg * z[u];
+                const float d = act - mu;
+                logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
+                a.actions_out[o] = act;
+                a.st_actions[o] = act;
+                a.st_mu[o] = mu;
+                a.st_sigma[o] = sg;
+            }
+        }
+        a.st_logp[i] = logp;
+        a.st_value[i] = a.value[i];
+    }
+    // observations into the storage row (float4 when aligned)
+    const int64_t no = (int64_t)a.N * a.O;
+    if ((no & 3) == 0 && (((uintptr_t)a.obs | (uintptr_t)a.st_obs) & 15) == 0) {
+        for (int64_t j = tid; j < no / 4; j += nth) ((float4*)a.st_obs)[j] = ((const float4*)a.obs)[j];
+    } else {
+        for (int64_t j = tid; j < no; j += nth) a.st_obs[j] = a.obs[j];
+    }
+    if (a.st_cobs) {
+        const int64_t nc = (int64_t)a.N * a.CO;
+        for (int64_t j = tid; j < nc; j += nth) a.st_cobs[j] = a.cobs[j];
+    }
+}
+
+// rewards[i] + gamma * (value[i] * time_out[i]) and dones into the storage row;
+// then the policy-noise draw counter advances (one thread, after k_act)
+__global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ rew, const uint8_t* __restrict__ dones,
+                                                    const uint8_t* __restrict__ time_outs,
+                                                    const float* __restrict__ st_value, float* __restrict__ st_rew,
+                                                    uint8_t* __restrict__ st_dones, int N, float gamma,
+                                                    int64_t* draw) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) {
+        float r = rew[i];
+        if (time_outs) r = r + gamma * (st_value[i] * (time_outs[i] ? 1.f : 0.f));
+        st_rew[i] = r;
+        st_dones[i] = dones[i] ? 1 : 0;
+    }
+    if (i == 0 && draw) *draw += 1;
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
@@ -805,6 +892,33 @@ PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* v
     hipLaunchKernelGGL(k_adv_norm, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, advantages, n,
                        partial, nb);
     PMLP_CHECK_LAUNCH("pmlp_gae");
+    return 0;
+}
+
+PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, const float* obs, const float* cobs,
+                      int32_t N, int32_t A, int32_t O, int32_t CO, const int64_t* draw, uint64_t seed,
+                      float* actions_out, float* st_actions, float* st_logp, float* st_mu, float* st_sigma,
+                      float* st_value, float* st_obs, float* st_cobs, void* stream) {
+    if (!mu || !stdv || !value || !obs || !draw || !actions_out || !st_actions || !st_logp || !st_mu || !st_sigma ||
+        !st_value || !st_obs || N <= 0 || A <= 0 || O <= 0 || (st_cobs && (!cobs || CO <= 0)))
+        return fail(-1, "pmlp_act: null buffer or empty shape");
+    ActArgs a{mu, stdv, value, obs, cobs, actions_out, st_actions, st_logp, st_mu, st_sigma, st_value, st_obs,
+              st_cobs, draw, seed, N, A, O, CO};
+    const int64_t work = std::max<int64_t>(N, (int64_t)N * O / 4);
+    const int blocks = (int)std::min<int64_t>(1024, (work + 255) / 256);
+    hipLaunchKernelGGL(k_act, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    PMLP_CHECK_LAUNCH("pmlp_act");
+    return 0;
+}
+
+PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                             const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                             int64_t* draw, void* stream) {
+    if (!rewards || !dones || !st_value || !st_rewards || !st_dones || N <= 0)
+        return fail(-1, "pmlp_store_step: null buffer or empty batch");
+    hipLaunchKernelGGL(k_store_step, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
+                       time_outs, st_value, st_rewards, st_dones, N, gamma, draw);
+    PMLP_CHECK_LAUNCH("pmlp_store_step");
     return 0;
 }
 

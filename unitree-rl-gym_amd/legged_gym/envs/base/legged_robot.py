@@ -263,6 +263,9 @@ class LeggedRobot(BaseTask):
         E.leg_phase = p(self.leg_phase)
         E.rew_terms = None
         E.step_counter = p(self._d_step_counter)
+        E.ep_means = p(self._ep_means)
+        E.ep_snapshot = None  # set per step (step())
+        E.time_outs_carry = p(self._time_outs) if self.cfg.env.send_timeouts else None
         return E
 
     @property
@@ -297,33 +300,21 @@ class LeggedRobot(BaseTask):
         self._buf_idx ^= 1
         i = self._buf_idx
         self.actions.copy_(actions)
-        self._episode_acc.zero_()
-        self.sim.step(self._env_structs[i], self._step_mirror)
+        # this step's extras["episode"] values (a fresh buffer per step, like the
+        # reference's per-reset tensors; inside a captured rollout, one per step)
+        snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
+        E = self._env_structs[i]
+        E.ep_snapshot = snap.data_ptr()
+        self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
         self._step_mirror += 1
         self.obs_buf = self._obs_bufs[i]
         self.privileged_obs_buf = self._priv_bufs[i]
         self.reset_buf = self._reset_bufs[i]
         self.time_out_buf = self._timeout_bufs[i]
-        self._update_extras()
-        return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
-
-    def _update_extras(self):
-        """extras["episode"] / ["time_outs"] refresh only when >= 1 env reset (:742-768).
-
-        The values carried from step to step live in persistent buffers updated in
-        place (so a captured rollout graph carries them across replays); each step's
-        extras["episode"] dict holds views of that step's own snapshot, like the
-        reference's fresh per-reset tensors."""
-        nsum = len(self._sum_names)
-        cnt = self._episode_acc[nsum]
-        any_reset = cnt > 0
-        means = self._episode_acc[:nsum] / cnt.clamp(min=1.0) / self.max_episode_length_s
-        snap = torch.where(any_reset, means, self._ep_means)
-        self._ep_means.copy_(snap)
-        self.extras["episode"] = {"rew_" + k: snap[i] for i, k in enumerate(self._sum_names)}
+        self.extras["episode"] = {"rew_" + k: snap[j] for j, k in enumerate(self._sum_names)}
         if self.cfg.env.send_timeouts:
-            self._time_outs.copy_(torch.where(any_reset, self.time_out_buf, self._time_outs))
             self.extras["time_outs"] = self._time_outs
+        return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
     def reset_idx(self, env_ids):
         """Reset the given envs.  The native kernel resets every env of the batch

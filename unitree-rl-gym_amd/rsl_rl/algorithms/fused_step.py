@@ -242,6 +242,85 @@ class FusedPPOStep:
                              float(b2), float(eps), st), "pmlp_adam")
 
 
+class FusedRollout:
+    """PPO.act + RolloutStorage.add_transitions and PPO.process_env_step for the
+    Gaussian MLP policy in 5 + 1 + 1 launches per env step: the bf16 forward of both
+    nets (one convert, L GEMMs), pmlp_act (sample, log-prob, storage row incl. the
+    observations) and pmlp_store_step (bootstrapped reward, dones).  The policy
+    noise is Philox keyed on a device draw counter, so a captured rollout draws
+    fresh noise on every replay; the seed comes from torch's (seeded) generator."""
+
+    def __init__(self, step: FusedPPOStep, num_envs):
+        self.f = step
+        N, dev, bf = int(num_envs), step.dev, torch.bfloat16
+        self.N = N
+        lins = step.lins
+        self.x = [torch.empty(N, k, dtype=bf, device=dev) for k in step.k0p]
+        self.y = [[torch.empty(N, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in lins]
+        self.out = [torch.empty(N, ls[-1].out_features, device=dev) for ls in lins]
+        self.actions = torch.empty(N, lins[0][-1].out_features, device=dev)
+        self.draw = torch.zeros((), dtype=torch.int64, device=dev)
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+
+    def usable(self, obs, cobs, storage):
+        ok = lambda t, w: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
+                           t.shape == (self.N, w) and t.is_contiguous())
+        f = self.f
+        if not ok(obs, f.lins[0][0].in_features) or not ok(cobs, f.lins[1][0].in_features):
+            return False
+        if storage.privileged_observations is None and cobs is not obs:
+            return False
+        return storage.num_envs == self.N
+
+    def act(self, obs, cobs, storage, t):
+        f, N = self.f, self.N
+        shared = cobs is obs and f.k0p[0] == f.k0p[1]
+        jobs = [(obs, f.k0p[0], self.x[0], None)]
+        if not shared:
+            jobs.append((cobs, f.k0p[1], self.x[1], None))
+        for n in range(2):
+            for l, lin in enumerate(f.lins[n]):
+                jobs.append((lin.weight.detach(), f.wb[n][l].shape[1], f.wb[n][l], None))
+        mm._convert(jobs)
+        xs = [self.x[0], self.x[0] if shared else self.x[1]]
+        for l in range(f.L):
+            last = l == f.L - 1
+            gj = []
+            for n in range(2):
+                lin = f.lins[n][l]
+                a_in = xs[n] if l == 0 else self.y[n][l - 1]
+                K = f.k0p[n] if l == 0 else lin.in_features
+                if last:
+                    gj.append(dict(A=a_in, B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cf=self.out[n]))
+                else:
+                    gj.append(dict(A=a_in, B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cb=self.y[n][l]))
+            mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
+        A = self.actions.shape[1]
+        priv = storage.privileged_observations
+        P = mm._p
+        mm._ok(mm.load().pmlp_act(P(self.out[0]), P(f.ac.std.detach()), P(self.out[1]), P(obs),
+                                  P(cobs) if priv is not None else None, N, A, obs.shape[1],
+                                  cobs.shape[1] if priv is not None else 0, P(self.draw), self.seed, P(self.actions),
+                                  P(storage.actions[t]), P(storage.actions_log_prob[t]), P(storage.mu[t]),
+                                  P(storage.sigma[t]), P(storage.values[t]), P(storage.observations[t]),
+                                  P(priv[t]) if priv is not None else None, mm._stream()), "pmlp_act")
+        return self.actions
+
+    def store(self, rewards, dones, time_outs, storage, t, gamma):
+        P = mm._p
+        mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+                                         P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
+                                         P(self.draw), mm._stream()), "pmlp_store_step")
+
+    @staticmethod
+    def storable(rewards, dones, time_outs, N):
+        ok = lambda t, dt: t.is_cuda and t.dtype == dt and t.numel() == N and t.is_contiguous()  # noqa: E731
+        return ok(rewards, torch.float32) and ok(dones, torch.bool) and (time_outs is None or
+                                                                         ok(time_outs, torch.bool))
+
+
 def gae(storage, last_values, gamma, lam):
     """RolloutStorage.compute_returns on the GPU in two launches (pmlp_gae): GAE
     backwards over T per env, then advantage normalisation."""

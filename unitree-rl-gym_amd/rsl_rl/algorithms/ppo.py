@@ -76,6 +76,8 @@ class PPO:
         # the torch statement of the loss, _reference_loss)
         self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "mean_and_value")
         self._fused = None  # FusedPPOStep, built with the storage (init_storage)
+        self._rollout = None  # FusedRollout: act/process_env_step of the same policy
+        self._stored_t = None  # storage row the fused act() filled, awaiting process_env_step
         self._fgraph = None
         self._diag, self._diag_i = None, 0
         self._graph_calls = 0
@@ -104,8 +106,9 @@ class PPO:
                 getattr(self.actor_critic, "mixed_precision", False) and batch % self.num_mini_batches == 0:
             try:  # whole optimizer step in ~20 launches (algorithms/fused_step.py)
                 self._fused = fused_step.FusedPPOStep(self, batch // self.num_mini_batches)
+                self._rollout = fused_step.FusedRollout(self._fused, num_envs) if num_envs % 8 == 0 else None
             except ValueError:
-                self._fused = None
+                self._fused = self._rollout = None
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -114,6 +117,19 @@ class PPO:
         self.actor_critic.train()
 
     def act(self, obs, critic_obs):
+        ro, st = self._rollout, self.storage
+        if ro is not None and ro.usable(obs, critic_obs, st):
+            # forward, sample, log-prob and the storage row in 6 launches (FusedRollout)
+            t = st.step
+            if t >= st.num_transitions_per_env:
+                raise AssertionError("Rollout buffer overflow")
+            actions = ro.act(obs, critic_obs, st, t)
+            tr = self.transition
+            tr.actions, tr.values, tr.actions_log_prob = st.actions[t], st.values[t], st.actions_log_prob[t]
+            tr.action_mean, tr.action_sigma = st.mu[t], st.sigma[t]
+            tr.observations, tr.critic_observations = obs, critic_obs
+            self._stored_t = t
+            return actions
         if self.actor_critic.is_recurrent:
             self.transition.hidden_states = self.actor_critic.get_hidden_states()
         if not self.actor_critic.is_recurrent and hasattr(self.actor_critic, "act_and_value"):  # shared launches
@@ -130,6 +146,15 @@ class PPO:
         return self.transition.actions
 
     def process_env_step(self, rewards, dones, infos):
+        t, self._stored_t = self._stored_t, None
+        time_outs = infos["time_outs"] if "time_outs" in infos else None
+        if t is not None and t == self.storage.step and \
+                fused_step.FusedRollout.storable(rewards, dones, time_outs, self.storage.num_envs):
+            self._rollout.store(rewards, dones, time_outs, self.storage, t, self.gamma)
+            self.storage.step += 1
+            self.transition.clear()
+            self.actor_critic.reset(dones)
+            return
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones
         if "time_outs" in infos:  # bootstrap on time-outs

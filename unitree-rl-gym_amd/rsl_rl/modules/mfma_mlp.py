@@ -79,6 +79,8 @@ def load():
         L.pmlp_gae_parts.argtypes = [i32]
         L.pmlp_gae_parts.restype = i32
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
+        L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
+        L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         _lib = L
     return _lib
 
