@@ -689,6 +689,156 @@ __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ re
     if (i == 0 && draw) *draw += 1;
 }
 
+// ------------------------------------------------ register-chained MLP forward --
+// Policy inference (PPO.act, compute_returns' value): y = W3 ELU(W2 ELU(W1 ELU(W0 x))).
+// A block of 4 waves owns 128 batch rows (32 per wave) and runs ALL layers with the
+// activations kept in registers: computing H^T = W . X^T, the 32x32 accumulator tile
+// of one layer (rows = features, column = batch row on the lane) is directly the B
+// operand of the next layer's MFMA (guide §3 "accumulator tile as the next MFMA's
+// operand"), the weights supplying the matching permuted k order.  The weights are
+// the only stream: 32-row x 128-k chunks (fp32 -> bf16) are staged through a double-
+// buffered LDS tile shared by the 4 waves, the next chunk's global loads in flight
+// while the MFMAs of this one run.  No intermediate HBM traffic.
+struct Mlp4Job {
+    const float* x;
+    const float* W[4];
+    const float* b[4];
+    float* out;
+    int ldx, K0, ldo, NO;
+};
+struct Mlp4Jobs {
+    Mlp4Job j[2];
+};
+
+#define MLP4_WAVES 4
+#define MLP4_KC 128             // k per staged chunk
+#define MLP4_LS (MLP4_KC + 4)   // LDS row stride (bf16): 264 B, == 8 mod 256 -> conflict-free b64 reads
+
+struct Mlp4Stage {
+    float4 v[4];  // 32 rows x 128 k fp32 / 256 threads
+};
+
+// global -> registers: rows n0..n0+31 (< nrows), k k0..k0+127 (< K) of W[., K]
+__device__ __forceinline__ void mlp4_load(Mlp4Stage& st, const float* __restrict__ W, int K, int nrows, int n0,
+                                          int k0) {
+    const int tid = threadIdx.x, row = tid >> 3, c = (tid & 7) * 16;
+    const int n = n0 + row;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = k0 + c + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < nrows) {
+            if (k + 3 < K && (K & 3) == 0) {
+                v = *(const float4*)(W + (size_t)n * K + k);
+            } else {
+                const float* w = W + (size_t)n * K;
+                v.x = k < K ? w[k] : 0.f;
+                v.y = k + 1 < K ? w[k + 1] : 0.f;
+                v.z = k + 2 < K ? w[k + 2] : 0.f;
+                v.w = k + 3 < K ? w[k + 3] : 0.f;
+            }
+        }
+        st.v[q] = v;
+    }
+}
+__device__ __forceinline__ void mlp4_store(const Mlp4Stage& st, bf16* __restrict__ tile) {
+    const int tid = threadIdx.x, row = tid >> 3, c = (tid & 7) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        bf16x4 w;
+        w[0] = (bf16)st.v[q].x; w[1] = (bf16)st.v[q].y; w[2] = (bf16)st.v[q].z; w[3] = (bf16)st.v[q].w;
+        *(bf16x4*)(tile + row * MLP4_LS + c + 4 * q) = w;
+    }
+}
+
+// One layer: operand `xin` (KS k-steps; natural k order for the input layer, the
+// accumulator-permuted order otherwise) -> NT output tiles of 32 features, bias (+ ELU)
+// -> the next layer's operand `xout` (hidden) or out[] (last layer, NO features).
+// W: [NT*32 (rows < nrows valid), K] fp32.  Chunk c = (tile c / CPT, k-chunk c % CPT).
+template <int KS, int NT, bool NATURAL, bool LAST>
+__device__ __forceinline__ void mlp4_layer(const bf16x8 (&xin)[KS], bf16x8 (&xout)[LAST ? 1 : 2 * NT],
+                                           const float* __restrict__ W, const float* __restrict__ bias, int K,
+                                           int nrows, bf16* __restrict__ lds, float* __restrict__ out, int ldo,
+                                           int grow, int M) {
+    constexpr int SPC = MLP4_KC / 16;                 // k-steps per chunk
+    constexpr int CPT = (KS + SPC - 1) / SPC;         // chunks per tile
+    constexpr int NC = NT * CPT;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    Mlp4Stage st;
+    mlp4_load(st, W, K, nrows, 0, 0);
+    floatx16 acc;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int t = c / CPT, kc = c % CPT;
+        bf16* tile = lds + (c & 1) * 32 * MLP4_LS;
+        mlp4_store(st, tile);
+        __syncthreads();
+        if (c + 1 < NC) mlp4_load(st, W, K, nrows, 32 * ((c + 1) / CPT), MLP4_KC * ((c + 1) % CPT));
+        if (kc == 0) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc[u] = 0.f;
+        }
+#pragma unroll
+        for (int ss = 0; ss < SPC; ++ss) {
+            const int s = kc * SPC + ss;
+            if (s < KS) {
+                bf16x8 wa;
+                const bf16* wrow = tile + r * MLP4_LS + 16 * ss;
+                if (NATURAL) {
+                    wa = *(const bf16x8*)(wrow + 8 * h);
+                } else {
+                    const bf16x4 lo = *(const bf16x4*)(wrow + 4 * h);
+                    const bf16x4 hi = *(const bf16x4*)(wrow + 8 + 4 * h);
+                    wa[0] = lo[0]; wa[1] = lo[1]; wa[2] = lo[2]; wa[3] = lo[3];
+                    wa[4] = hi[0]; wa[5] = hi[1]; wa[6] = hi[2]; wa[7] = hi[3];
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xin[s], acc, 0, 0, 0);
+            }
+        }
+        if (kc == CPT - 1) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int f = 32 * t + (u & 3) + 8 * (u >> 2) + 4 * h;
+                if (LAST) {
+                    if (f < nrows && grow < M) out[(size_t)grow * ldo + f] = acc[u] + bias[f];
+                } else {
+                    xout[LAST ? 0 : 2 * t + (u >> 3)][u & 7] = (bf16)elu(acc[u] + bias[f]);
+                }
+            }
+        }
+    }
+}
+
+template <int H0, int H1, int H2>
+__global__ __launch_bounds__(64 * MLP4_WAVES) void k_mlp4_fwd(Mlp4Jobs jobs, int M) {
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * 32 * MLP4_LS];
+    const Mlp4Job& J = jobs.j[blockIdx.y];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+    const int grow = blockIdx.x * 32 * MLP4_WAVES + 32 * wave + r;
+    // input operand, natural k order: lane (r, h) holds x[grow][16s + 8h + j]  (K0 <= 128)
+    bf16x8 x0[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * s + 8 * h + j;
+            x0[s][j] = (bf16)((grow < M && k < J.K0) ? J.x[(size_t)grow * J.ldx + k] : 0.f);
+        }
+    bf16x8 x1[H0 / 16];
+    if (J.K0 <= 64) mlp4_layer<4, H0 / 32, true, false>(*(const bf16x8(*)[4])x0, x1, J.W[0], J.b[0], J.K0, H0, lds,
+                                                        nullptr, 0, grow, M);
+    else mlp4_layer<8, H0 / 32, true, false>(x0, x1, J.W[0], J.b[0], J.K0, H0, lds, nullptr, 0, grow, M);
+    __syncthreads();
+    bf16x8 x2[H1 / 16];
+    mlp4_layer<H0 / 16, H1 / 32, false, false>(x1, x2, J.W[1], J.b[1], H0, H1, lds, nullptr, 0, grow, M);
+    __syncthreads();
+    bf16x8 x3[H2 / 16];
+    mlp4_layer<H1 / 16, H2 / 32, false, false>(x2, x3, J.W[2], J.b[2], H1, H2, lds, nullptr, 0, grow, M);
+    __syncthreads();
+    bf16x8 dummy[1];
+    mlp4_layer<H2 / 16, 1, false, true>(x3, dummy, J.W[3], J.b[3], H2, J.NO, lds, J.out, J.ldo, grow, M);
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
@@ -760,6 +910,8 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
     if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, st);
     else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, st);
     else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, st);
+    else if (epi != PMLP_EPI_PARTIAL && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
+        launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, st);  // small grids: 4x the blocks hide the k-loop latency
     else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, st);
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
@@ -919,6 +1071,29 @@ PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const u
     hipLaunchKernelGGL(k_store_step, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
                        time_outs, st_value, st_rewards, st_dones, N, gamma, draw);
     PMLP_CHECK_LAUNCH("pmlp_store_step");
+    return 0;
+}
+
+PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t M, int32_t H0, int32_t H1,
+                               int32_t H2, void* stream) {
+    if (njobs <= 0 || njobs > 2 || !jobs || M <= 0) return fail(-1, "pmlp_mlp4_forward: 1..2 jobs, M > 0");
+    Mlp4Jobs mj{};
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_mlp4_job& J = jobs[i];
+        bool ok = J.x && J.out && J.K0 > 0 && J.K0 <= 128 && J.ldx >= J.K0 && J.NO > 0 && J.NO <= 32 &&
+                  J.ldo >= J.NO;
+        for (int l = 0; l < 4; ++l) ok = ok && J.W[l] && J.b[l];
+        if (!ok) return fail(-1, "pmlp_mlp4_forward: bad job " + std::to_string(i));
+        mj.j[i] = Mlp4Job{J.x, {J.W[0], J.W[1], J.W[2], J.W[3]}, {J.b[0], J.b[1], J.b[2], J.b[3]}, J.out,
+                          J.ldx, J.K0, J.ldo, J.NO};
+    }
+    const int rows = 32 * MLP4_WAVES;
+    dim3 grid((M + rows - 1) / rows, njobs), block(64 * MLP4_WAVES);
+    hipStream_t st = (hipStream_t)stream;
+    if (H0 == 512 && H1 == 256 && H2 == 128) hipLaunchKernelGGL((k_mlp4_fwd<512, 256, 128>), grid, block, 0, st, mj, M);
+    else if (H0 == 256 && H1 == 128 && H2 == 64) hipLaunchKernelGGL((k_mlp4_fwd<256, 128, 64>), grid, block, 0, st, mj, M);
+    else return fail(-1, "pmlp_mlp4_forward: hidden sizes (512,256,128) or (256,128,64)");
+    PMLP_CHECK_LAUNCH("pmlp_mlp4_forward");
     return 0;
 }
 
