@@ -60,7 +60,7 @@ typedef struct {
 PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream);
 
 /* C = A . B^T with epilogue `epi` (see enum).  A: [M,K] (lda), B: [N,K] (ldb).
- *   FWD_HIDDEN: bias[N]; cb[M,N] (ldcb); ct[N,M] (ldct, may be NULL)
+ *   FWD_HIDDEN: bias[N]; cb[M,N] (ldcb) and/or ct[N,M] (ldct): either may be NULL
  *   FWD_OUT:    bias[N]; cf[M,N] (ldcf)
  *   BWD_DX:     yprev[M,N] bf16 (ldyp) = the ELU output the gradient flows through;
  *               cb/ct as FWD_HIDDEN
@@ -79,12 +79,16 @@ typedef struct {
 } pmlp_gemm_job;
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
 
-/* out[i] = sum_s slab[s*stride + i], i < n (fp32): the split-K combine. */
+/* out[i] = sum_s slab[s*stride + i], i < n (fp32): the split-K combine.
+ * bias_out (optional): the slab is [n/cols_in, cols_in]; columns < cols_out go to
+ * out[n/cols_in, cols_out] and column cols_out to bias_out (the weight gradient's
+ * extra ones-row column = the bias gradient); later columns are dropped.     */
 typedef struct {
     const float* slab;
     float* out;
+    float* bias_out;
     int64_t stride, n;
-    int32_t nslabs;
+    int32_t nslabs, cols_in, cols_out;
 } pmlp_reduce_job;
 PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream);
 
@@ -180,5 +184,19 @@ typedef struct {
 } pmlp_mlp4_job;
 PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t M, int32_t H0, int32_t H1,
                                int32_t H2, void* stream);
+
+/* The same loss for the fused optimizer step (gradient of the loss itself):
+ * one pass writes the output gradients straight into the MLP backward's bf16
+ * operands, dmu[M,Ap] + dmu_t[Ap,M] and dvalue[M,Vp] + dvalue_t[Vp,M]
+ * (padding columns/rows written as zero), dstd[A] (incl. the entropy term) and
+ * stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean}.
+ * partial: pmlp_ppo_loss_step_parts(M, A) floats of scratch.                */
+PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A);
+PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float* value, const float* actions,
+                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                                const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                                float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
+                                float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
+                                pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
 
 #endif

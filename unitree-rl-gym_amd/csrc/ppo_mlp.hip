@@ -199,7 +199,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         __syncthreads();  // the tile is written by every wave
         // row-major: 16-byte chunks along n; transposed: 16-byte chunks along m
         constexpr int RCH = BM * BN / 8;
-        for (int c = tid; c < RCH; c += NT) {
+        for (int c = tid; g.cb && c < RCH; c += NT) {
             const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
             const int row = m0 + lr, col = n0 + lc;
             if (row >= g.M || col >= g.N) continue;
@@ -266,19 +266,35 @@ __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
 struct RedJob {
     const float* slab;
     float* out;
+    float* bias_out;
     int64_t stride, n;
-    int nslabs;
+    int nslabs, cols_in, cols_out;
 };
 struct RedJobs {
     RedJob j[PMLP_MAX_JOBS];
 };
+// out = sum over slabs.  With bias_out: the slab is [rows, cols_in]; columns < cols_out go
+// to out[rows, cols_out] and column cols_out (the ones-row product) to bias_out[rows].
 __global__ void k_reduce_jobs(RedJobs jobs) {
     const RedJob J = jobs.j[blockIdx.y];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= J.n) return;
+    int64_t o = i;
+    float* dst = J.out;
+    if (J.bias_out) {
+        const int64_t row = i / J.cols_in, col = i % J.cols_in;
+        if (col < J.cols_out) {
+            o = row * J.cols_out + col;
+        } else if (col == J.cols_out) {
+            dst = J.bias_out;
+            o = row;
+        } else {
+            return;
+        }
+    }
     float s = 0.f;
     for (int k = 0; k < J.nslabs; ++k) s += J.slab[(size_t)k * J.stride + i];
-    J.out[i] = s;
+    dst[o] = s;
 }
 
 struct SumJob {
@@ -466,6 +482,117 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_std(LossArgs a, 
         for (int b = threadIdx.x; b < nblocks; b += PMLP_LOSS_THREADS) c += partial_std[(size_t)b * a.A + k];
         c = block_sum(c, sh);
         if (threadIdx.x == 0) dstd[k] = c - a.ecoef * gout[0] / a.stdv[k];  // + entropy term
+    }
+}
+
+// Fused PPO loss forward + backward for the optimizer step (the gradient of the
+// loss itself, gout = 1): one wave per 64 rows, writing the output gradients straight
+// into the MLP backward's bf16 operands (row-major and transposed, padded columns
+// zero) and per-wave partials of [surrogate, value loss, kl, d/dstd_k (k < A)].
+struct LossStepOut {
+    float* partial;
+    bf16 *dmu_b, *dmu_t, *dv_b, *dv_t;
+    int Ap, Vp;  // padded widths of the actor / critic output gradients
+};
+__global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    const int W = 3 + a.A;
+    float surr = 0.f, vl = 0.f, kl = 0.f, dlogp = 0.f;
+    const bool valid = i < a.M;
+    const size_t si = valid ? a.src(i) : 0;
+    if (valid) {
+        float logp = 0.f;
+        for (int k = 0; k < a.A; ++k) {
+            const float sg = a.stdv[k], mu = a.mu[(size_t)i * a.A + k];
+            const float d = a.actions[si * a.A + k] - mu;
+            logp += -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
+            const float os = a.old_sigma[si * a.A + k], om = a.old_mu[si * a.A + k] - mu;
+            kl += logf(sg / os + 1.0e-5f) + (os * os + om * om) / (2.f * sg * sg) - 0.5f;
+        }
+        const float ratio = expf(logp - a.old_logp[si]);
+        const float adv = a.adv[si];
+        const float lo = 1.f - a.clip, hi = 1.f + a.clip;
+        const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, lo), hi);
+        surr = fmaxf(s1, s2);
+        float w1, w2;
+        max_weights(s1, s2, w1, w2);
+        const float dclamp = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float gs = 1.f / (float)a.M, gv = a.vcoef / (float)a.M;
+        dlogp = gs * (-adv) * (w1 + w2 * dclamp) * ratio;
+        for (int k = 0; k < o.Ap; ++k) {
+            float g = 0.f;
+            if (k < a.A) {
+                const float sg = a.stdv[k];
+                const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
+                g = dlogp * d / (sg * sg);
+            }
+            o.dmu_b[(size_t)i * o.Ap + k] = (bf16)g;
+            o.dmu_t[(size_t)k * a.M + i] = (bf16)g;
+        }
+        const float v = a.value[i], r = a.ret[si];
+        float dv;
+        if (a.clipped_value) {
+            const float t = a.target[si];
+            const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
+            vl = fmaxf((v - r) * (v - r), (vc - r) * (vc - r));
+            float u1, u2;
+            max_weights((v - r) * (v - r), (vc - r) * (vc - r), u1, u2);
+            const float dcv = (v - t >= -a.clip && v - t <= a.clip) ? 1.f : 0.f;
+            dv = gv * (u1 * 2.f * (v - r) + u2 * 2.f * (vc - r) * dcv);
+        } else {
+            vl = (r - v) * (r - v);
+            dv = gv * 2.f * (v - r);
+        }
+        for (int k = 0; k < o.Vp; ++k) {
+            o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
+            o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+        }
+    }
+    auto wsum = [](float x) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        return x;
+    };
+    surr = wsum(surr);
+    vl = wsum(vl);
+    kl = wsum(kl);
+    if (threadIdx.x == 0) {
+        o.partial[(size_t)blockIdx.x * W + 0] = surr;
+        o.partial[(size_t)blockIdx.x * W + 1] = vl;
+        o.partial[(size_t)blockIdx.x * W + 2] = kl;
+    }
+    for (int k = 0; k < a.A; ++k) {
+        float c = 0.f;
+        if (valid) {
+            const float sg = a.stdv[k];
+            const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
+            c = dlogp * (d * d / (sg * sg * sg) - 1.f / sg);
+        }
+        c = wsum(c);
+        if (threadIdx.x == 0) o.partial[(size_t)blockIdx.x * W + 3 + k] = c;
+    }
+}
+
+// stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term
+__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_step_final(LossArgs a, const float* __restrict__ partial,
+                                                                           int nblocks, float* __restrict__ stats,
+                                                                           float* __restrict__ dstd) {
+    __shared__ float sh[4];
+    const int W = 3 + a.A;
+    const float inv = 1.f / (float)a.M;
+    for (int q = 0; q < W; ++q) {
+        float x = 0.f;
+        for (int b = threadIdx.x; b < nblocks; b += PMLP_LOSS_THREADS) x += partial[(size_t)b * W + q];
+        x = block_sum(x, sh);
+        if (threadIdx.x == 0) {
+            if (q < 3) stats[q] = x * inv;
+            else dstd[q - 3] = x - a.ecoef / a.stdv[q - 3];
+        }
+    }
+    if (threadIdx.x == 0) {
+        float ent = 0.f;
+        for (int k = 0; k < a.A; ++k) ent += 0.5f + kHalfLog2Pi + logf(a.stdv[k]);
+        stats[3] = ent;
     }
 }
 
@@ -889,7 +1016,7 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         if ((epi == PMLP_EPI_FWD_OUT || epi == PMLP_EPI_PARTIAL) && (!J.cf || J.ldcf < J.N))
             return fail(-1, w + "fp32 output missing or ldcf < N");
         if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) &&
-            (!J.cb || J.ldcb < J.N || (J.ct && (J.ldct < J.M || J.ldct % 4))))
+            ((!J.cb && !J.ct) || (J.cb && J.ldcb < J.N) || (J.ct && (J.ldct < J.M || J.ldct % 4))))
             return fail(-1, w + "bf16 output missing or bad leading dimension");
         if (epi == PMLP_EPI_BWD_DX && (!J.yprev || J.ldyp < J.N)) return fail(-1, w + "BWD_DX needs yprev");
         GemmArgs& g = gb.j[i];
@@ -923,9 +1050,10 @@ PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void*
     int64_t maxn = 0;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_reduce_job& J = jobs[i];
-        if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n)
+        if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n ||
+            (J.bias_out && (J.cols_in <= J.cols_out || J.cols_out <= 0 || J.n % J.cols_in)))
             return fail(-1, "pmlp_reduce_slabs: bad job " + std::to_string(i));
-        rj.j[i] = RedJob{J.slab, J.out, J.stride, J.n, J.nslabs};
+        rj.j[i] = RedJob{J.slab, J.out, J.bias_out, J.stride, J.n, J.nslabs, J.cols_in, J.cols_out};
         maxn = std::max(maxn, J.n);
     }
     const int bs = 256;
@@ -1094,6 +1222,29 @@ PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t
     else if (H0 == 256 && H1 == 128 && H2 == 64) hipLaunchKernelGGL((k_mlp4_fwd<256, 128, 64>), grid, block, 0, st, mj, M);
     else return fail(-1, "pmlp_mlp4_forward: hidden sizes (512,256,128) or (256,128,64)");
     PMLP_CHECK_LAUNCH("pmlp_mlp4_forward");
+    return 0;
+}
+
+PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A) { return ((M + 63) / 64) * (3 + A); }
+
+PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float* value, const float* actions,
+                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                                const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                                float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
+                                float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
+                                pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream) {
+    LossArgs a;
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
+                          clipped_value, vcoef, ecoef))
+        return e;
+    if (!partial || !stats || !dstd || !dmu || !dmu_t || !dvalue || !dvalue_t || Ap < A || Vp < 1)
+        return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
+    LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
+    const int nb = (M + 63) / 64;
+    hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
+    hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(1), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, partial,
+                       nb, stats, dstd);
+    PMLP_CHECK_LAUNCH("pmlp_ppo_loss_step");
     return 0;
 }
 

@@ -84,28 +84,25 @@ class FusedPPOStep:
         self.L = L
         self.k0p = [_ceil8(ls[0].in_features) for ls in self.lins]
         self.xb = [torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
-        self.xt = [torch.empty(k, M, dtype=bf, device=dev) for k in self.k0p]
+        # transposed activations carry 8 extra rows: a row of ones (then zeros) makes the
+        # weight-gradient GEMM's extra column the bias gradient (no separate row sums)
+        self.xt = [self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k) for k in self.k0p]
         self.wb = [[torch.empty(lin.out_features, self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
                     for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
         self.wt = [[torch.empty(lin.in_features, _ceil8(lin.out_features), dtype=bf, device=dev) if l > 0 else None
                     for l, lin in enumerate(ls)] for ls in self.lins]
         self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
-        self.yt = [[torch.empty(lin.out_features, M, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
+        self.yt = [[self._ones_row(torch.empty(lin.out_features + 8, M, dtype=bf, device=dev), lin.out_features)
+                    for lin in ls[:-1]] for ls in self.lins]
         self.out = [torch.empty(M, ls[-1].out_features, device=dev) for ls in self.lins]
         A = self.lins[0][-1].out_features
         if self.lins[1][-1].out_features != 1:
             raise ValueError("fused PPO step: the critic must output one value")
-        nb = mm.load().pmlp_ppo_loss_blocks(M)
-        self.loss_partial = torch.empty(4 * nb, device=dev)
-        self.loss = torch.empty((), device=dev)
-        self.one = torch.ones((), device=dev)
-        self.dmu = torch.empty(M, A, device=dev)
-        self.dvalue = torch.empty(M, 1, device=dev)
-        self.std_partial = torch.empty(A * nb, device=dev)
+        self.loss_partial = torch.empty(mm.load().pmlp_ppo_loss_step_parts(M, A), device=dev)
         # output gradients (bf16, both layouts) and the hidden-layer input gradients
         self.dz_out = [torch.empty(M, _ceil8(ls[-1].out_features), dtype=bf, device=dev) for ls in self.lins]
         self.dzt_out = [torch.empty(_ceil8(ls[-1].out_features), M, dtype=bf, device=dev) for ls in self.lins]
-        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 0 else None
+        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 1 else None
                     for l, lin in enumerate(ls)] for ls in self.lins]
         self.dzt = [[torch.empty(lin.in_features, M, dtype=bf, device=dev) if l > 0 else None
                      for l, lin in enumerate(ls)] for ls in self.lins]
@@ -114,13 +111,20 @@ class FusedPPOStep:
         self.ks, self.slab, self.dw_stage = [], [], []
         for l in range(L):
             kps = [self.k0p[n] if l == 0 else self.lins[n][l].in_features for n in range(2)]
-            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n]) for n in range(2)))
+            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n] + 8) for n in range(2)))
             nsl = (M + ks - 1) // ks
             self.ks.append(ks)
-            self.slab.append([torch.empty(nsl, self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
+            self.slab.append([torch.empty(nsl, self.lins[n][l].out_features, kps[n] + 8, device=dev)
+                              for n in range(2)])
             self.dw_stage.append([None if kps[n] == self.lins[n][l].in_features else
                                   torch.empty(self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
         self.opt_partial = torch.empty(mm.load().pmlp_opt_parts(), device=dev)
+
+    @staticmethod
+    def _ones_row(t, k):
+        t[k:].zero_()
+        t[k].fill_(1.0)
+        return t
 
     # -------------------------------------------------------- optimizer state --
     def sync_optimizer_state(self, opt):
@@ -178,23 +182,22 @@ class FusedPPOStep:
                     gj.append(dict(A=a_in, B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
                                    cb=self.y[n][l], ct=self.yt[n][l]))
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
-        # 3. loss forward / backward (rollout inputs read through `rows`)
+        # 3. loss forward + backward in one pass (rollout inputs read through `rows`); the
+        #    output gradients land directly in the backward's bf16 operands
         A = self.out[0].shape[1]
         std = ac.std.detach()
-        common = [mm._p(t) for t in (self.out[0], std, self.out[1], actions, logp, mu_old, sigma_old, adv, ret,
-                                     values)] + [mm._p(rows), M, A, float(alg.clip_param),
-                                                 int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
-                                                 float(alg.entropy_coef)]
         st = mm._stream()
-        mm._ok(lib.pmlp_ppo_loss_fwd(*common, mm._p(self.loss_partial), mm._p(self.loss), mm._p(self.stats), st),
-               "pmlp_ppo_loss_fwd")
-        mm._ok(lib.pmlp_ppo_loss_bwd(*common, mm._p(self.one), mm._p(self.dmu), mm._p(self.dvalue),
-                                     mm._p(self.std_partial), mm._p(self._gview[id(ac.std)]), st), "pmlp_ppo_loss_bwd")
-        # 4. backward through both MLPs
-        mm._convert([(self.dmu, self.dz_out[0].shape[1], self.dz_out[0], self.dzt_out[0]),
-                     (self.dvalue, self.dz_out[1].shape[1], self.dz_out[1], self.dzt_out[1])])
+        P = mm._p
+        mm._ok(lib.pmlp_ppo_loss_step(P(self.out[0]), P(std), P(self.out[1]), P(actions), P(logp), P(mu_old),
+                                      P(sigma_old), P(adv), P(ret), P(values), P(rows), M, A, float(alg.clip_param),
+                                      int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
+                                      float(alg.entropy_coef), P(self.loss_partial), P(self.stats),
+                                      P(self._gview[id(ac.std)]), P(self.dz_out[0]), P(self.dzt_out[0]),
+                                      self.dz_out[0].shape[1], P(self.dz_out[1]), P(self.dzt_out[1]),
+                                      self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
+        # 4. backward through both MLPs; the weight-gradient slabs carry the bias column
         dz, dzt = list(self.dz_out), list(self.dzt_out)
-        red, rsum, copies = [], [], []
+        red, copies = [], []
         for l in range(L - 1, -1, -1):
             gj = []
             for n in range(2):
@@ -202,10 +205,10 @@ class FusedPPOStep:
                 B = xt[n] if l == 0 else self.yt[n][l - 1]
                 kp = self.k0p[n] if l == 0 else lin.in_features
                 slab = self.slab[l][n]
-                gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab))
+                gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
                 dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
-                red.append((slab, dw, lin.out_features * kp, slab.shape[0]))
-                rsum.append((dzt[n], self._gview[id(lin.bias)], lin.out_features))
+                red.append((slab, dw, lin.out_features * (kp + 8), slab.shape[0], self._gview[id(lin.bias)],
+                            kp + 8, kp))
                 if self.dw_stage[l][n] is not None:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
             mm._gemm(mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
@@ -213,13 +216,14 @@ class FusedPPOStep:
                 gj = []
                 for n in range(2):
                     lin = self.lins[n][l]
+                    # the input layer's gradient is only consumed transposed (its weight gradient)
                     gj.append(dict(A=dz[n], B=self.wt[n][l], M=M, N=lin.in_features, K=dz[n].shape[1],
-                                   yprev=self.y[n][l - 1], cb=self.dz[n][l], ct=self.dzt[n][l]))
+                                   yprev=self.y[n][l - 1], cb=self.dz[n][l] if l > 1 else None,
+                                   ct=self.dzt[n][l]))
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
                 dzt = [self.dzt[n][l] for n in range(2)]
         mm._reduce(red)
-        mm._rowsum(rsum)
         for dst, srcv in copies:
             dst.copy_(srcv)
         # 5. data-parallel: one bucket (gradient + loss statistics)

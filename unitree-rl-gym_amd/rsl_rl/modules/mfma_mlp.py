@@ -42,8 +42,8 @@ class GemmJob(C.Structure):
 
 
 class ReduceJob(C.Structure):
-    _fields_ = [("slab", C.c_void_p), ("out", C.c_void_p), ("stride", C.c_int64), ("n", C.c_int64),
-                ("nslabs", C.c_int32)]
+    _fields_ = [("slab", C.c_void_p), ("out", C.c_void_p), ("bias_out", C.c_void_p), ("stride", C.c_int64),
+                ("n", C.c_int64), ("nslabs", C.c_int32), ("cols_in", C.c_int32), ("cols_out", C.c_int32)]
 
 
 class RowsumJob(C.Structure):
@@ -86,6 +86,10 @@ def load():
         L.pmlp_gae_parts.restype = i32
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
         L.pmlp_mlp4_forward.argtypes = [i32, C.POINTER(Mlp4Job), i32, i32, i32, i32, vp]
+        L.pmlp_ppo_loss_step_parts.argtypes = [i32, i32]
+        L.pmlp_ppo_loss_step_parts.restype = i32
+        L.pmlp_ppo_loss_step.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, i32, vp, vp,
+                                                     i32, vp]
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         _lib = L
@@ -152,9 +156,14 @@ def _gemm(epi, jobs, ksplit=0):
 
 
 def _reduce(jobs):
+    """jobs: (slab, out, n, nslabs[, bias_out, cols_in, cols_out])"""
+    def mk(j):
+        sl, out, n, ns = j[:4]
+        bias, ci, co = j[4:7] if len(j) > 4 else (None, 0, 0)
+        return ReduceJob(_p(sl), _p(out), _p(bias), n, n, ns, ci, co)
     for i in range(0, len(jobs), MAX_JOBS):
         chunk = jobs[i:i + MAX_JOBS]
-        arr = (ReduceJob * len(chunk))(*[ReduceJob(_p(sl), _p(out), n, n, ns) for sl, out, n, ns in chunk])
+        arr = (ReduceJob * len(chunk))(*[mk(j) for j in chunk])
         _ok(load().pmlp_reduce_slabs(len(chunk), arr, _stream()), "pmlp_reduce_slabs")
 
 
