@@ -16,6 +16,7 @@ kernel against the HBM roofline (algorithmic bytes), and the CPU
 oracle baseline (rank 0, N=1 only).
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -120,9 +121,10 @@ def main():
     dev = f"cuda:{local}"
     gargs = get_args(["--task", "go2", "--num_envs", str(args.num_envs), "--headless", "--sim_device", dev,
                       "--rl_device", dev])
-    env, env_cfg = task_registry.make_env(name="go2", args=gargs)
-    _, train_cfg = task_registry.get_cfgs("go2")
-    runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device=dev)
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+        env, env_cfg = task_registry.make_env(name="go2", args=gargs)
+        _, train_cfg = task_registry.get_cfgs("go2")
+        runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device=dev)
     T = runner.num_steps_per_env
     N = env.num_envs
 
@@ -132,20 +134,26 @@ def main():
     for i in range(20):
         env.step(acts[i % 8])
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.env_steps)]
+    env._sync_stream()
+    # (a) back-to-back lgs_step launches (k_step + its one-block extras kernel) between two
+    #     HIP events on the env's stream: the per-launch device time of the fused step
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    env.actions.copy_(acts[0])
     torch.cuda.synchronize(dev)
+    e0.record(stream)
+    for i in range(args.env_steps):
+        env._buf_idx ^= 1
+        env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
+        env.account_replayed_steps(1)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = e0.elapsed_time(e1) / args.env_steps
+    # (b) env.step() as the runner calls it (actions copy + launch + extras dict)
     t0 = time.time()
     for i in range(args.env_steps):
-        env._sync_stream()
-        env._buf_idx ^= 1
-        env.actions.copy_(acts[i % 8])
-        ev[i][0].record(stream)
-        env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
-        ev[i][1].record(stream)
-        env.account_replayed_steps(1)
+        env.step(acts[i % 8])
     torch.cuda.synchronize(dev)
     env_wall = time.time() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.env_steps
     env_only = N * args.env_steps / env_wall
 
     # ---- rollout leg: policy inference + env.step (no update)
