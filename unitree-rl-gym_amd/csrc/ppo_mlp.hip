@@ -42,6 +42,11 @@ static int fail(int code, const std::string& m) {
         if (_e != hipSuccess) return fail(-2, std::string(what) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
+// LDS stages of the GEMM main loop (2: one barrier per k-tile)
+#ifndef PMLP_NBUF
+#define PMLP_NBUF 1
+#endif
+
 struct GemmArgs {
     const bf16* A;
     const bf16* B;
@@ -74,9 +79,11 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     constexpr int ACH = BM * BK / 8, BCH = BN * BK / 8;  // 16-byte chunks per tile
     constexpr int AL = (ACH + NT - 1) / NT, BL = (BCH + NT - 1) / NT;
     static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
-    constexpr int CS = BN + 8;  // epilogue tile row stride (bf16)
-    constexpr int STAGE = (BM + BN) * LS, CTILE = BM * CS;
-    __shared__ __attribute__((aligned(16))) bf16 smem[STAGE > CTILE ? STAGE : CTILE];
+    constexpr int CS = BN + 8;  // row-major epilogue tile [BM][CS] (bf16)
+    constexpr int TS = BM + 8;  // transposed epilogue tile [BN][TS]: 16-B aligned rows, 2-way b64 writes
+    constexpr int STAGE = (BM + BN) * LS * PMLP_NBUF, CTILE = BM * CS, TTILE = BN * TS;
+    constexpr int SMEM = STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE);
+    __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
     bf16* As = smem;
     bf16* Bs = smem + BM * LS;
 
@@ -130,12 +137,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         }
     };
 
-    gload(kb);
-    for (int k0 = kb; k0 < ke; k0 += BK) {
-        __syncthreads();
-        lstore();
-        __syncthreads();
-        if (k0 + BK < ke) gload(k0 + BK);
+    auto compute = [&]() {
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             bf16x8 af[FM], bfr[FN];
@@ -150,10 +152,69 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 for (int j = 0; j < FN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
+    };
+
+    gload(kb);
+#if PMLP_NBUF == 2
+    // two LDS stages: the next k-tile is stored into the other stage while this one
+    // is consumed -> one barrier per k-tile
+    lstore();
+    __syncthreads();
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        const bool more = k0 + BK < ke;
+        if (more) gload(k0 + BK);
+        compute();
+        if (more) {
+            As = (As == smem) ? smem + (BM + BN) * LS : smem;
+            Bs = As + BM * LS;
+            lstore();
+        }
+        __syncthreads();
     }
+#else
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (k0 + BK < ke) gload(k0 + BK);
+        compute();
+    }
+#endif
 
     // ---- epilogue: lane owns column (lane&31), rows (t&3)+8(t>>2)+4(lane>>5)
-    if (EPI == PMLP_EPI_FWD_HIDDEN || EPI == PMLP_EPI_BWD_DX) __syncthreads();  // LDS reuse
+    constexpr int RCH = BM * BN / 8;  // 16-byte chunks of a bf16 output tile
+    if (EPI == PMLP_EPI_BWD_DX) {
+        // ELU' operand: the y tile [BM][BN] read coalesced (16-byte chunks along n),
+        // issued before the LDS-reuse barrier, then staged in LDS for the accumulator
+        // layout (per-element global loads in that layout cost 2x the kernel's time)
+        constexpr int YL = (RCH + NT - 1) / NT;
+        uint4 yr[YL];
+#pragma unroll
+        for (int u = 0; u < YL; ++u) {
+            const int c = tid + u * NT;
+            const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
+            const int row = m0 + lr, col = n0 + lc;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (c < RCH && row < g.M && col < g.N) {
+                if (col + 8 <= g.N && (g.ldyp % 8) == 0) {
+                    v = *(const uint4*)(g.yp + (size_t)row * g.ldyp + col);
+                } else {
+                    bf16x8 t;
+                    for (int e = 0; e < 8; ++e) t[e] = col + e < g.N ? g.yp[(size_t)row * g.ldyp + col + e] : (bf16)0.f;
+                    v = *(const uint4*)&t;
+                }
+            }
+            yr[u] = v;
+        }
+        __syncthreads();  // LDS reuse
+#pragma unroll
+        for (int u = 0; u < YL; ++u) {
+            const int c = tid + u * NT;
+            if (c < RCH) *(uint4*)(smem + (c / (BN / 8)) * CS + (c % (BN / 8)) * 8) = yr[u];
+        }
+        __syncthreads();
+    }
+    if (EPI == PMLP_EPI_FWD_HIDDEN) __syncthreads();  // LDS reuse
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -176,52 +237,81 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                     if (row < g.M) g.cf[(size_t)row * g.ldcf + col] = acc[i][j][t] + b;
                 }
             } else {
-                // bf16 result into the LDS tile; stored below in both layouts
+                // bias + ELU (forward) or ELU' (input gradient) in place; stored below
                 const float b = (EPI == PMLP_EPI_FWD_HIDDEN && g.bias && col < g.N) ? g.bias[col] : 0.f;
-                const int lc = wn * TN + j * 32 + (lane & 31);
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const int lr = wm * TM + i * 32 + 4 * (lane >> 5) + (t & 3) + 8 * (t >> 2);
-                    const int row = m0 + lr;
+                    const int row = rbase + (t & 3) + 8 * (t >> 2);
                     float v = acc[i][j][t];
                     if (EPI == PMLP_EPI_FWD_HIDDEN) {
                         v = elu(v + b);
                     } else {  // BWD_DX: d/dx ELU from its output y: 1 (y>0) or y+1
-                        const float y = (row < g.M && col < g.N) ? (float)g.yp[(size_t)row * g.ldyp + col] : 0.f;
+                        const int lr = row - m0, lc = col - n0;
+                        const float y = (float)smem[lr * CS + lc];
                         v = y > 0.f ? v : v * (y + 1.f);
                     }
-                    smem[lr * CS + lc] = (bf16)v;
+                    acc[i][j][t] = v;
                 }
             }
         }
     }
     if (EPI == PMLP_EPI_FWD_HIDDEN || EPI == PMLP_EPI_BWD_DX) {
-        __syncthreads();  // the tile is written by every wave
-        // row-major: 16-byte chunks along n; transposed: 16-byte chunks along m
-        constexpr int RCH = BM * BN / 8;
-        for (int c = tid; g.cb && c < RCH; c += NT) {
-            const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
-            const int row = m0 + lr, col = n0 + lc;
-            if (row >= g.M || col >= g.N) continue;
-            const bf16* src = smem + lr * CS + lc;
-            if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
-                *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
-            } else {
-                for (int u = 0; u < 8 && col + u < g.N; ++u) g.cb[(size_t)row * g.ldcb + col + u] = src[u];
+        if (EPI == PMLP_EPI_BWD_DX) __syncthreads();  // y tile consumed before the LDS is rewritten
+        if (g.cb) {
+            // row-major: bf16 tile [BM][CS] in LDS, then 16-byte chunks along n
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int lc = wn * TN + j * 32 + (lane & 31);
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) {
+                        const int lr = wm * TM + i * 32 + 4 * (lane >> 5) + (t & 3) + 8 * (t >> 2);
+                        smem[lr * CS + lc] = (bf16)acc[i][j][t];
+                    }
+                }
+            __syncthreads();
+            for (int c = tid; c < RCH; c += NT) {
+                const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
+                const int row = m0 + lr, col = n0 + lc;
+                if (row >= g.M || col >= g.N) continue;
+                const bf16* src = smem + lr * CS + lc;
+                if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
+                    *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
+                } else {
+                    for (int u = 0; u < 8 && col + u < g.N; ++u) g.cb[(size_t)row * g.ldcb + col + u] = src[u];
+                }
             }
+            if (g.ct) __syncthreads();  // the transposed tile reuses the LDS
         }
         if (g.ct) {
+            // transposed: a lane's 4 consecutive accumulator rows are 4 consecutive m of
+            // one column -> one 8-byte write into the [BN][TS] tile; then 16-byte chunks
+            // along m (coalesced rows of C^T)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int lc = wn * TN + j * 32 + (lane & 31);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int lr = wm * TM + i * 32 + 4 * (lane >> 5) + 8 * q;
+                        bf16x4 v;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v[u] = (bf16)acc[i][j][4 * q + u];
+                        *(bf16x4*)(smem + lc * TS + lr) = v;
+                    }
+                }
+            __syncthreads();
             for (int c = tid; c < RCH; c += NT) {
                 const int lc = c / (BM / 8), lr = (c % (BM / 8)) * 8;
                 const int col = n0 + lc, row = m0 + lr;
                 if (col >= g.N || row >= g.M) continue;
-                bf16x8 v;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = smem[(lr + u) * CS + lc];
+                const bf16* src = smem + lc * TS + lr;
                 if (row + 8 <= g.M && (g.ldct % 8) == 0) {
-                    *(bf16x8*)(g.ct + (size_t)col * g.ldct + row) = v;
+                    *(uint4*)(g.ct + (size_t)col * g.ldct + row) = *(const uint4*)src;
                 } else {
-                    for (int u = 0; u < 8 && row + u < g.M; ++u) g.ct[(size_t)col * g.ldct + row + u] = v[u];
+                    for (int u = 0; u < 8 && row + u < g.M; ++u) g.ct[(size_t)col * g.ldct + row + u] = src[u];
                 }
             }
         }
@@ -240,12 +330,16 @@ struct CvtJob {
 };
 struct CvtJobs {
     CvtJob j[PMLP_MAX_JOBS];
+    int start[PMLP_MAX_JOBS + 1];  // first block of each job (1-D grid, no idle blocks)
+    int gm[PMLP_MAX_JOBS];         // 64-row tiles of each job
+    int njobs;
 };
 __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
-    const CvtJob J = jobs.j[blockIdx.z];
-    const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    const int mext = J.yt ? max(J.M, J.ldyt) : J.M;
-    if (m0 >= mext || k0 >= J.Kp) return;
+    int jb = 0;
+    while (jb + 1 < jobs.njobs && (int)blockIdx.x >= jobs.start[jb + 1]) ++jb;
+    const CvtJob J = jobs.j[jb];
+    const int b = blockIdx.x - jobs.start[jb];
+    const int m0 = (b % jobs.gm[jb]) * 64, k0 = (b / jobs.gm[jb]) * 64;
     __shared__ float tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
@@ -272,29 +366,49 @@ struct RedJob {
 };
 struct RedJobs {
     RedJob j[PMLP_MAX_JOBS];
+    int start[PMLP_MAX_JOBS + 1];  // first block of each job (1-D grid)
+    int njobs;
 };
-// out = sum over slabs.  With bias_out: the slab is [rows, cols_in]; columns < cols_out go
-// to out[rows, cols_out] and column cols_out (the ones-row product) to bias_out[rows].
-__global__ void k_reduce_jobs(RedJobs jobs) {
-    const RedJob J = jobs.j[blockIdx.y];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= J.n) return;
-    int64_t o = i;
-    float* dst = J.out;
-    if (J.bias_out) {
-        const int64_t row = i / J.cols_in, col = i % J.cols_in;
-        if (col < J.cols_out) {
-            o = row * J.cols_out + col;
-        } else if (col == J.cols_out) {
-            dst = J.bias_out;
-            o = row;
-        } else {
-            return;
+// out = sum over slabs (slab order, per element: deterministic).  With bias_out: the slab
+// is [rows, cols_in]; columns < cols_out go to out[rows, cols_out] and column cols_out
+// (the ones-row product) to bias_out[rows].  Four consecutive elements per thread (16-byte
+// loads), the slab loop unrolled so the loads of several slabs are in flight together.
+__global__ __launch_bounds__(256) void k_reduce_jobs(RedJobs jobs) {
+    int jb = 0;
+    while (jb + 1 < jobs.njobs && (int)blockIdx.x >= jobs.start[jb + 1]) ++jb;
+    const RedJob J = jobs.j[jb];
+    const int64_t i0 = 4 * ((int64_t)(blockIdx.x - jobs.start[jb]) * blockDim.x + threadIdx.x);
+    if (i0 >= J.n) return;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (i0 + 4 <= J.n && (J.stride % 4) == 0 && ((uintptr_t)J.slab & 15) == 0) {
+        const float4* p = (const float4*)(J.slab + i0);
+        const int64_t st = J.stride / 4;
+#pragma unroll 8
+        for (int k = 0; k < J.nslabs; ++k) {
+            const float4 v = p[(size_t)k * st];
+            s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
         }
+    } else {
+        for (int k = 0; k < J.nslabs; ++k)
+            for (int e = 0; e < 4 && i0 + e < J.n; ++e) s[e] += J.slab[(size_t)k * J.stride + i0 + e];
     }
-    float s = 0.f;
-    for (int k = 0; k < J.nslabs; ++k) s += J.slab[(size_t)k * J.stride + i];
-    dst[o] = s;
+    for (int e = 0; e < 4 && i0 + e < J.n; ++e) {
+        const int64_t i = i0 + e;
+        int64_t o = i;
+        float* dst = J.out;
+        if (J.bias_out) {
+            const int64_t row = i / J.cols_in, col = i % J.cols_in;
+            if (col < J.cols_out) {
+                o = row * J.cols_out + col;
+            } else if (col == J.cols_out) {
+                dst = J.bias_out;
+                o = row;
+            } else {
+                continue;
+            }
+        }
+        dst[o] = s[e];
+    }
 }
 
 struct SumJob {
@@ -986,17 +1100,20 @@ PMLP_API const char* pmlp_last_error(void) { return g_err.c_str(); }
 PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream) {
     if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_convert: 1..PMLP_MAX_JOBS jobs");
     CvtJobs cj{};
-    int maxm = 0, maxk = 0;
+    cj.njobs = njobs;
+    int nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_convert_job& J = jobs[i];
         if (!J.x || J.M <= 0 || J.K <= 0 || J.Kp < J.K || J.ldx < J.K || (!J.y && !J.yt) || (J.yt && J.ldyt < J.M))
             return fail(-1, "pmlp_convert: bad job " + std::to_string(i));
         cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.rows, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0};
-        maxm = std::max(maxm, std::max(J.M, J.yt ? J.ldyt : 0));
-        maxk = std::max(maxk, J.Kp);
+        const int mext = std::max(J.M, J.yt ? J.ldyt : 0);
+        cj.gm[i] = (mext + 63) / 64;
+        cj.start[i] = nb;
+        nb += cj.gm[i] * ((J.Kp + 63) / 64);
     }
-    dim3 grid((maxm + 63) / 64, (maxk + 63) / 64, njobs);
-    hipLaunchKernelGGL(k_convert_jobs, grid, dim3(256), 0, (hipStream_t)stream, cj);
+    cj.start[njobs] = nb;
+    hipLaunchKernelGGL(k_convert_jobs, dim3(nb), dim3(256), 0, (hipStream_t)stream, cj);
     PMLP_CHECK_LAUNCH("pmlp_convert");
     return 0;
 }
@@ -1047,18 +1164,19 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
 PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream) {
     if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_reduce_slabs: 1..PMLP_MAX_JOBS jobs");
     RedJobs rj{};
-    int64_t maxn = 0;
+    int64_t nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_reduce_job& J = jobs[i];
         if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n ||
             (J.bias_out && (J.cols_in <= J.cols_out || J.cols_out <= 0 || J.n % J.cols_in)))
             return fail(-1, "pmlp_reduce_slabs: bad job " + std::to_string(i));
         rj.j[i] = RedJob{J.slab, J.out, J.bias_out, J.stride, J.n, J.nslabs, J.cols_in, J.cols_out};
-        maxn = std::max(maxn, J.n);
+        rj.start[i] = (int)nb;
+        nb += (J.n + 4 * 256 - 1) / (4 * 256);
     }
-    const int bs = 256;
-    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)((maxn + bs - 1) / bs), njobs), dim3(bs), 0, (hipStream_t)stream,
-                       rj);
+    rj.start[njobs] = (int)nb;
+    rj.njobs = njobs;
+    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, rj);
     PMLP_CHECK_LAUNCH("pmlp_reduce_slabs");
     return 0;
 }

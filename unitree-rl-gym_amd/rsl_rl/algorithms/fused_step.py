@@ -111,7 +111,8 @@ class FusedPPOStep:
         self.ks, self.slab, self.dw_stage = [], [], []
         for l in range(L):
             kps = [self.k0p[n] if l == 0 else self.lins[n][l].in_features for n in range(2)]
-            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n] + 8) for n in range(2)))
+            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n] + 8) for n in range(2)),
+                            slab_bytes=max(4 * self.lins[n][l].out_features * (kps[n] + 8) for n in range(2)))
             nsl = (M + ks - 1) // ks
             self.ks.append(ks)
             self.slab.append([torch.empty(nsl, self.lins[n][l].out_features, kps[n] + 8, device=dev)

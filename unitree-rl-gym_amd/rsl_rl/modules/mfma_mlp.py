@@ -188,9 +188,14 @@ def _tiles(M, N):
     return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
 
 
-def _ksplit(batch, tiles, target_blocks=256):
-    # >= ~1024 rows per slab: the slab combine reads every slab once
-    slabs = max(1, min(batch // 1024, round(target_blocks / tiles)))
+def _ksplit(batch, tiles, slab_bytes=0, target_blocks=256, min_rows=256, budget=12 << 20):
+    """Rows per slab of a split-K weight gradient: ~target_blocks workgroups per job (the
+    short-K GEMM is latency-bound, so more slabs = more blocks in flight), >= min_rows rows
+    per slab, and at most `budget` bytes of fp32 slabs per job (written once by the GEMM,
+    read once by the slab combine)."""
+    slabs = max(1, min(batch // min_rows, round(target_blocks / tiles)))
+    if slab_bytes:
+        slabs = max(1, min(slabs, budget // slab_bytes))
     ks = (batch + slabs - 1) // slabs
     return (ks + 63) // 64 * 64
 
@@ -271,7 +276,8 @@ class _MfmaMLPsFn(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             # weight gradients dW = dz^T x (split over the batch) for every net in one launch
             kps = [k0p[n] if l == 0 else shapes[n][l][1] for n in range(nnets)]
-            ks = _ksplit(M, max(_tiles(shapes[n][l][0], kps[n]) for n in range(nnets)))
+            ks = _ksplit(M, max(_tiles(shapes[n][l][0], kps[n]) for n in range(nnets)),
+                         slab_bytes=max(4 * shapes[n][l][0] * kps[n] for n in range(nnets)))
             slabs = (M + ks - 1) // ks
             gj = []
             for n in range(nnets):
