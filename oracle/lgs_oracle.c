@@ -168,33 +168,38 @@ static void fk(const lgs_model_desc* md, const float* root13, const float* dofq,
     }
 }
 
-/* dense Cholesky in place (lower), n <= NMAX */
-static void cholesky(float* M, int n) {
+/* dense Cholesky in place (lower), n <= NMAX.  The reciprocal of each pivot is taken
+ * once (IEEE 1/d) and every division by L_kk -- here and in the triangular solves --
+ * is a multiplication by it: the HIP kernel's arithmetic, operation for operation
+ * (one division per pivot instead of five on its serial chain). */
+static void cholesky(float* M, float* invd, int n) {
     for (int k = 0; k < n; ++k) {
         float d = M[k * NMAX + k];
         for (int s = 0; s < k; ++s) d -= M[k * NMAX + s] * M[k * NMAX + s];
         d = sqrtf(fmaxf(d, 1e-12f));
+        const float inv = 1.0f / d;
         M[k * NMAX + k] = d;
+        invd[k] = inv;
         for (int i = k + 1; i < n; ++i) {
             float v = M[i * NMAX + k];
             for (int s = 0; s < k; ++s) v -= M[i * NMAX + s] * M[k * NMAX + s];
-            M[i * NMAX + k] = v / d;
+            M[i * NMAX + k] = v * inv;
         }
     }
 }
-static void fwd_sub(const float* L, int n, float* x) {
+static void fwd_sub(const float* L, const float* invd, int n, float* x) {
     for (int i = 0; i < n; ++i) {
         float v = x[i];
         for (int s = 0; s < i; ++s) v -= L[i * NMAX + s] * x[s];
-        x[i] = v / L[i * NMAX + i];
+        x[i] = v * invd[i];
     }
 }
-static void bwd_sub(const float* L, int n, float* x) {
+static void bwd_sub(const float* L, const float* invd, int n, float* x) {
     /* subtraction order s = n-1 .. i+1 (the order a column sweep produces) */
     for (int i = n - 1; i >= 0; --i) {
         float v = x[i];
         for (int s = n - 1; s > i; --s) v -= L[s * NMAX + i] * x[s];
-        x[i] = v / L[i * NMAX + i];
+        x[i] = v * invd[i];
     }
 }
 
@@ -340,9 +345,10 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     float rhs[NMAX];
     for (int k = 0; k < 6; ++k) rhs[k] = -C[k];
     for (int j = 0; j < D; ++j) rhs[6 + j] = tau[j] - C[6 + j];
-    cholesky(M, n);
-    fwd_sub(M, n, rhs);
-    bwd_sub(M, n, rhs); /* rhs = qdd */
+    float invd[NMAX];
+    cholesky(M, invd, n);
+    fwd_sub(M, invd, n, rhs);
+    bwd_sub(M, invd, n, rhs); /* rhs = qdd */
 
     /* free velocity (classical velocity of the root origin after dt) */
     float qf[NMAX];
@@ -425,7 +431,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     static __thread float A[ROWMAX][ROWMAX];
     for (int r = 0; r < nr; ++r) {
         memcpy(Y[r], J[r], sizeof(float) * n);
-        fwd_sub(M, n, Y[r]);
+        fwd_sub(M, invd, n, Y[r]);
         float s = 0.f;
         for (int i = 0; i < n; ++i) s += J[r][i] * qf[i];
         v[r] = s;
@@ -468,7 +474,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         for (int r = 0; r < nr; ++r) s += Y[r][i] * lam[r];
         z[i] = s;
     }
-    bwd_sub(M, n, z);
+    bwd_sub(M, invd, n, z);
     float qn[NMAX];
     for (int i = 0; i < n; ++i) qn[i] = qf[i] + z[i];
     if (sp->clamp_joint_velocity)

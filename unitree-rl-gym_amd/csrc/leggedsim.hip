@@ -216,6 +216,7 @@ __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fmi
 template <int D, int B>
 struct ModelCache {
     int dof[B], depth[B], se[B], dofbody[D > 0 ? D : 1];
+    unsigned anc[D > 0 ? D : 1];  // bit i: DOF i is an ancestor-or-self of DOF j (i <= j)
     unsigned char chain[B][MAXD];
     float jr[B][9], jp[B][3], ax[B][3], com[B][3], mass[B], in[B][6];
     float lo[D > 0 ? D : 1], hi[D > 0 ? D : 1], vl[D > 0 ? D : 1];
@@ -232,11 +233,13 @@ struct Smem {
     float R[B][9], p[B][3], aw[B][3], cw[B][3];
     union {
         struct {
+            // per body, packed for 16-byte LDS reads in the subtree sums:
+            // pk  = [m, h(3), I(6), fn(3), ff(3)]  (spatial inertia at O, bias force)
+            // cpk = [cm, ch(3), cI(6), Fn(3), Ff(3)]  (the subtree sums of pk)
+            __attribute__((aligned(16))) float pk[B][16];
+            __attribute__((aligned(16))) float cpk[B][16];
             float Sw[B][3], Sv[B][3];
-            float m[B], h[B][3], I[B][6];
-            float fn[B][3], ff[B][3];
-            float cm[B], ch[B][3], cI[B][6];
-            float Fn[B][3], Ff[B][3];
+            __attribute__((aligned(16))) float Sd[D > 0 ? D : 1][8];  // per DOF: [Sw(3), Sv(3), 0, 0]
             float Fj[D][6];
         } dyn;
         struct {
@@ -285,6 +288,14 @@ __device__ __forceinline__ void load_model(Smem<D, B, ROWS>& s, const DevModel& 
     }
     for (int i = lane; i < 6 * B; i += WAVE) (&c.in[0][0])[i] = md.inertia[i];
     if (lane < D) {
+        int bj = 0;
+        for (int b = 0; b < B; ++b) bj = md.dof[b] == lane ? b : bj;
+        unsigned am = 0u;
+        for (int b = 0; b <= bj; ++b) {
+            const int i = md.dof[b];
+            if (i >= 0 && i <= lane && bj < md.subtree_end[b]) am |= 1u << i;
+        }
+        c.anc[lane] = am;
         c.lo[lane] = md.dof_lower[lane];
         c.hi[lane] = md.dof_upper[lane];
         c.vl[lane] = md.dof_velocity[lane];
@@ -378,19 +389,25 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         matmul(T, Rt, Iw);
         float r[3] = {s.cw[lane][0] - O[0], s.cw[lane][1] - O[1], s.cw[lane][2] - O[2]};
         float rr = dot3(r, r);
-        s.u.dyn.m[lane] = m;
-        s.u.dyn.h[lane][0] = m * r[0]; s.u.dyn.h[lane][1] = m * r[1]; s.u.dyn.h[lane][2] = m * r[2];
-        s.u.dyn.I[lane][0] = Iw[0] + m * (rr - r[0] * r[0]);
-        s.u.dyn.I[lane][1] = Iw[4] + m * (rr - r[1] * r[1]);
-        s.u.dyn.I[lane][2] = Iw[8] + m * (rr - r[2] * r[2]);
-        s.u.dyn.I[lane][3] = Iw[1] - m * r[0] * r[1];
-        s.u.dyn.I[lane][4] = Iw[2] - m * r[0] * r[2];
-        s.u.dyn.I[lane][5] = Iw[5] - m * r[1] * r[2];
+        s.u.dyn.pk[lane][0] = m;
+        s.u.dyn.pk[lane][1 + 0] = m * r[0]; s.u.dyn.pk[lane][1 + 1] = m * r[1]; s.u.dyn.pk[lane][1 + 2] = m * r[2];
+        s.u.dyn.pk[lane][4 + 0] = Iw[0] + m * (rr - r[0] * r[0]);
+        s.u.dyn.pk[lane][4 + 1] = Iw[4] + m * (rr - r[1] * r[1]);
+        s.u.dyn.pk[lane][4 + 2] = Iw[8] + m * (rr - r[2] * r[2]);
+        s.u.dyn.pk[lane][4 + 3] = Iw[1] - m * r[0] * r[1];
+        s.u.dyn.pk[lane][4 + 4] = Iw[2] - m * r[0] * r[2];
+        s.u.dyn.pk[lane][4 + 5] = Iw[5] - m * r[1] * r[2];
         float rp[3] = {s.p[lane][0] - O[0], s.p[lane][1] - O[1], s.p[lane][2] - O[2]}, sv[3];
         float a[3] = {s.aw[lane][0], s.aw[lane][1], s.aw[lane][2]};
         cross3(rp, a, sv);
 #pragma unroll
         for (int k = 0; k < 3; ++k) { s.u.dyn.Sw[lane][k] = a[k]; s.u.dyn.Sv[lane][k] = sv[k]; }
+        const int jd = mc.dof[lane];
+        if (jd >= 0) {
+            float4* o = (float4*)s.u.dyn.Sd[jd];
+            o[0] = make_float4(a[0], a[1], a[2], sv[0]);
+            o[1] = make_float4(sv[1], sv[2], 0.f, 0.f);
+        }
     }
     __syncthreads();
     STAMP(2);
@@ -418,11 +435,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                 Vv[k] += sv[k];
             }
         }
-        const float m = s.u.dyn.m[lane];
-        float h[3] = {s.u.dyn.h[lane][0], s.u.dyn.h[lane][1], s.u.dyn.h[lane][2]};
+        const float m = s.u.dyn.pk[lane][0];
+        float h[3] = {s.u.dyn.pk[lane][1 + 0], s.u.dyn.pk[lane][1 + 1], s.u.dyn.pk[lane][1 + 2]};
         float I[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) I[k] = s.u.dyn.I[lane][k];
+        for (int k = 0; k < 6; ++k) I[k] = s.u.dyn.pk[lane][4 + k];
         float IAn[3], IAf[3], IVn[3], IVf[3], a1[3], a2[3], a3[3];
         sin_apply(m, h, I, Aw, Av, IAn, IAf);
         sin_apply(m, h, I, Vw, Vv, IVn, IVf);
@@ -431,8 +448,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         cross3(Vw, IVf, a3);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            s.u.dyn.fn[lane][k] = IAn[k] + a1[k] + a2[k];
-            s.u.dyn.ff[lane][k] = IAf[k] + a3[k];
+            s.u.dyn.pk[lane][10 + k] = IAn[k] + a1[k] + a2[k];
+            s.u.dyn.pk[lane][13 + k] = IAf[k] + a3[k];
         }
     }
     __syncthreads();
@@ -442,21 +459,18 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // unrolling lets them overlap the 16 add chains.
     if (lane < B) {
         const int end = mc.se[lane];
-        float cm = 0.f, ch[3] = {0.f, 0.f, 0.f}, cI[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        float Fn[3] = {0.f, 0.f, 0.f}, Ff[3] = {0.f, 0.f, 0.f};
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
 #pragma unroll 4
         for (int k = end - 1; k >= lane; --k) {
-            cm += s.u.dyn.m[k];
-#pragma unroll
-            for (int t = 0; t < 3; ++t) { ch[t] += s.u.dyn.h[k][t]; Fn[t] += s.u.dyn.fn[k][t]; Ff[t] += s.u.dyn.ff[k][t]; }
-#pragma unroll
-            for (int t = 0; t < 6; ++t) cI[t] += s.u.dyn.I[k][t];
+            const float4* q = (const float4*)s.u.dyn.pk[k];
+            const float4 b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
+            a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+            a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+            a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
+            a3.x += b3.x; a3.y += b3.y; a3.z += b3.z; a3.w += b3.w;
         }
-        s.u.dyn.cm[lane] = cm;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) { s.u.dyn.ch[lane][t] = ch[t]; s.u.dyn.Fn[lane][t] = Fn[t]; s.u.dyn.Ff[lane][t] = Ff[t]; }
-#pragma unroll
-        for (int t = 0; t < 6; ++t) s.u.dyn.cI[lane][t] = cI[t];
+        float4* o = (float4*)s.u.dyn.cpk[lane];
+        o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
     }
     __syncthreads();
     // F_j = Ic(b_j) S_j (lane per DOF): the base block of M's row 6+j and, dotted
@@ -466,7 +480,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
         float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
         float cn[3], cf[3];
-        sin_apply(s.u.dyn.cm[bj], s.u.dyn.ch[bj], s.u.dyn.cI[bj], Sw, Sv, cn, cf);
+        sin_apply(s.u.dyn.cpk[bj][0], (&s.u.dyn.cpk[bj][1]), (&s.u.dyn.cpk[bj][4]), Sw, Sv, cn, cf);
 #pragma unroll
         for (int k = 0; k < 3; ++k) { s.u.dyn.Fj[lane][k] = cn[k]; s.u.dyn.Fj[lane][3 + k] = cf[k]; }
     }
@@ -478,9 +492,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
     for (int c = 0; c < n; ++c) m[c] = 0.f;
     if (lane < 6) {
-        const float* I = s.u.dyn.cI[0];
-        const float* h = s.u.dyn.ch[0];
-        const float cm0 = s.u.dyn.cm[0];
+        const float* I = (&s.u.dyn.cpk[0][4]);
+        const float* h = (&s.u.dyn.cpk[0][1]);
+        const float cm0 = s.u.dyn.cpk[0][0];
         // [[I, [h]x], [[h]x^T, m 1]]: rows 0-2 need cols 0-2 only (lower triangle)
         if (lane < 3) {
             const int r = lane;
@@ -495,7 +509,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             m[4] = (i == 1) ? cm0 : 0.f;
             m[5] = (i == 2) ? cm0 : 0.f;
         }
-        x = -(lane < 3 ? s.u.dyn.Fn[0][lane] : s.u.dyn.Ff[0][lane - 3]);
+        x = -(lane < 3 ? s.u.dyn.cpk[0][10 + lane] : s.u.dyn.cpk[0][13 + lane - 3]);
     } else if (lane < n) {
         const int j = lane - 6;
         const int bj = mc.dofbody[j];
@@ -504,22 +518,22 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < 3; ++k) { cn[k] = s.u.dyn.Fj[j][k]; cf[k] = s.u.dyn.Fj[j][3 + k]; }
         m[0] = cn[0]; m[1] = cn[1]; m[2] = cn[2];
         m[3] = cf[0]; m[4] = cf[1]; m[5] = cf[2];
+        const unsigned am = mc.anc[j];
 #pragma unroll
         for (int c = 6; c < n; ++c) {
             const int i = c - 6;
-            const int bi = mc.dofbody[i];
-            if (i <= j && bj >= bi && bj < mc.se[bi]) {
-                float Si_w[3] = {s.u.dyn.Sw[bi][0], s.u.dyn.Sw[bi][1], s.u.dyn.Sw[bi][2]};
-                float Si_v[3] = {s.u.dyn.Sv[bi][0], s.u.dyn.Sv[bi][1], s.u.dyn.Sv[bi][2]};
-                float val = dot3(Si_w, cn) + dot3(Si_v, cf);
-                if (i == j) val += sp.armature;
-                m[c] = val;
-            }
+            const float4* q = (const float4*)s.u.dyn.Sd[i];
+            const float4 s0 = q[0], s1 = q[1];
+            const float Si_w[3] = {s0.x, s0.y, s0.z};
+            const float Si_v[3] = {s0.w, s1.x, s1.y};
+            float val = dot3(Si_w, cn) + dot3(Si_v, cf);
+            if (i == j) val += sp.armature;
+            m[c] = ((am >> i) & 1u) ? val : 0.f;
         }
         float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
         float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
-        float Fn[3] = {s.u.dyn.Fn[bj][0], s.u.dyn.Fn[bj][1], s.u.dyn.Fn[bj][2]};
-        float Ff[3] = {s.u.dyn.Ff[bj][0], s.u.dyn.Ff[bj][1], s.u.dyn.Ff[bj][2]};
+        float Fn[3] = {s.u.dyn.cpk[bj][10 + 0], s.u.dyn.cpk[bj][10 + 1], s.u.dyn.cpk[bj][10 + 2]};
+        float Ff[3] = {s.u.dyn.cpk[bj][13 + 0], s.u.dyn.cpk[bj][13 + 1], s.u.dyn.cpk[bj][13 + 2]};
         float C = dot3(Sw, Fn) + dot3(Sv, Ff);
         x = s.tau[j] - C;
     }
@@ -527,15 +541,20 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // ---- 6. Cholesky, right-looking on register rows.  Entry (i,j) receives
     // -L_ik L_jk for k = 0..j-1 in ascending order, then / L_jj: the oracle's
     // left-looking arithmetic, operation for operation.
+    // One IEEE reciprocal per pivot (wave-uniform); every division by L_kk here and
+    // in the solves below is a multiplication by it (the oracle's arithmetic).  Lane k
+    // keeps 1/L_kk in idg.
+    float idg = 0.f;
 #pragma unroll
     for (int k = 0; k < n; ++k) {
         const float d = sqrtf(fmaxf(rl(m[k], k), 1e-12f));
-        if (lane == k) m[k] = d;
-        else if (lane > k) m[k] = m[k] / d;
+        const float inv = 1.0f / d;
+        m[k] = lane == k ? d : (lane > k ? m[k] * inv : m[k]);
+        idg = lane == k ? inv : idg;
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
             const float ljk = rl(m[k], j);
-            if (lane >= j) m[j] -= m[k] * ljk;
+            m[j] = lane >= j ? m[j] - m[k] * ljk : m[j];
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -549,9 +568,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // ---- 7. qdd = M^-1 rhs: forward on rows (registers), backward on columns
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-        if (lane == i) x = x / m[i];
+        x = lane == i ? x * idg : x;
         const float xi = rl(x, i);
-        if (lane > i) x -= m[i] * xi;
+        x = lane > i ? x - m[i] * xi : x;
     }
     __syncthreads();
     {
@@ -560,9 +579,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
 #pragma unroll
         for (int i = n - 1; i >= 0; --i) {
-            if (lane == i) x = x / lc[i];
+            x = lane == i ? x * idg : x;
             const float xi = rl(x, i);
-            if (lane < i) x -= lc[i] * xi;
+            x = lane < i ? x - lc[i] * xi : x;
         }
     }
     // free velocity (classical velocity of the root origin after dt)
@@ -683,7 +702,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             float t = y[i];
 #pragma unroll
             for (int k = 0; k < i; ++k) t -= rl(m[k], i) * y[k];
-            y[i] = t / rl(m[i], i);
+            y[i] = t * rl(idg, i);
             // keep row i's L broadcasts next to their use: hoisting all 171 of them
             // exhausts the SGPRs and spills the kernel to scratch
             __builtin_amdgcn_sched_barrier(0);
@@ -827,9 +846,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
 #pragma unroll
         for (int i = n - 1; i >= 0; --i) {
-            if (lane == i) z = z / lc[i];
+            z = lane == i ? z * idg : z;
             const float zi = rl(z, i);
-            if (lane < i) z -= lc[i] * zi;
+            z = lane < i ? z - lc[i] * zi : z;
         }
     }
     float qn = (lane < n) ? s.qf[lane] + z : 0.f;
