@@ -247,13 +247,18 @@ struct Smem {
             // <= 32 rows: A never leaves registers (one MFMA tile, columns per lane)
             float A[ROWS > 32 ? ROWS : 1][ROWS > 32 ? AS : 1];
         } con;
+        struct {  // FK scratch: per-DOF joint rotation R(axis, q)
+            float Ra[D > 0 ? D : 1][9];
+        } fk;
         struct {  // post-physics scratch
             float obs_tmp[LGS_MAX_OBS];
             float terms[LGS_MAX_REWARDS + 1];
             float misc[32];
         } post;
     } u;
-    float L[n][NP];
+    static constexpr int LP = (n + 3) / 4 * 4;  // 16-byte rows: uniform row reads are ds_read_b128
+    __attribute__((aligned(16))) float L[n][LP];
+    float Linv[n];
     float qf[n];
     float tgt[ROWS];
     int c_body[ROWS / 3];
@@ -327,7 +332,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     const float dt = sp.dt;
 
     STAMP(0);
-    // ---- 1. forward kinematics: lane b walks root..b
+    // ---- 1. forward kinematics: joint rotations lane per DOF, then lane b walks root..b
+    if (lane < D) axis_angle(mc.ax[mc.dofbody[lane]], s.q[lane], s.u.fk.Ra[lane]);
+    __syncthreads();
     if (lane < B) {
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
         quat_to_mat(s.root + 3, R);
@@ -342,9 +349,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             const int j = mc.dof[a];
             if (j >= 0) {
                 if (l == d) matvec(Rj, mc.ax[a], aw);
-                float Ra[9];
-                axis_angle(mc.ax[a], s.q[j], Ra);
-                matmul(Rj, Ra, R);
+                matmul(Rj, s.u.fk.Ra[j], R);
             } else {
 #pragma unroll
                 for (int k = 0; k < 9; ++k) R[k] = Rj[k];
@@ -547,14 +552,19 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     float idg = 0.f;
 #pragma unroll
     for (int k = 0; k < n; ++k) {
+        // opaque per step: lane masks are recomputed here (one v_cmp each) instead of
+        // being CSE'd across the factorisation and solves, where ~70 live mask SGPRs
+        // spilled to VGPR lanes
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
         const float d = sqrtf(fmaxf(rl(m[k], k), 1e-12f));
         const float inv = 1.0f / d;
-        m[k] = lane == k ? d : (lane > k ? m[k] * inv : m[k]);
-        idg = lane == k ? inv : idg;
+        m[k] = ln == k ? d : (ln > k ? m[k] * inv : m[k]);
+        idg = ln == k ? inv : idg;
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
             const float ljk = rl(m[k], j);
-            m[j] = lane >= j ? m[j] - m[k] * ljk : m[j];
+            m[j] = ln >= j ? m[j] - m[k] * ljk : m[j];
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -563,14 +573,17 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int c = 0; c < n; ++c)
             if (c <= lane) s.L[lane][c] = m[c];
+        s.Linv[lane] = idg;
     }
     STAMP(6);
     // ---- 7. qdd = M^-1 rhs: forward on rows (registers), backward on columns
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-        x = lane == i ? x * idg : x;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        x = ln == i ? x * idg : x;
         const float xi = rl(x, i);
-        x = lane > i ? x - m[i] * xi : x;
+        x = ln > i ? x - m[i] * xi : x;
     }
     __syncthreads();
     {
@@ -579,9 +592,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
 #pragma unroll
         for (int i = n - 1; i >= 0; --i) {
-            x = lane == i ? x * idg : x;
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            x = ln == i ? x * idg : x;
             const float xi = rl(x, i);
-            x = lane < i ? x - lc[i] * xi : x;
+            x = ln < i ? x - lc[i] * xi : x;
         }
     }
     // free velocity (classical velocity of the root origin after dt)
@@ -697,15 +712,15 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int i = 0; i < n; ++i) y[i] = used ? s.u.con.Y[lane][i] : 0.f;
 #pragma unroll
         for (int i = 0; i < n; ++i) v += y[i] * s.qf[i];
+        // row i of L and 1/L_ii as wave-uniform LDS reads (16-byte row loads on the LDS
+        // pipe) instead of ~170 v_readlane broadcasts on the VALU
 #pragma unroll
         for (int i = 0; i < n; ++i) {
+            const float* Li = s.L[i];
             float t = y[i];
 #pragma unroll
-            for (int k = 0; k < i; ++k) t -= rl(m[k], i) * y[k];
-            y[i] = t * rl(idg, i);
-            // keep row i's L broadcasts next to their use: hoisting all 171 of them
-            // exhausts the SGPRs and spills the kernel to scratch
-            __builtin_amdgcn_sched_barrier(0);
+            for (int k = 0; k < i; ++k) t -= Li[k] * y[k];
+            y[i] = t * s.Linv[i];
         }
         if (lane < ROWS) {
 #pragma unroll
@@ -846,9 +861,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
 #pragma unroll
         for (int i = n - 1; i >= 0; --i) {
-            z = lane == i ? z * idg : z;
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            z = ln == i ? z * idg : z;
             const float zi = rl(z, i);
-            z = lane < i ? z - lc[i] * zi : z;
+            z = ln < i ? z - lc[i] * zi : z;
         }
     }
     float qn = (lane < n) ? s.qf[lane] + z : 0.f;
