@@ -174,6 +174,9 @@ typedef struct lgs_task_params {
     /* 1: refresh rigid_body_states [N,B,13] every control step (the humanoid envs
      * read it, h1_env.py:37,49); 0: leave it untouched (LeggedRobot never reads it) */
     int32_t write_body_states;
+    /* 1: env origins are terrain tiles (legged_robot.py:582-585, custom_origins): reset_idx adds a
+     * U[-1,1] xy offset to the root position (LGS_STREAM_RESET_ROOT draws 6, 7) */
+    int32_t custom_origins;
 } lgs_task_params;
 
 /* ---- per-env buffers of the VecEnv (device pointers; torch owns them) ---- */
@@ -253,6 +256,16 @@ LGS_API int lgs_set_task(lgs_sim* sim, const lgs_task_params* task);
 LGS_API int lgs_step(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(all) as used by BaseTask.reset (base_task.py:82-86) */
 LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+
+/* gym.add_heightfield -- the rough-terrain ground of legged_gym (utils/terrain.py builds
+ * height_field_raw; the reference's create_sim only ever adds the plane, legged_robot.py:240-257).
+ * heights: HOST int16 [rows][cols]; sample (i, j) sits at world x = i*horizontal_scale - border_size,
+ * y = j*horizontal_scale - border_size, z = heights[i][j]*vertical_scale.  Cell (i, j) is split into
+ * two triangles along its (i,j)-(i+1,j+1) diagonal (terrain_utils.convert_heightfield_to_trimesh);
+ * contact points are tested against the triangle under them (outside the map: its edge samples).
+ * Replaces the z = 0 plane for every env; heights = NULL (or rows = 0) restores the plane. */
+LGS_API int lgs_set_heightfield(lgs_sim* sim, const int16_t* heights, int32_t rows, int32_t cols,
+                                float horizontal_scale, float vertical_scale, float border_size);
 
 /* name/index queries */
 LGS_API int lgs_get_counts(lgs_sim* sim, int32_t* num_envs, int32_t* num_bodies, int32_t* num_dofs);

@@ -72,9 +72,26 @@ def _env_struct(b):
     return E
 
 
+_ground = None  # the heightfield array the oracle points at (kept alive here)
+
+
+def set_ground(lib, terrain=None, terrain_cfg=None):
+    """Point the oracle's contact ground at an env's heightfield (or the z = 0 plane)."""
+    global _ground
+    if terrain is None:
+        lib.orc_set_heightfield(None, 0, 0, 0.0, 0.0, 0.0)
+        _ground = None
+        return
+    _ground = np.ascontiguousarray(terrain.heightsamples, dtype=np.int16)
+    lib.orc_set_heightfield(_ground.ctypes.data, _ground.shape[0], _ground.shape[1],
+                            float(terrain_cfg.horizontal_scale), float(terrain_cfg.vertical_scale),
+                            float(terrain_cfg.border_size))
+
+
 def step(env, snap, actions, step_counter, lib=None):
     """One fused control step of every env on the CPU oracle.  Returns new arrays."""
     lib = lib or ensure_built()
+    set_ground(lib, getattr(env, "terrain", None), env.cfg.terrain)
     b = {k: (None if v is None else np.ascontiguousarray(v).copy()) for k, v in snap.items()}
     b["actions"] = np.ascontiguousarray(actions, dtype=np.float32).copy()
     b["episode_acc"][:] = 0
@@ -87,9 +104,10 @@ def step(env, snap, actions, step_counter, lib=None):
     return b
 
 
-def step_raw(model, sim_params, task, num_envs, bufs, step_counter, lib=None):
+def step_raw(model, sim_params, task, num_envs, bufs, step_counter, lib=None, terrain=None, terrain_cfg=None):
     """orc_step on caller-provided host arrays (bench cpu_baseline / golden tests)."""
     lib = lib or ensure_built()
+    set_ground(lib, terrain, terrain_cfg)
     mh = cabi.ModelHandle(model)
     E = _env_struct(bufs)
     p = lambda a: a.ctypes.data  # noqa: E731

@@ -65,6 +65,59 @@ static void cross3(const float a[3], const float b[3], float o[3]) {
     float z = a[0] * b[1] - a[1] * b[0];
     o[0] = x; o[1] = y; o[2] = z;
 }
+
+/* ---- ground: the z = 0 plane, or a heightfield (lgs_set_heightfield semantics).
+ * Cell (i, j) is split along its (i,j)-(i+1,j+1) diagonal (isaacgym
+ * terrain_utils.convert_heightfield_to_trimesh); outside the map the edge samples
+ * continue.  Set once per process by orc_set_heightfield (test infrastructure). */
+static struct {
+    const int16_t* h;
+    int rows, cols;
+    float inv_hs, vs, border;
+} g_hf;
+
+void orc_set_heightfield(const int16_t* heights, int rows, int cols, float horizontal_scale, float vertical_scale,
+                         float border_size) {
+    g_hf.h = (heights && rows > 0) ? heights : NULL;
+    g_hf.rows = rows; g_hf.cols = cols;
+    g_hf.inv_hs = horizontal_scale > 0.f ? 1.0f / horizontal_scale : 0.f;
+    g_hf.vs = vertical_scale;
+    g_hf.border = border_size;
+}
+
+/* ground height under (x, y) and the unit normal of the triangle there */
+float orc_terrain_sample(float x, float y, float* nrm) {
+    if (!g_hf.h) {
+        nrm[0] = 0.f; nrm[1] = 0.f; nrm[2] = 1.f;
+        return 0.f;
+    }
+    float u = (x + g_hf.border) * g_hf.inv_hs, v = (y + g_hf.border) * g_hf.inv_hs;
+    u = fminf(fmaxf(u, 0.f), (float)(g_hf.rows - 1));
+    v = fminf(fmaxf(v, 0.f), (float)(g_hf.cols - 1));
+    int i = (int)u, j = (int)v;
+    if (i > g_hf.rows - 2) i = g_hf.rows - 2;
+    if (j > g_hf.cols - 2) j = g_hf.cols - 2;
+    const float fu = u - (float)i, fv = v - (float)j;
+    const int16_t* h0 = g_hf.h + (size_t)i * g_hf.cols + j;
+    const float h00 = (float)h0[0] * g_hf.vs, h01 = (float)h0[1] * g_hf.vs;
+    const float h10 = (float)h0[g_hf.cols] * g_hf.vs, h11 = (float)h0[g_hf.cols + 1] * g_hf.vs;
+    float du, dv;
+    if (fu >= fv) { du = h10 - h00; dv = h11 - h10; }
+    else { du = h11 - h01; dv = h01 - h00; }
+    const float h = h00 + fu * du + fv * dv;
+    const float gx = du * g_hf.inv_hs, gy = dv * g_hf.inv_hs;
+    const float inv = 1.f / sqrtf(gx * gx + gy * gy + 1.f);
+    nrm[0] = 0.f - gx * inv; nrm[1] = 0.f - gy * inv; nrm[2] = inv;
+    return h;
+}
+
+/* contact frame: t1 = normalise(e_x - n_x n), t2 = n x t1 (flat ground: +x, +y exactly) */
+static void contact_tangents(const float* n, float* t1, float* t2) {
+    const float a0 = 1.f - n[0] * n[0], a1 = 0.f - n[0] * n[1], a2 = 0.f - n[0] * n[2];
+    const float inv = 1.f / sqrtf(a0 * a0 + a1 * a1 + a2 * a2);
+    t1[0] = a0 * inv; t1[1] = a1 * inv; t1[2] = a2 * inv;
+    cross3(n, t1, t2);
+}
 static float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 static void matvec(const float R[9], const float v[3], float o[3]) {
     float x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
@@ -374,17 +427,25 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     const int max_limit = max_rows - 3 * sp->max_contacts;
     int nc = 0;
     float cpt[ROWMAX / 3 + 1][3];
+    float cfr[ROWMAX / 3 + 1][3][3]; /* contact frame: normal, tangent 1, tangent 2 */
     for (int k = 0; k < md->num_points; ++k) {
         if (nc >= sp->max_contacts || nr + 3 > max_rows) break;
         int b = md->pt_body[k];
         float c[3];
         matvec(K.R[b], md->pt_pos + 3 * k, c);
         c[0] += K.p[b][0]; c[1] += K.p[b][1]; c[2] += K.p[b][2];
-        float sep = c[2] - md->pt_radius[k] - sp->rest_offset;
+        float nrm[3];
+        const float rad = md->pt_radius[k];
+        const float hg = orc_terrain_sample(c[0], c[1], nrm);
+        /* signed distance of the sphere centre to the ground triangle's plane */
+        float sep = (c[2] - hg) * nrm[2] - rad - sp->rest_offset;
         if (!(sep < sp->contact_offset)) continue;
-        float pc[3] = {c[0], c[1], c[2] - md->pt_radius[k]};
+        float pc[3] = {c[0] - rad * nrm[0], c[1] - rad * nrm[1], c[2] - rad * nrm[2]};
         float r[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]};
-        static const float dirs[3][3] = {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}};
+        float dirs[3][3];
+        memcpy(dirs[0], nrm, 12);
+        contact_tangents(nrm, dirs[1], dirs[2]);
+        memcpy(cfr[nc], dirs, 36);
         for (int dd = 0; dd < 3; ++dd) {
             const float* d = dirs[dd];
             float* row = J[nr + dd];
@@ -487,9 +548,8 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     for (int c = 0; c < nc; ++c) {
         int r = 3 * c;
         float* F = cforce + 3 * cb[c];
-        F[0] += lam[r + 1] / dt;
-        F[1] += lam[r + 2] / dt;
-        F[2] += lam[r] / dt;
+        for (int t = 0; t < 3; ++t) /* ln n + l1 t1 + l2 t2 */
+            F[t] += (lam[r] * cfr[c][0][t] + lam[r + 1] * cfr[c][1][t] + lam[r + 2] * cfr[c][2][t]) / dt;
     }
     (void)cpt;
     /* integrate (semi-implicit Euler) */
@@ -828,6 +888,8 @@ void orc_post_physics_env(const lgs_model_desc* md, const lgs_task_params* T, in
         }
         for (int k = 0; k < 13; ++k) root[k] = T->base_init_state[k];  /* _reset_root_states :587-590 */
         for (int k = 0; k < 3; ++k) root[k] += E->env_origins[3 * e + k];
+        if (T->custom_origins) /* terrain tiles: xy within 1 m of the centre (:582-585) */
+            for (int k = 0; k < 2; ++k) root[k] += rand_range(-1.f, 1.f, orc_uniform(seed, e, step, LGS_STREAM_RESET_ROOT, 6 + k));
         for (int k = 0; k < 6; ++k) root[7 + k] = rand_range(-0.5f, 0.5f, orc_uniform(seed, e, step, LGS_STREAM_RESET_ROOT, k));
         resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_RESET_CMD);
         for (int j = 0; j < A; ++j) { act[j] = 0.f; last_act[j] = 0.f; }

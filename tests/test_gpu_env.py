@@ -72,6 +72,39 @@ def test_fused_step_matches_oracle(task):
         compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=0.01)
 
 
+@pytest.mark.parametrize("task", ["go2", "g1_rough"])
+def test_heightfield_step_matches_oracle(task):
+    """Rough terrain (lgs_set_heightfield: the utils/terrain.py curriculum map, envs on
+    its tiles): one fused control step vs the oracle on the same heightfield, with the
+    tile-origin resets (custom_origins xy jitter) included."""
+    env = make(task, 512, terrain__mesh_type="heightfield", terrain__num_rows=5, terrain__num_cols=8)
+    assert env.terrain is not None and env.custom_origins
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(30):
+        env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
+    for _ in range(3):
+        snap = bridge.snapshot(env)
+        a = 0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g)
+        ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
+        env.step(a)
+        torch.cuda.synchronize()
+        compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
+        compare(env, ref, ["obs", "rew", "commands", "feet_air_time", "last_contacts", "episode_sums"] +
+                (["priv_obs"] if env.num_privileged_obs else []), 1e-4, frac_ok=0.01)
+        compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=0.01)
+    # the robots stand on the terrain, not on z = 0: feet above the local ground
+    hs = env.cfg.terrain.horizontal_scale
+    b = env.cfg.terrain.border_size
+    root = env.root_states[:, :3]
+    hf = env.height_samples
+    i = ((root[:, 0] + b) / hs).long().clamp(0, hf.shape[0] - 1)
+    j = ((root[:, 1] + b) / hs).long().clamp(0, hf.shape[1] - 1)
+    ground = hf[i, j].float() * env.cfg.terrain.vertical_scale
+    assert float((root[:, 2] - ground).median()) > 0.1
+    bridge.set_ground(bridge.ensure_built())
+
+
 @pytest.mark.parametrize("task", ["go2", "h1"])
 def test_timeouts_reset_push_match_oracle_exactly(task):
     """Every env times out at once: the reset/push/resample draws (Philox) and the

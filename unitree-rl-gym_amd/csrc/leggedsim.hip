@@ -105,6 +105,10 @@ struct DevSim {
     int iters;
     float contact_offset, rest_offset, max_depen, beta, ground_friction, armature;
     int clamp_qd, max_contacts, max_rows;
+    // heightfield ground (lgs_set_heightfield); hf == nullptr: the z = 0 plane
+    const int16_t* hf;
+    int hf_rows, hf_cols;
+    float hf_inv_hs, hf_vs, hf_border;
 };
 
 struct DevState {
@@ -208,6 +212,42 @@ __host__ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint32_t
     return (float)(c0 >> 8) * (1.0f / 16777216.0f);
 }
 __device__ __forceinline__ float rand_range(float lo, float hi, float u) { return (hi - lo) * u + lo; }
+
+// ------------------------------------------------------------- terrain --
+// Ground height under (x, y) and the unit normal of the triangle there.  The
+// heightfield cell (i, j) is split along its (i,j)-(i+1,j+1) diagonal
+// (terrain_utils.convert_heightfield_to_trimesh); outside the map the edge samples
+// continue.  Without a heightfield: the plane z = 0, normal +z.  Same arithmetic
+// as oracle/lgs_oracle.c terrain_sample().
+__device__ __forceinline__ float terrain_sample(const DevSim& sp, float x, float y, float* nrm) {
+    if (!sp.hf) {
+        nrm[0] = 0.f; nrm[1] = 0.f; nrm[2] = 1.f;
+        return 0.f;
+    }
+    float u = (x + sp.hf_border) * sp.hf_inv_hs, v = (y + sp.hf_border) * sp.hf_inv_hs;
+    u = fminf(fmaxf(u, 0.f), (float)(sp.hf_rows - 1));
+    v = fminf(fmaxf(v, 0.f), (float)(sp.hf_cols - 1));
+    const int i = min((int)u, sp.hf_rows - 2), j = min((int)v, sp.hf_cols - 2);
+    const float fu = u - (float)i, fv = v - (float)j;
+    const int16_t* h0 = sp.hf + (size_t)i * sp.hf_cols + j;
+    const float h00 = (float)h0[0] * sp.hf_vs, h01 = (float)h0[1] * sp.hf_vs;
+    const float h10 = (float)h0[sp.hf_cols] * sp.hf_vs, h11 = (float)h0[sp.hf_cols + 1] * sp.hf_vs;
+    float du, dv;
+    if (fu >= fv) { du = h10 - h00; dv = h11 - h10; }
+    else { du = h11 - h01; dv = h01 - h00; }
+    const float h = h00 + fu * du + fv * dv;
+    const float gx = du * sp.hf_inv_hs, gy = dv * sp.hf_inv_hs;
+    const float inv = 1.f / sqrtf(gx * gx + gy * gy + 1.f);
+    nrm[0] = 0.f - gx * inv; nrm[1] = 0.f - gy * inv; nrm[2] = inv;
+    return h;
+}
+// contact frame: t1 = normalise(e_x - n_x n), t2 = n x t1 (flat ground: +x, +y exactly)
+__device__ __forceinline__ void contact_tangents(const float* n, float* t1, float* t2) {
+    const float a0 = 1.f - n[0] * n[0], a1 = 0.f - n[0] * n[1], a2 = 0.f - n[0] * n[2];
+    const float inv = 1.f / sqrtf(a0 * a0 + a1 * a1 + a2 * a2);
+    t1[0] = a0 * inv; t1[1] = a1 * inv; t1[2] = a2 * inv;
+    cross3(n, t1, t2);
+}
 __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
 // ------------------------------------------------------------ LDS layout --
@@ -263,6 +303,7 @@ struct Smem {
     float tgt[ROWS];
     int c_body[ROWS / 3];
     float c_pt[ROWS / 3][3];
+    float c_fr[ROWS / 3][9];  // contact frame: normal, tangent 1, tangent 2
     float c_sep[ROWS / 3];
     float cf[B][3];
     int flags[8];
@@ -624,7 +665,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int base = 0; base < md.P && nc < maxc; base += WAVE) {
             const int k = base + lane;
             bool act = false;
-            float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f;
+            float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f, nrm[3] = {0.f, 0.f, 1.f};
             int b = 0;
             if (k < md.P) {
                 b = md.pt_body[k];
@@ -635,15 +676,25 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                 for (int t = 0; t < 9; ++t) R[t] = s.R[b][t];
                 matvec(R, pp, c);
                 c[0] += s.p[b][0]; c[1] += s.p[b][1]; c[2] += s.p[b][2];
-                sep = c[2] - rad - sp.rest_offset;
+                // signed distance of the point's sphere centre to the ground triangle's plane
+                const float h = terrain_sample(sp, c[0], c[1], nrm);
+                sep = (c[2] - h) * nrm[2] - rad - sp.rest_offset;
                 act = sep < sp.contact_offset;
             }
             const uint64_t mask = __ballot(act);
             const int slot = nc + __popcll(mask & ((1ull << lane) - 1ull));
             if (act && slot < maxc) {
                 s.c_body[slot] = b;
-                s.c_pt[slot][0] = c[0]; s.c_pt[slot][1] = c[1]; s.c_pt[slot][2] = c[2] - rad;
+                s.c_pt[slot][0] = c[0] - rad * nrm[0];
+                s.c_pt[slot][1] = c[1] - rad * nrm[1];
+                s.c_pt[slot][2] = c[2] - rad * nrm[2];
                 s.c_sep[slot] = sep;
+                float t1[3], t2[3];
+                contact_tangents(nrm, t1, t2);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    s.c_fr[slot][t] = nrm[t]; s.c_fr[slot][3 + t] = t1[t]; s.c_fr[slot][6 + t] = t2[t];
+                }
             }
             nc += __popcll(mask);
             if (nc > maxc) nc = maxc;
@@ -679,7 +730,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // contact rows (lane per row): J row into Y[r]
     if (lane < 3 * nc) {
         const int cc = lane / 3, dd = lane % 3;
-        const float d[3] = {dd == 1 ? 1.f : 0.f, dd == 2 ? 1.f : 0.f, dd == 0 ? 1.f : 0.f};
+        const float d[3] = {s.c_fr[cc][3 * dd], s.c_fr[cc][3 * dd + 1], s.c_fr[cc][3 * dd + 2]};
         const int b = s.c_body[cc];
         float pc[3] = {s.c_pt[cc][0], s.c_pt[cc][1], s.c_pt[cc][2]};
         float r[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]}, rxd[3];
@@ -880,7 +931,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
                 const float ln = rl(lam, 3 * c), l1 = rl(lam, 3 * c + 1), l2 = rl(lam, 3 * c + 2);
-                if (s.c_body[c] == lane) { F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt; }
+                if (s.c_body[c] == lane) {
+                    const float* fr = s.c_fr[c];  // world force = ln n + l1 t1 + l2 t2
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) / dt;
+                }
             }
         if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
     }
@@ -1290,6 +1345,9 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         if (lane < 13) {
             float x = T.base_init_state[lane];
             if (lane < 3) x += E.env_origins[3 * e + lane];
+            // terrain origins: xy within 1 m of the tile centre (legged_robot.py:582-585)
+            if (lane < 2 && T.custom_origins)
+                x += rand_range(-1.f, 1.f, philox_uniform(seed, e, step, LGS_STREAM_RESET_ROOT, 6 + lane));
             s.root[lane] = x;
         }
         __syncthreads();
@@ -1470,6 +1528,7 @@ struct lgs_sim {
     float* rbs = nullptr;
     const float* torques = nullptr;
     lgs_task_params* task_dev = nullptr;
+    int16_t* hf_mem = nullptr;
     int has_task = 0;
     int rows = 32;
 };
@@ -1577,6 +1636,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     sp.max_depen = p->max_depenetration_velocity; sp.beta = p->baumgarte; sp.ground_friction = p->ground_friction;
     sp.armature = p->armature; sp.clamp_qd = p->clamp_joint_velocity; sp.max_contacts = p->max_contacts;
     sp.max_rows = p->max_rows;
+    sp.hf = nullptr; sp.hf_rows = sp.hf_cols = 0; sp.hf_inv_hs = sp.hf_vs = sp.hf_border = 0.f;
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
     HIP_TRY(hipMemset(s->added_mass, 0, sizeof(float) * num_envs));
@@ -1597,7 +1657,30 @@ LGS_API int lgs_destroy_sim(lgs_sim* s) {
     (void)hipFree(s->friction);
     (void)hipFree(s->added_mass);
     (void)hipFree(s->task_dev);
+    (void)hipFree(s->hf_mem);
     delete s;
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_heightfield(lgs_sim* s, const int16_t* heights, int32_t rows, int32_t cols,
+                                float horizontal_scale, float vertical_scale, float border_size) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    if (heights && rows > 0 && (rows < 2 || cols < 2 || !(horizontal_scale > 0.f) || !(vertical_scale > 0.f)))
+        return set_err(LGS_ERR_ARG, "lgs_set_heightfield: need rows, cols >= 2 and positive scales");
+    HIP_TRY(hipStreamSynchronize(s->stream));  // no step may still read the previous map
+    (void)hipFree(s->hf_mem);
+    s->hf_mem = nullptr;
+    s->sp.hf = nullptr;
+    s->sp.hf_rows = s->sp.hf_cols = 0;
+    if (!heights || rows <= 0) return LGS_OK;
+    const size_t bytes = sizeof(int16_t) * (size_t)rows * (size_t)cols;
+    HIP_TRY(hipMalloc(&s->hf_mem, bytes));
+    HIP_TRY(hipMemcpy(s->hf_mem, heights, bytes, hipMemcpyHostToDevice));
+    s->sp.hf = s->hf_mem;
+    s->sp.hf_rows = rows; s->sp.hf_cols = cols;
+    s->sp.hf_inv_hs = 1.0f / horizontal_scale;
+    s->sp.hf_vs = vertical_scale;
+    s->sp.hf_border = border_size;
     return LGS_OK;
 }
 

@@ -6,7 +6,7 @@ from legged_gym.envs.h1.h1_config import H1RoughCfg, H1RoughCfgPPO
 from legged_gym.envs.h1.h1_env import H1Robot
 from legged_gym.envs.h1_2.h1_2_config import H1_2RoughCfg, H1_2RoughCfgPPO
 from legged_gym.envs.h1_2.h1_2_env import H1_2Robot
-from legged_gym.envs.g1.g1_config import G1RoughCfg, G1RoughCfgPPO
+from legged_gym.envs.g1.g1_config import G1HeightfieldCfg, G1RoughCfg, G1RoughCfgPPO
 from legged_gym.envs.g1.g1_env import G1Robot
 from .base.legged_robot import LeggedRobot
 
@@ -16,3 +16,4 @@ task_registry.register("go2", LeggedRobot, GO2RoughCfg(), GO2RoughCfgPPO())
 task_registry.register("h1", H1Robot, H1RoughCfg(), H1RoughCfgPPO())
 task_registry.register("h1_2", H1_2Robot, H1_2RoughCfg(), H1_2RoughCfgPPO())
 task_registry.register("g1", G1Robot, G1RoughCfg(), G1RoughCfgPPO())
+task_registry.register("g1_rough", G1Robot, G1HeightfieldCfg(), G1RoughCfgPPO())

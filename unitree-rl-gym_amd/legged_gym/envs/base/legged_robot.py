@@ -29,6 +29,7 @@ from legged_gym.utils.helpers import class_to_dict
 from leggedsim import cabi, native
 from leggedsim.model import load_model
 from leggedsim.task import build_task_params
+from legged_gym.utils.terrain import Terrain
 
 from .env_spec import derive_env_spec
 from .legged_robot_config import LeggedRobotCfg
@@ -88,6 +89,10 @@ class LeggedRobot(BaseTask):
         self.penalised_contact_indices = torch.tensor(spec.penalised_contact_indices, dtype=torch.long, device=dev)
         self.termination_contact_indices = torch.tensor(spec.termination_contact_indices, dtype=torch.long, device=dev)
         self.base_init_state = torch.tensor(spec.base_init_state, device=dev)
+        # rough terrain (utils/terrain.py): the height map the contact kernel samples
+        self.terrain = None
+        if self.cfg.terrain.mesh_type in ("heightfield", "trimesh"):
+            self.terrain = Terrain(self.cfg.terrain, self.num_envs)
         self._get_env_origins()
         self.dof_pos_limits = torch.tensor(spec.dof_pos_limits, device=dev)
         self.dof_vel_limits = torch.tensor(spec.dof_vel_limits, device=dev)
@@ -114,12 +119,40 @@ class LeggedRobot(BaseTask):
         self.sim = native.Sim(model, sp, self.num_envs, self.sim_device_id)
         self.sim.set_env_properties(friction, added_mass)
         self.shape_friction = friction
+        if self.terrain is not None:
+            self._create_heightfield()
+        else:
+            self._create_ground_plane()
 
     def _create_ground_plane(self):
-        """The plane is the z = 0 half-space inside the contact kernel."""
+        """The plane is the z = 0 half-space inside the contact kernel (legged_robot.py:244-256)."""
+        self.sim.set_heightfield(None, 0.0, 0.0, 0.0)
+
+    def _create_heightfield(self):
+        """gym.add_heightfield of legged_gym's rough-terrain path: the int16 map of
+        utils/terrain.py, offset by -border_size in x and y."""
+        tc = self.cfg.terrain
+        self.sim.set_heightfield(self.terrain.heightsamples, tc.horizontal_scale, tc.vertical_scale, tc.border_size)
+        self.height_samples = torch.tensor(self.terrain.heightsamples).view(
+            self.terrain.tot_rows, self.terrain.tot_cols).to(self.device)
 
     def _get_env_origins(self):
-        """Grid of env origins (legged_robot.py:258-272)."""
+        """Env origins (legged_robot.py:258-272): the terrain tiles on rough terrain
+        (levels U{0..max_init_terrain_level}, types by env id, as legged_gym's
+        rough-terrain path), otherwise a grid."""
+        if self.terrain is not None:
+            tc = self.cfg.terrain
+            self.custom_origins = True
+            self.env_origins = torch.zeros(self.num_envs, 3, device=self.device, requires_grad=False)
+            max_init_level = tc.max_init_terrain_level if tc.curriculum else tc.num_rows - 1
+            max_init_level = min(max_init_level, tc.num_rows - 1)  # a level must be a terrain row
+            self.terrain_levels = torch.randint(0, max_init_level + 1, (self.num_envs,), device=self.device)
+            self.terrain_types = torch.div(torch.arange(self.num_envs, device=self.device),
+                                           (self.num_envs / tc.num_cols), rounding_mode="floor").to(torch.long)
+            self.max_terrain_level = tc.num_rows
+            self.terrain_origins = torch.from_numpy(self.terrain.env_origins).to(self.device).to(torch.float)
+            self.env_origins[:] = self.terrain_origins[self.terrain_levels, self.terrain_types]
+            return
         self.custom_origins = False
         self.env_origins = torch.zeros(self.num_envs, 3, device=self.device, requires_grad=False)
         num_cols = np.floor(np.sqrt(self.num_envs))

@@ -85,3 +85,13 @@ class G1RoughCfgPPO(LeggedRobotCfgPPO):
         max_iterations = 10000
         run_name = ""
         experiment_name = "g1"
+
+
+class G1HeightfieldCfg(G1RoughCfg):
+    """BASELINE configs[2]: G1 on the rough-terrain heightfield (utils/terrain.py's
+    curriculum map: 10 x 20 tiles of slopes, stairs and obstacles).  The reference
+    registers no such task (its create_sim only adds a plane); everything else is
+    G1RoughCfg."""
+
+    class terrain(G1RoughCfg.terrain):
+        mesh_type = "heightfield"

@@ -91,6 +91,7 @@ class TaskParams(C.Structure):
         ("swing_height_target", C.c_float),
         ("seed", C.c_uint64),
         ("write_body_states", C.c_int32),
+        ("custom_origins", C.c_int32),
     ]
 
 
@@ -197,4 +198,8 @@ def load_oracle():
                                      C.POINTER(EnvBuffers), C.c_int64]
     lib.orc_compute_torques.argtypes = [C.POINTER(TaskParams), C.c_int, C.c_int, vp, vp, vp, C.c_float, vp]
     lib.orc_body_states_env.argtypes = [C.POINTER(ModelDesc), vp, vp, vp]
+    lib.orc_set_heightfield.argtypes = [vp, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float]
+    lib.orc_set_heightfield.restype = None
+    lib.orc_terrain_sample.argtypes = [C.c_float, C.c_float, vp]
+    lib.orc_terrain_sample.restype = C.c_float
     return lib

@@ -63,10 +63,11 @@ def load():
     lib.lgs_step.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_reset_all.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
                  "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
-                 "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts"):
+                 "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield"):
         getattr(lib, name).restype = C.c_int
     _LIB = lib
     return lib
@@ -81,7 +82,7 @@ EXPORTED_SYMBOLS = [
     "lgs_last_error", "lgs_version", "lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize",
     "lgs_set_env_properties", "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
-    "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform",
+    "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
 ]
 
 
@@ -109,6 +110,19 @@ class Sim:
         check(self.lib, self.lib.lgs_set_env_properties(
             self.handle, None if f is None else f.ctypes.data, None if m is None else m.ctypes.data),
             "lgs_set_env_properties")
+
+    def set_heightfield(self, heights, horizontal_scale, vertical_scale, border_size):
+        """gym.add_heightfield: int16 [rows, cols] height samples (None: the z = 0 plane)."""
+        import numpy as np
+        if heights is None:
+            check(self.lib, self.lib.lgs_set_heightfield(self.handle, None, 0, 0, 0.0, 0.0, 0.0), "lgs_set_heightfield")
+            self._hf = None
+            return
+        hf = np.ascontiguousarray(heights, dtype=np.int16)
+        self._hf = hf
+        check(self.lib, self.lib.lgs_set_heightfield(self.handle, hf.ctypes.data, hf.shape[0], hf.shape[1],
+                                                     float(horizontal_scale), float(vertical_scale),
+                                                     float(border_size)), "lgs_set_heightfield")
 
     def bind(self, root, dofs, cforce, rbs):
         for t in (root, dofs, cforce, rbs):

@@ -102,4 +102,5 @@ def build_task_params(env) -> cabi.TaskParams:
     rank = int(os.environ.get("RANK", "0"))
     T.seed = (seed & 0xFFFFFFFF) | (rank << 32)
     T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)))
+    T.custom_origins = int(bool(getattr(env, "custom_origins", False)))
     return T
