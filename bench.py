@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--env_steps", type=int, default=200, help="timed control steps of the env-only leg")
     p.add_argument("--cpu_seconds", type=float, default=12.0, help="budget of the CPU oracle baseline")
     p.add_argument("--no_cpu_baseline", action="store_true")
+    p.add_argument("--no_other_configs", action="store_true",
+                   help="skip the env-only legs of BASELINE configs[2..4] (G1 heightfield, H1, H1_2)")
     return p.parse_args()
 
 
@@ -106,6 +108,38 @@ def cpu_baseline(env, seconds):
     return {"value": n_envs * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"Go2 {n_envs} envs x {steps} fused control steps (PD + 4 physics substeps + post-physics), "
                       f"oracle/lgs_oracle.c with OpenMP over envs, no policy; {el:.1f} s"}
+
+
+def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
+    """Back-to-back fused env steps of another BASELINE config (env only, no policy),
+    timed with HIP events on the env's stream: env-steps/s and ms per step."""
+    import torch
+    gargs = get_args(["--task", task, "--num_envs", str(n), "--headless", "--sim_device", dev, "--rl_device", dev])
+    with contextlib.redirect_stdout(sys.stderr):
+        env, _ = task_registry.make_env(name=task, args=gargs)
+    env.reset()
+    g = torch.Generator(device=dev).manual_seed(0)
+    acts = [0.5 * torch.randn(n, env.num_actions, device=dev, generator=g) for _ in range(4)]
+    for i in range(10):
+        env.step(acts[i % 4])
+    stream = torch.cuda.current_stream(dev)
+    env._sync_stream()
+    env.actions.copy_(acts[0])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record(stream)
+    for i in range(steps):
+        env._buf_idx ^= 1
+        env.sim.step(env._env_structs[env._buf_idx], env.common_step_counter)
+        env.account_replayed_steps(1)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    out = {"num_envs": n, "decimation": env.cfg.control.decimation, "env_step_kernel_ms": round(ms, 4),
+           "env_steps_per_s": round(n / (ms * 1e-3), 1),
+           "terrain": env.cfg.terrain.mesh_type}
+    env.close()
+    return out
 
 
 def main():
@@ -211,6 +245,14 @@ def main():
                      "kernel": "k_step<12,19,32> (fused Go2 control step)",
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
+    if world == 1 and not args.no_other_configs:
+        # the other BASELINE configs' env step on this GPU (their multi-GPU/LSTM PPO legs are
+        # not this line's metric): G1 rough heightfield 4096, H1 8192, H1_2 8192 (+DR)
+        line["other_configs_env_only"] = {
+            "g1_rough_heightfield_4096": env_kernel_rate("g1_rough", 4096, dev, 50, get_args, task_registry),
+            "h1_8192": env_kernel_rate("h1", 8192, dev, 50, get_args, task_registry),
+            "h1_2_8192": env_kernel_rate("h1_2", 8192, dev, 50, get_args, task_registry),
+        }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(env, args.cpu_seconds)
     print(json.dumps(line), flush=True)

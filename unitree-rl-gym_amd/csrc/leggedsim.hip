@@ -689,8 +689,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                 s.c_pt[slot][1] = c[1] - rad * nrm[1];
                 s.c_pt[slot][2] = c[2] - rad * nrm[2];
                 s.c_sep[slot] = sep;
-                float t1[3], t2[3];
-                contact_tangents(nrm, t1, t2);
+                float t1[3] = {1.f, 0.f, 0.f}, t2[3] = {0.f, 1.f, 0.f};  // plane: +x, +y
+                if (sp.hf) contact_tangents(nrm, t1, t2);
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
                     s.c_fr[slot][t] = nrm[t]; s.c_fr[slot][3 + t] = t1[t]; s.c_fr[slot][6 + t] = t2[t];
@@ -932,9 +932,13 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             if (c < nc) {
                 const float ln = rl(lam, 3 * c), l1 = rl(lam, 3 * c + 1), l2 = rl(lam, 3 * c + 2);
                 if (s.c_body[c] == lane) {
-                    const float* fr = s.c_fr[c];  // world force = ln n + l1 t1 + l2 t2
+                    if (sp.hf) {
+                        const float* fr = s.c_fr[c];  // world force = ln n + l1 t1 + l2 t2
 #pragma unroll
-                    for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) / dt;
+                        for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) / dt;
+                    } else {  // plane: the same numbers (n = z, t1 = x, t2 = y exactly)
+                        F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt;
+                    }
                 }
             }
         if (lane < B) { s.cf[lane][0] = F[0]; s.cf[lane][1] = F[1]; s.cf[lane][2] = F[2]; }
