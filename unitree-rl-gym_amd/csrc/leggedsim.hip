@@ -1119,206 +1119,232 @@ __device__ __forceinline__ void resample_commands(const lgs_task_params& T, floa
     cmd[0] *= keep; cmd[1] *= keep;
 }
 
-// ------------------------------------------------ post-physics (lane 0) ----
+// ------------------------------------------------ post-physics (scalar) ----
 // legged_robot.py:673-709 with _post_physics_step_callback, check_termination,
 // compute_reward; humanoid variants h1_env.py / g1_env.py.  Everything up to
-// the reset decision; returns reset flag in s.flags[0].
+// the reset decision; returns the reset flag in s.flags[0].  Called by all lanes:
+// lane 0 derives the base-frame state, commands and termination; then lane k
+// evaluates reward term k (all terms at once); lane 0 sums them in the reference's
+// (alphabetical) order, the same arithmetic as one lane summing term by term.
 template <int D, int B, int ROWS>
-__device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
-                                    const float* rbs, int N, int e, uint32_t step) {
+__device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
+                                             const float* rbs, int e, int id) {
     const int A = T.num_actions;
-    float* root = s.root;
-    float* cmd = E.commands + 4 * e;
+    const float* root = s.root;
+    const float* bl = s.u.post.misc;
+    const float* ba = s.u.post.misc + 3;
+    const float* pg = s.u.post.misc + 6;
+    const float* leg_phase = s.u.post.misc + 10;
+    const float* cmd = s.u.post.misc + 12;
     const float* act = s.act;
     const float* last_act = E.last_actions + A * e;
     const float* last_qd = E.last_dof_vel + D * e;
     float* air = E.feet_air_time + T.num_feet * e;
     uint8_t* lastc = E.last_contacts + T.num_feet * e;
-    int64_t* ep = E.episode_length + e;
     const float* tau = s.tau;
-
-    *ep += 1;
-    float bl[3], ba[3], pg[3], rpy[3];
-    const float g[3] = {0.f, 0.f, -1.f};
-    quat_rotate_inverse(root + 3, root + 7, bl);
-    quat_rotate_inverse(root + 3, root + 10, ba);
-    quat_rotate_inverse(root + 3, g, pg);
-    {
-        const float* q = root + 3;
-        float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
-        float sinr = 2.0f * (qw * qx + qy * qz);
-        float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
-        rpy[0] = atan2f(sinr, cosr);
-        float sinp = 2.0f * (qw * qy - qz * qx);
-        rpy[1] = fabsf(sinp) >= 1.f ? copysignf(3.14159265358979323846f / 2.0f, sinp) : asinf(sinp);
-        float siny = 2.0f * (qw * qz + qx * qy);
-        float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
-        rpy[2] = atan2f(siny, cosy);
-    }
-    float phase = 0.f, leg_phase[2] = {0.f, 0.f};
-    if (T.obs_layout == LGS_OBS_HUMANOID) {
-        float t = (float)(*ep) * T.control_dt;
-        phase = fmod_pos(t, T.phase_period) / T.phase_period;
-        leg_phase[0] = phase;
-        leg_phase[1] = fmod_pos(phase + T.phase_offset, 1.0f);
-    }
-    const uint64_t seed = T.seed;
-    if ((*ep) % T.resample_interval == 0) resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_CMD);
-    if (T.heading_command) {
-        const float* q = root + 3;
-        const float fx[3] = {1.f, 0.f, 0.f};
-        float t[3], u[3];
-        cross3(q, fx, t);
-        t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
-        cross3(q, t, u);
-        float fwd0 = fx[0] + q[3] * t[0] + u[0];
-        float fwd1 = fx[1] + q[3] * t[1] + u[1];
-        float heading = atan2f(fwd1, fwd0);
-        const float tp = 2.0f * 3.14159265358979323846f;
-        float wv = fmod_pos(cmd[3] - heading, tp);
-        if (wv > 3.14159265358979323846f) wv -= tp;
-        cmd[2] = clipf(0.5f * wv, -1.f, 1.f);
-    }
-    int reset = 0;
-    for (int i = 0; i < T.num_termination; ++i) {
-        const float* F = s.cf[T.termination_idx[i]];
-        if (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f) reset = 1;
-    }
-    if (fabsf(rpy[1]) > 1.0f || fabsf(rpy[0]) > 0.8f) reset = 1;
-    const int timeout = (float)(*ep) > T.max_episode_length;
-    reset |= timeout;
-    // rewards, active terms in alphabetical order
-    float rew = 0.f;
-    for (int k = 0; k < T.num_rewards; ++k) {
-        float sum = 0.f, r;
-        switch (T.reward_ids[k]) {
-        case LGS_REW_LIN_VEL_Z: r = bl[2] * bl[2]; break;
-        case LGS_REW_ANG_VEL_XY: r = ba[0] * ba[0] + ba[1] * ba[1]; break;
-        case LGS_REW_ORIENTATION: r = pg[0] * pg[0] + pg[1] * pg[1]; break;
-        case LGS_REW_BASE_HEIGHT: { float d = root[2] - T.base_height_target; r = d * d; } break;
-        case LGS_REW_TORQUES: for (int j = 0; j < A; ++j) sum += tau[j] * tau[j]; r = sum; break;
-        case LGS_REW_DOF_VEL: for (int j = 0; j < A; ++j) sum += s.qd[j] * s.qd[j]; r = sum; break;
-        case LGS_REW_DOF_ACC:
-            for (int j = 0; j < A; ++j) { float d = (last_qd[j] - s.qd[j]) / T.control_dt; sum += d * d; }
-            r = sum; break;
-        case LGS_REW_ACTION_RATE:
-            for (int j = 0; j < A; ++j) { float d = last_act[j] - act[j]; sum += d * d; }
-            r = sum; break;
-        case LGS_REW_COLLISION:
-            for (int i = 0; i < T.num_penalised; ++i) {
-                const float* F = s.cf[T.penalised_idx[i]];
-                sum += (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 0.1f) ? 1.f : 0.f;
-            }
-            r = sum; break;
-        case LGS_REW_DOF_POS_LIMITS:
-            for (int j = 0; j < A; ++j) {
-                float o = -fminf(s.q[j] - T.soft_dof_pos_lower[j], 0.f);
-                o += fmaxf(s.q[j] - T.soft_dof_pos_upper[j], 0.f);
-                sum += o;
-            }
-            r = sum; break;
-        case LGS_REW_DOF_VEL_LIMITS:
-            for (int j = 0; j < A; ++j) sum += clipf(fabsf(s.qd[j]) - T.dof_vel_limits[j] * T.soft_dof_vel_limit, 0.f, 1.f);
-            r = sum; break;
-        case LGS_REW_TORQUE_LIMITS:
-            for (int j = 0; j < A; ++j) sum += fmaxf(fabsf(tau[j]) - T.torque_limits[j] * T.soft_torque_limit, 0.f);
-            r = sum; break;
-        case LGS_REW_TRACKING_LIN_VEL: {
-            float e0 = cmd[0] - bl[0], e1 = cmd[1] - bl[1];
-            r = expf(-(e0 * e0 + e1 * e1) / T.tracking_sigma);
-        } break;
-        case LGS_REW_TRACKING_ANG_VEL: {
-            float d = cmd[2] - ba[2];
-            r = expf(-(d * d) / T.tracking_sigma);
-        } break;
-        case LGS_REW_FEET_AIR_TIME: {
-            int filt[LGS_MAX_FEET];
-            for (int f = 0; f < T.num_feet; ++f) {
-                int contact = s.cf[T.feet_idx[f]][2] > 1.f;
-                filt[f] = contact || lastc[f];
-                lastc[f] = (uint8_t)contact;
-                float first = (air[f] > 0.f && filt[f]) ? 1.f : 0.f;
-                air[f] += T.control_dt;
-                sum += (air[f] - 0.5f) * first;
-            }
-            float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
-            sum *= (cn > 0.1f) ? 1.f : 0.f;
-            for (int f = 0; f < T.num_feet; ++f)
-                if (filt[f]) air[f] = 0.f;
-            r = sum;
-        } break;
-        case LGS_REW_FEET_STUMBLE: {
-            r = 0.f;
-            for (int f = 0; f < T.num_feet; ++f) {
-                const float* F = s.cf[T.feet_idx[f]];
-                if (sqrtf(F[0] * F[0] + F[1] * F[1]) > 5.f * fabsf(F[2])) r = 1.f;
-            }
-        } break;
-        case LGS_REW_STAND_STILL: {
-            for (int j = 0; j < A; ++j) sum += fabsf(s.q[j] - T.default_dof_pos[j]);
-            float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
-            r = sum * ((cn < 0.1f) ? 1.f : 0.f);
-        } break;
-        case LGS_REW_FEET_CONTACT_FORCES:
-            for (int f = 0; f < T.num_feet; ++f) {
-                const float* F = s.cf[T.feet_idx[f]];
-                sum += fmaxf(sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) - T.max_contact_force, 0.f);
-            }
-            r = sum; break;
-        case LGS_REW_ALIVE: r = 1.0f; break;
-        case LGS_REW_CONTACT:
-            for (int f = 0; f < T.num_feet; ++f) {
-                int stance = leg_phase[f] < T.stance_threshold;
-                int contact = s.cf[T.feet_idx[f]][2] > 1.f;
-                sum += (contact == stance) ? 1.f : 0.f;
-            }
-            r = sum; break;
-        case LGS_REW_FEET_SWING_HEIGHT:
-            for (int f = 0; f < T.num_feet; ++f) {
-                const float* F = s.cf[T.feet_idx[f]];
-                int contact = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f;
-                float d = rbs[13 * T.feet_idx[f] + 2] - T.swing_height_target;
-                sum += d * d * (contact ? 0.f : 1.f);
-            }
-            r = sum; break;
-        case LGS_REW_CONTACT_NO_VEL:
-            for (int f = 0; f < T.num_feet; ++f) {
-                const float* F = s.cf[T.feet_idx[f]];
-                float c = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f ? 1.f : 0.f;
-                const float* vv = rbs + 13 * T.feet_idx[f] + 7;
-                for (int k2 = 0; k2 < 3; ++k2) { float xx = vv[k2] * c; sum += xx * xx; }
-            }
-            r = sum; break;
-        case LGS_REW_HIP_POS:
-            for (int i = 0; i < T.num_hip; ++i) sum += s.q[T.hip_dofs[i]] * s.q[T.hip_dofs[i]];
-            r = sum; break;
-        default: r = 0.f;
+    float sum = 0.f, r;
+    switch (id) {
+    case LGS_REW_LIN_VEL_Z: r = bl[2] * bl[2]; break;
+    case LGS_REW_ANG_VEL_XY: r = ba[0] * ba[0] + ba[1] * ba[1]; break;
+    case LGS_REW_ORIENTATION: r = pg[0] * pg[0] + pg[1] * pg[1]; break;
+    case LGS_REW_BASE_HEIGHT: { float d = root[2] - T.base_height_target; r = d * d; } break;
+    case LGS_REW_TORQUES: for (int j = 0; j < A; ++j) sum += tau[j] * tau[j]; r = sum; break;
+    case LGS_REW_DOF_VEL: for (int j = 0; j < A; ++j) sum += s.qd[j] * s.qd[j]; r = sum; break;
+    case LGS_REW_DOF_ACC:
+        for (int j = 0; j < A; ++j) { float d = (last_qd[j] - s.qd[j]) / T.control_dt; sum += d * d; }
+        r = sum; break;
+    case LGS_REW_ACTION_RATE:
+        for (int j = 0; j < A; ++j) { float d = last_act[j] - act[j]; sum += d * d; }
+        r = sum; break;
+    case LGS_REW_COLLISION:
+        for (int i = 0; i < T.num_penalised; ++i) {
+            const float* F = s.cf[T.penalised_idx[i]];
+            sum += (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 0.1f) ? 1.f : 0.f;
         }
-        r = r * T.reward_scales[k];
-        rew += r;
-        E.episode_sums[(size_t)k * N + e] += r;
-        if (E.rew_terms) E.rew_terms[(size_t)k * N + e] = r;
+        r = sum; break;
+    case LGS_REW_DOF_POS_LIMITS:
+        for (int j = 0; j < A; ++j) {
+            float o = -fminf(s.q[j] - T.soft_dof_pos_lower[j], 0.f);
+            o += fmaxf(s.q[j] - T.soft_dof_pos_upper[j], 0.f);
+            sum += o;
+        }
+        r = sum; break;
+    case LGS_REW_DOF_VEL_LIMITS:
+        for (int j = 0; j < A; ++j) sum += clipf(fabsf(s.qd[j]) - T.dof_vel_limits[j] * T.soft_dof_vel_limit, 0.f, 1.f);
+        r = sum; break;
+    case LGS_REW_TORQUE_LIMITS:
+        for (int j = 0; j < A; ++j) sum += fmaxf(fabsf(tau[j]) - T.torque_limits[j] * T.soft_torque_limit, 0.f);
+        r = sum; break;
+    case LGS_REW_TRACKING_LIN_VEL: {
+        float e0 = cmd[0] - bl[0], e1 = cmd[1] - bl[1];
+        r = expf(-(e0 * e0 + e1 * e1) / T.tracking_sigma);
+    } break;
+    case LGS_REW_TRACKING_ANG_VEL: {
+        float d = cmd[2] - ba[2];
+        r = expf(-(d * d) / T.tracking_sigma);
+    } break;
+    case LGS_REW_FEET_AIR_TIME: {
+        int filt[LGS_MAX_FEET];
+        for (int f = 0; f < T.num_feet; ++f) {
+            int contact = s.cf[T.feet_idx[f]][2] > 1.f;
+            filt[f] = contact || lastc[f];
+            lastc[f] = (uint8_t)contact;
+            float first = (air[f] > 0.f && filt[f]) ? 1.f : 0.f;
+            air[f] += T.control_dt;
+            sum += (air[f] - 0.5f) * first;
+        }
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+        sum *= (cn > 0.1f) ? 1.f : 0.f;
+        for (int f = 0; f < T.num_feet; ++f)
+            if (filt[f]) air[f] = 0.f;
+        r = sum;
+    } break;
+    case LGS_REW_FEET_STUMBLE: {
+        r = 0.f;
+        for (int f = 0; f < T.num_feet; ++f) {
+            const float* F = s.cf[T.feet_idx[f]];
+            if (sqrtf(F[0] * F[0] + F[1] * F[1]) > 5.f * fabsf(F[2])) r = 1.f;
+        }
+    } break;
+    case LGS_REW_STAND_STILL: {
+        for (int j = 0; j < A; ++j) sum += fabsf(s.q[j] - T.default_dof_pos[j]);
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+        r = sum * ((cn < 0.1f) ? 1.f : 0.f);
+    } break;
+    case LGS_REW_FEET_CONTACT_FORCES:
+        for (int f = 0; f < T.num_feet; ++f) {
+            const float* F = s.cf[T.feet_idx[f]];
+            sum += fmaxf(sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) - T.max_contact_force, 0.f);
+        }
+        r = sum; break;
+    case LGS_REW_ALIVE: r = 1.0f; break;
+    case LGS_REW_CONTACT:
+        for (int f = 0; f < T.num_feet; ++f) {
+            int stance = leg_phase[f] < T.stance_threshold;
+            int contact = s.cf[T.feet_idx[f]][2] > 1.f;
+            sum += (contact == stance) ? 1.f : 0.f;
+        }
+        r = sum; break;
+    case LGS_REW_FEET_SWING_HEIGHT:
+        for (int f = 0; f < T.num_feet; ++f) {
+            const float* F = s.cf[T.feet_idx[f]];
+            int contact = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f;
+            float d = rbs[13 * T.feet_idx[f] + 2] - T.swing_height_target;
+            sum += d * d * (contact ? 0.f : 1.f);
+        }
+        r = sum; break;
+    case LGS_REW_CONTACT_NO_VEL:
+        for (int f = 0; f < T.num_feet; ++f) {
+            const float* F = s.cf[T.feet_idx[f]];
+            float c = sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f ? 1.f : 0.f;
+            const float* vv = rbs + 13 * T.feet_idx[f] + 7;
+            for (int k2 = 0; k2 < 3; ++k2) { float xx = vv[k2] * c; sum += xx * xx; }
+        }
+        r = sum; break;
+    case LGS_REW_HIP_POS:
+        for (int i = 0; i < T.num_hip; ++i) sum += s.q[T.hip_dofs[i]] * s.q[T.hip_dofs[i]];
+        r = sum; break;
+    default: r = 0.f;
     }
-    if (T.only_positive_rewards) rew = fmaxf(rew, 0.f);
-    if (T.has_termination_reward) {
-        float r = ((reset && !timeout) ? 1.f : 0.f) * T.termination_scale;
-        rew += r;
-        E.episode_sums[(size_t)T.num_rewards * N + e] += r;
+    return r;
+}
+
+template <int D, int B, int ROWS>
+__device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
+                                    const float* rbs, int N, int e, uint32_t step) {
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+        float* root = s.root;
+        float* cmd = E.commands + 4 * e;
+        int64_t* ep = E.episode_length + e;
+        *ep += 1;
+        float bl[3], ba[3], pg[3], rpy[3];
+        const float g[3] = {0.f, 0.f, -1.f};
+        quat_rotate_inverse(root + 3, root + 7, bl);
+        quat_rotate_inverse(root + 3, root + 10, ba);
+        quat_rotate_inverse(root + 3, g, pg);
+        {
+            const float* q = root + 3;
+            float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+            float sinr = 2.0f * (qw * qx + qy * qz);
+            float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+            rpy[0] = atan2f(sinr, cosr);
+            float sinp = 2.0f * (qw * qy - qz * qx);
+            rpy[1] = fabsf(sinp) >= 1.f ? copysignf(3.14159265358979323846f / 2.0f, sinp) : asinf(sinp);
+            float siny = 2.0f * (qw * qz + qx * qy);
+            float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+            rpy[2] = atan2f(siny, cosy);
+        }
+        float phase = 0.f, leg_phase[2] = {0.f, 0.f};
+        if (T.obs_layout == LGS_OBS_HUMANOID) {
+            float t = (float)(*ep) * T.control_dt;
+            phase = fmod_pos(t, T.phase_period) / T.phase_period;
+            leg_phase[0] = phase;
+            leg_phase[1] = fmod_pos(phase + T.phase_offset, 1.0f);
+        }
+        const uint64_t seed = T.seed;
+        if ((*ep) % T.resample_interval == 0) resample_commands(T, cmd, seed, (uint32_t)e, step, LGS_STREAM_CMD);
+        if (T.heading_command) {
+            const float* q = root + 3;
+            const float fx[3] = {1.f, 0.f, 0.f};
+            float t[3], u[3];
+            cross3(q, fx, t);
+            t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
+            cross3(q, t, u);
+            float fwd0 = fx[0] + q[3] * t[0] + u[0];
+            float fwd1 = fx[1] + q[3] * t[1] + u[1];
+            float heading = atan2f(fwd1, fwd0);
+            const float tp = 2.0f * 3.14159265358979323846f;
+            float wv = fmod_pos(cmd[3] - heading, tp);
+            if (wv > 3.14159265358979323846f) wv -= tp;
+            cmd[2] = clipf(0.5f * wv, -1.f, 1.f);
+        }
+        int reset = 0;
+        for (int i = 0; i < T.num_termination; ++i) {
+            const float* F = s.cf[T.termination_idx[i]];
+            if (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f) reset = 1;
+        }
+        if (fabsf(rpy[1]) > 1.0f || fabsf(rpy[0]) > 0.8f) reset = 1;
+        const int timeout = (float)(*ep) > T.max_episode_length;
+        reset |= timeout;
+        for (int i = 0; i < 3; ++i) {
+            E.base_lin_vel[3 * e + i] = bl[i];
+            E.base_ang_vel[3 * e + i] = ba[i];
+            E.projected_gravity[3 * e + i] = pg[i];
+            E.rpy[3 * e + i] = rpy[i];
+            s.u.post.misc[i] = bl[i]; s.u.post.misc[3 + i] = ba[i]; s.u.post.misc[6 + i] = pg[i];
+        }
+        s.u.post.misc[9] = phase;
+        s.u.post.misc[10] = leg_phase[0]; s.u.post.misc[11] = leg_phase[1];
+        for (int i = 0; i < 4; ++i) s.u.post.misc[12 + i] = cmd[i];
+        if (E.phase) E.phase[e] = phase;
+        if (E.leg_phase) { E.leg_phase[2 * e] = leg_phase[0]; E.leg_phase[2 * e + 1] = leg_phase[1]; }
+        s.flags[0] = reset;
+        s.flags[1] = timeout;
     }
-    E.rew[e] = rew;
-    E.reset[e] = (uint8_t)reset;
-    E.time_out[e] = (uint8_t)timeout;
-    for (int i = 0; i < 3; ++i) {
-        E.base_lin_vel[3 * e + i] = bl[i];
-        E.base_ang_vel[3 * e + i] = ba[i];
-        E.projected_gravity[3 * e + i] = pg[i];
-        E.rpy[3 * e + i] = rpy[i];
-        s.u.post.misc[i] = bl[i]; s.u.post.misc[3 + i] = ba[i]; s.u.post.misc[6 + i] = pg[i];
+    __syncthreads();
+    // rewards: lane k evaluates active term k (alphabetical order, legged_robot.py:770-787)
+    if (lane < T.num_rewards) {
+        const float r = reward_term(s, T, E, rbs, e, T.reward_ids[lane]) * T.reward_scales[lane];
+        s.u.post.terms[lane] = r;
+        E.episode_sums[(size_t)lane * N + e] += r;
+        if (E.rew_terms) E.rew_terms[(size_t)lane * N + e] = r;
     }
-    s.u.post.misc[9] = phase;
-    if (E.phase) E.phase[e] = phase;
-    if (E.leg_phase) { E.leg_phase[2 * e] = leg_phase[0]; E.leg_phase[2 * e + 1] = leg_phase[1]; }
-    s.flags[0] = reset;
+    __syncthreads();
+    if (lane == 0) {
+        const int reset = s.flags[0], timeout = s.flags[1];
+        float rew = 0.f;
+        for (int k = 0; k < T.num_rewards; ++k) rew += s.u.post.terms[k];
+        if (T.only_positive_rewards) rew = fmaxf(rew, 0.f);
+        if (T.has_termination_reward) {
+            float r = ((reset && !timeout) ? 1.f : 0.f) * T.termination_scale;
+            rew += r;
+            E.episode_sums[(size_t)T.num_rewards * N + e] += r;
+        }
+        E.rew[e] = rew;
+        E.reset[e] = (uint8_t)reset;
+        E.time_out[e] = (uint8_t)timeout;
+    }
 }
 
 template <int D, int B, int ROWS>
@@ -1328,7 +1354,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     const int A = T.num_actions;
     const uint64_t seed = T.seed;
     if (!force_reset) {
-        if (lane == 0) post_physics_scalar(s, T, E, rbs, N, e, step);
+        post_physics_scalar(s, T, E, rbs, N, e, step);
     } else {
         if (lane == 0) s.flags[0] = 1;
     }

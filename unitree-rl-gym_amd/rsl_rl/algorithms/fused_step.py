@@ -74,6 +74,8 @@ class FusedPPOStep:
                 self._vview[id(p)] = self.exp_avg_sq[off:off + k].view_as(p)
                 off += k
         self.stats = self.grad[n:n + 4]
+        # the bf16 weight copies (wb) lag the fp32 weights after an optimizer step
+        self.weights_changed = True
         self.sync_optimizer_state(alg.optimizer)
         self._alloc()
 
@@ -245,6 +247,7 @@ class FusedPPOStep:
         mm._ok(lib.pmlp_adam(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg), mm._p(self.exp_avg_sq), self.n,
                              scale, mm._p(self.opt_partial), mm._p(self.step_t), mm._p(alg._lr), max_norm, float(b1),
                              float(b2), float(eps), st), "pmlp_adam")
+        self.weights_changed = True
 
 
 class FusedRollout:
@@ -281,8 +284,10 @@ class FusedRollout:
             return False
         return storage.num_envs == self.N
 
-    def forward(self, obs, cobs):
-        """(mu, value) of the actor and critic on N rows into static buffers."""
+    def forward(self, obs, cobs, t=None):
+        """(mu, value) of the actor and critic on N rows into static buffers.  The bf16
+        weight copies are refreshed at the first step of a rollout (t == 0; the update
+        changes the weights only between rollouts) or on any call outside one."""
         f, N = self.f, self.N
         if self.regs:  # one launch, activations in registers
             return mm.mlp4_forward([self.f.ac.actor, self.f.ac.critic], [obs, cobs], self.out)
@@ -290,9 +295,11 @@ class FusedRollout:
         jobs = [(obs, f.k0p[0], self.x[0], None)]
         if not shared:
             jobs.append((cobs, f.k0p[1], self.x[1], None))
-        for n in range(2):
-            for l, lin in enumerate(f.lins[n]):
-                jobs.append((lin.weight.detach(), f.wb[n][l].shape[1], f.wb[n][l], None))
+        if t is None or t == 0 or f.weights_changed:
+            for n in range(2):
+                for l, lin in enumerate(f.lins[n]):
+                    jobs.append((lin.weight.detach(), f.wb[n][l].shape[1], f.wb[n][l], None))
+            f.weights_changed = False
         mm._convert(jobs)
         xs = [self.x[0], self.x[0] if shared else self.x[1]]
         for l in range(f.L):
@@ -313,7 +320,7 @@ class FusedRollout:
 
     def act(self, obs, cobs, storage, t):
         f, N = self.f, self.N
-        self.forward(obs, cobs)
+        self.forward(obs, cobs, t)
         A = self.actions.shape[1]
         priv = storage.privileged_observations
         P = mm._p

@@ -286,6 +286,8 @@ class OnPolicyRunner:
     def load(self, path, load_optimizer=True):
         loaded = torch.load(path, map_location=self.device, weights_only=True)
         self.alg.actor_critic.load_state_dict(loaded["model_state_dict"])
+        if getattr(self.alg, "_fused", None) is not None:  # bf16 weight copies of the native rollout
+            self.alg._fused.weights_changed = True
         if load_optimizer:
             self.alg.optimizer.load_state_dict(loaded["optimizer_state_dict"])
         self.current_learning_iteration = loaded["iter"]
