@@ -342,12 +342,23 @@ __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
     const int m0 = (b % jobs.gm[jb]) * 64, k0 = (b / jobs.gm[jb]) * 64;
     __shared__ float tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int r = ty; r < 64; r += 4) {
-        const int m = m0 + r, k = k0 + tx;
-        float v = 0.f;
-        if (m < J.M && k < J.K) v = J.x[(size_t)(J.rows ? J.rows[m] : m) * J.ldx + k];
-        tile[r][tx] = v;
-        if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v;
+    // every load of the tile is issued before any store (a store could alias the next
+    // row's source as far as the compiler knows, which serialised 16 gather round trips)
+    int64_t src[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int m = m0 + ty + 4 * u;
+        src[u] = (m < J.M) ? (J.rows ? J.rows[m] : (int64_t)m) : -1;
+    }
+    float v[16];
+    const int k = k0 + tx;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = (src[u] >= 0 && k < J.K) ? J.x[(size_t)src[u] * J.ldx + k] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int r = ty + 4 * u, m = m0 + r;
+        tile[r][tx] = v[u];
+        if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v[u];
     }
     if (!J.yt) return;
     __syncthreads();
@@ -687,26 +698,25 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
     }
 }
 
-// stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term
-__global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_step_final(LossArgs a, const float* __restrict__ partial,
-                                                                           int nblocks, float* __restrict__ stats,
-                                                                           float* __restrict__ dstd) {
-    __shared__ float sh[4];
-    const int W = 3 + a.A;
-    const float inv = 1.f / (float)a.M;
-    for (int q = 0; q < W; ++q) {
-        float x = 0.f;
-        for (int b = threadIdx.x; b < nblocks; b += PMLP_LOSS_THREADS) x += partial[(size_t)b * W + q];
-        x = block_sum(x, sh);
-        if (threadIdx.x == 0) {
-            if (q < 3) stats[q] = x * inv;
-            else dstd[q - 3] = x - a.ecoef / a.stdv[q - 3];
-        }
-    }
+// stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term.
+// One wave per reduced quantity q (block q): the per-wave partials of k_ppo_loss_step summed
+// in a fixed order (deterministic), all quantities at once.
+__global__ __launch_bounds__(64) void k_ppo_loss_step_final(LossArgs a, const float* __restrict__ partial,
+                                                            int nblocks, float* __restrict__ stats,
+                                                            float* __restrict__ dstd) {
+    const int W = 3 + a.A, q = blockIdx.x;
+    float x = 0.f;
+    for (int b = threadIdx.x; b < nblocks; b += 64) x += partial[(size_t)b * W + q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     if (threadIdx.x == 0) {
-        float ent = 0.f;
-        for (int k = 0; k < a.A; ++k) ent += 0.5f + kHalfLog2Pi + logf(a.stdv[k]);
-        stats[3] = ent;
+        if (q < 3) stats[q] = x * (1.f / (float)a.M);
+        else dstd[q - 3] = x - a.ecoef / a.stdv[q - 3];
+        if (q == 0) {
+            float ent = 0.f;
+            for (int k = 0; k < a.A; ++k) ent += 0.5f + kHalfLog2Pi + logf(a.stdv[k]);
+            stats[3] = ent;
+        }
     }
 }
 
@@ -1360,8 +1370,8 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
     const int nb = (M + 63) / 64;
     hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
-    hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(1), dim3(PMLP_LOSS_THREADS), 0, (hipStream_t)stream, a, partial,
-                       nb, stats, dstd);
+    hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(3 + A), dim3(64), 0, (hipStream_t)stream, a, partial, nb, stats,
+                       dstd);
     PMLP_CHECK_LAUNCH("pmlp_ppo_loss_step");
     return 0;
 }
