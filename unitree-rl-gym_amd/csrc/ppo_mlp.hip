@@ -698,6 +698,111 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
     }
 }
 
+// The same step with the row's A <= AM action entries held in registers (loaded once,
+// gathered rows read as one contiguous record) and the per-action constants of sigma
+// (1/(2s^2), 1/s^2, 1/s^3, 1/s, log s) computed once per block: the generic kernel above
+// re-reads actions/mu in each of its three loops and takes 12 logf(sigma) per row.
+template <int AM>
+__global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOut o) {
+    __shared__ float c_h[AM], c_i2[AM], c_i3[AM], c_i1[AM], c_lg[AM], c_sg[AM];
+    const int A = a.A, W = 3 + A;
+    if (threadIdx.x < A) {
+        const float sg = a.stdv[threadIdx.x];
+        c_sg[threadIdx.x] = sg;
+        c_h[threadIdx.x] = 1.f / (2.f * sg * sg);
+        c_i2[threadIdx.x] = 1.f / (sg * sg);
+        c_i3[threadIdx.x] = 1.f / (sg * sg * sg);
+        c_i1[threadIdx.x] = 1.f / sg;
+        c_lg[threadIdx.x] = logf(sg);
+    }
+    __syncthreads();
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    const bool valid = i < a.M;
+    const size_t si = valid ? a.src(i) : 0;
+    float d[AM];
+    float surr = 0.f, vl = 0.f, kl = 0.f, dlogp = 0.f;
+    if (valid) {
+        float logp = 0.f;
+#pragma unroll
+        for (int k = 0; k < AM; ++k) {
+            if (k < A) {
+                const float mu = a.mu[(size_t)i * A + k];
+                d[k] = a.actions[si * A + k] - mu;
+                logp += -(d[k] * d[k]) * c_h[k] - c_lg[k] - kHalfLog2Pi;
+                const float os = a.old_sigma[si * A + k], om = a.old_mu[si * A + k] - mu;
+                kl += logf(c_sg[k] / os + 1.0e-5f) + (os * os + om * om) * c_h[k] - 0.5f;
+            } else {
+                d[k] = 0.f;
+            }
+        }
+        const float ratio = expf(logp - a.old_logp[si]);
+        const float adv = a.adv[si];
+        const float lo = 1.f - a.clip, hi = 1.f + a.clip;
+        const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, lo), hi);
+        surr = fmaxf(s1, s2);
+        float w1, w2;
+        max_weights(s1, s2, w1, w2);
+        const float dclamp = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        dlogp = (1.f / (float)a.M) * (-adv) * (w1 + w2 * dclamp) * ratio;
+        for (int k = 0; k < o.Ap; k += 8) {  // 16-byte chunks of the padded dmu row
+            bf16x8 g;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float gv = 0.f;
+#pragma unroll
+                for (int kk = 0; kk < AM; ++kk)
+                    if (kk == k + u && kk < A) gv = dlogp * d[kk] * c_i2[kk];
+                g[u] = (bf16)gv;
+                o.dmu_t[(size_t)(k + u) * a.M + i] = (bf16)gv;
+            }
+            *(bf16x8*)(o.dmu_b + (size_t)i * o.Ap + k) = g;
+        }
+        const float v = a.value[i], r = a.ret[si];
+        float dv;
+        const float gvc = a.vcoef / (float)a.M;
+        if (a.clipped_value) {
+            const float t = a.target[si];
+            const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
+            vl = fmaxf((v - r) * (v - r), (vc - r) * (vc - r));
+            float u1, u2;
+            max_weights((v - r) * (v - r), (vc - r) * (vc - r), u1, u2);
+            const float dcv = (v - t >= -a.clip && v - t <= a.clip) ? 1.f : 0.f;
+            dv = gvc * (u1 * 2.f * (v - r) + u2 * 2.f * (vc - r) * dcv);
+        } else {
+            vl = (r - v) * (r - v);
+            dv = gvc * 2.f * (v - r);
+        }
+        for (int k = 0; k < o.Vp; ++k) {
+            o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
+            o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < AM; ++k) d[k] = 0.f;
+    }
+    auto wsum = [](float x) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        return x;
+    };
+    surr = wsum(surr);
+    vl = wsum(vl);
+    kl = wsum(kl);
+    if (threadIdx.x == 0) {
+        o.partial[(size_t)blockIdx.x * W + 0] = surr;
+        o.partial[(size_t)blockIdx.x * W + 1] = vl;
+        o.partial[(size_t)blockIdx.x * W + 2] = kl;
+    }
+#pragma unroll
+    for (int k = 0; k < AM; ++k) {
+        if (k < A) {
+            float c = valid ? dlogp * (d[k] * d[k] * c_i3[k] - c_i1[k]) : 0.f;
+            c = wsum(c);
+            if (threadIdx.x == 0) o.partial[(size_t)blockIdx.x * W + 3 + k] = c;
+        }
+    }
+}
+
 // stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term.
 // One wave per reduced quantity q (block q): the per-wave partials of k_ppo_loss_step summed
 // in a fixed order (deterministic), all quantities at once.
@@ -1369,7 +1474,10 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
     const int nb = (M + 63) / 64;
-    hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
+    if (A <= 16 && Ap % 8 == 0)
+        hipLaunchKernelGGL(k_ppo_loss_step_reg<16>, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
+    else
+        hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
     hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(3 + A), dim3(64), 0, (hipStream_t)stream, a, partial, nb, stats,
                        dstd);
     PMLP_CHECK_LAUNCH("pmlp_ppo_loss_step");
