@@ -24,6 +24,8 @@ state_dict keep their reference structure: the Parameters are the same objects
 of the flat moments.  With torch.distributed the gradient (and the statistics
 tail) is all-reduced as one bucket and averaged inside the kernels.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -74,6 +76,10 @@ class FusedPPOStep:
                 self._vview[id(p)] = self.exp_avg_sq[off:off + k].view_as(p)
                 off += k
         self.stats = self.grad[n:n + 4]
+        self._side = None  # side stream of the weight-gradient GEMMs (run())
+        # dW_l beside dX_l on a second stream: measured SLOWER (one update 6.44 -> 6.77 ms,
+        # tools/probes/update_graph_ab.py), the two latency-bound GEMMs contend; off by default
+        self.dw_side_stream = os.environ.get("PMLP_DW_SIDE_STREAM", "0") == "1"
         # the bf16 weight copies (wb) lag the fp32 weights after an optimizer step
         self.weights_changed = True
         self.sync_optimizer_state(alg.optimizer)
@@ -198,9 +204,16 @@ class FusedPPOStep:
                                       P(self._gview[id(ac.std)]), P(self.dz_out[0]), P(self.dzt_out[0]),
                                       self.dz_out[0].shape[1], P(self.dz_out[1]), P(self.dzt_out[1]),
                                       self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
-        # 4. backward through both MLPs; the weight-gradient slabs carry the bias column
+        # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
+        #    dW_l (split-K slabs) and dX_l both read only dz_l; with dw_side_stream dW_l runs
+        #    on a second stream (a fork/join inside the captured graph) that rejoins before
+        #    the slab combine.
         dz, dzt = list(self.dz_out), list(self.dzt_out)
         red, copies = [], []
+        main = torch.cuda.current_stream(self.dev)
+        if self._side is None and self.dw_side_stream:
+            self._side = torch.cuda.Stream(self.dev)
+        side = self._side if self.dw_side_stream else main
         for l in range(L - 1, -1, -1):
             gj = []
             for n in range(2):
@@ -214,7 +227,9 @@ class FusedPPOStep:
                             kp + 8, kp))
                 if self.dw_stage[l][n] is not None:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
-            mm._gemm(mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
+            side.wait_stream(main)  # dz_l is ready
+            with torch.cuda.stream(side):
+                mm._gemm(mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
             if l > 0:
                 gj = []
                 for n in range(2):
@@ -226,6 +241,7 @@ class FusedPPOStep:
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
                 dzt = [self.dzt[n][l] for n in range(2)]
+        main.wait_stream(side)  # every slab written
         mm._reduce(red)
         for dst, srcv in copies:
             dst.copy_(srcv)
