@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ppo_mlp.h"
@@ -1271,7 +1272,21 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
     else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, st);
     else if (epi != PMLP_EPI_PARTIAL && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
         launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, st);  // small grids: 4x the blocks hide the k-loop latency
-    else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, st);
+    else {
+        // 128x128 output tiles: 8 waves of 64x32 (accumulators in 32 VGPRs, no AGPRs:
+        // 4 waves/SIMD resident instead of 3) for the epilogue-heavy short-K GEMMs; 4 waves
+        // of 64x64 for the forward GEMMs with a long k-loop (K >= 256), where the 64x64
+        // wave tile's operand reuse wins (tools/gpu_tile_ab.sh: -18 us per optimizer step).
+        // PMLP_BIG_TILE=0/1/2 forces 4 waves / 8 waves 64x32 / 8 waves 32x64.
+        static const int big = [] {
+            const char* v = getenv("PMLP_BIG_TILE");
+            return v ? atoi(v) : -1;
+        }();
+        const int pick = big >= 0 ? big : ((epi == PMLP_EPI_FWD_HIDDEN && maxk >= 256) ? 0 : 1);
+        if (pick == 1) launch<128, 128, 2, 4>(epi, gb, njobs, maxm, maxn, st);
+        else if (pick == 2) launch<128, 128, 4, 2>(epi, gb, njobs, maxm, maxn, st);
+        else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, st);
+    }
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
 }
