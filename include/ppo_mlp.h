@@ -40,13 +40,17 @@ enum {
     PMLP_EPI_FWD_HIDDEN = 0, /* y = ELU(acc + bias[n]) -> bf16 y[M,N] and y^T[N,M]           */
     PMLP_EPI_FWD_OUT = 1,    /* out = acc + bias[n]    -> fp32 out[M,N]                      */
     PMLP_EPI_BWD_DX = 2,     /* dz = acc * ELU'(yprev) -> bf16 dz[M,N] and dz^T[N,M]          */
-    PMLP_EPI_PARTIAL = 3     /* split-K slab s: fp32 slab[s][M,N] over k in [s*ks, (s+1)*ks)  */
+    PMLP_EPI_PARTIAL = 3,    /* split-K slab s: fp32 slab[s][M,N] over k in [s*ks, (s+1)*ks)  */
+    PMLP_EPI_PARTIAL_TN = 4  /* PARTIAL with A[K,M] (lda) and B[K,N] (ldb), m / n contiguous:
+                                the weight gradient dz^T y read from the row-major activations */
 };
 
 PMLP_API const char* pmlp_last_error(void);
 
 /* fp32 x[M,K] (ld ldx) -> bf16 y[M,Kp] (ld Kp; columns K..Kp-1 zero) and/or
  * y^T[Kp,ldyt] (rows K..Kp-1 and columns M..ldyt-1 zero); y or yt may be NULL.
+ * one_col > 0: column one_col of y (< Kp) is 1.0 instead (the ones column that
+ * makes a weight-gradient GEMM's extra output column the bias gradient).
  * rows (optional, int64[M]): output row m is input row rows[m] (the PPO
  * mini-batch gather of RolloutStorage.mini_batch_generator fused in).
  * Used for observations, output gradients and weights (W and W^T).          */
@@ -55,7 +59,7 @@ typedef struct {
     pmlp_bf16* y;
     pmlp_bf16* yt;
     const int64_t* rows;
-    int32_t M, K, ldx, Kp, ldyt;
+    int32_t M, K, ldx, Kp, ldyt, one_col;
 } pmlp_convert_job;
 PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream);
 
@@ -65,7 +69,8 @@ PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* str
  *   BWD_DX:     yprev[M,N] bf16 (ldyp) = the ELU output the gradient flows through;
  *               cb/ct as FWD_HIDDEN
  *   PARTIAL:    cf = slab base, slab s at cf + s*M*ldcf; ksplit = k per slab
- *               (multiple of 32); every job must give the same ceil(K/ksplit) */
+ *               (multiple of 32); every job must give the same ceil(K/ksplit)
+ *   PARTIAL_TN: as PARTIAL with A[K,M], B[K,N] (lda >= ceil8(M), ldb >= ceil8(N)) */
 typedef struct {
     const pmlp_bf16* A;
     const pmlp_bf16* B;
@@ -188,7 +193,7 @@ PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t
 /* The same loss for the fused optimizer step (gradient of the loss itself):
  * one pass writes the output gradients straight into the MLP backward's bf16
  * operands, dmu[M,Ap] + dmu_t[Ap,M] and dvalue[M,Vp] + dvalue_t[Vp,M]
- * (padding columns/rows written as zero), dstd[A] (incl. the entropy term) and
+ * (padding columns/rows written as zero; dmu_t / dvalue_t may be NULL), dstd[A] (incl. the entropy term) and
  * stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean}.
  * partial: pmlp_ppo_loss_step_parts(M, A) floats of scratch.                */
 PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A);

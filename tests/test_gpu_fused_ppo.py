@@ -246,3 +246,60 @@ def test_register_chained_mlp_forward_matches_fp32_torch(rows, hidden):
             assert torch.isfinite(out).all()
             err = (out - ref).abs().max() / ref.abs().max()
             assert err <= 2e-2, float(err)
+
+
+@pytest.mark.parametrize("K,ks", [(24576, 1152), (1000, 320)])
+def test_partial_tn_gemm_matches_transposed_partial_and_fp32(K, ks):
+    """Weight-gradient GEMM read from the row-major activations (PARTIAL_TN, LDS-transposed
+    MFMA operands) == the k-contiguous PARTIAL on transposed copies, bitwise (same k order
+    into the same MFMAs), and == fp32 dz^T y within fp32 summation order."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for M, N in ((512, 56), (256, 520), (128, 264), (12, 136), (1, 136), (64, 64)):
+        mp, np_ = (M + 7) // 8 * 8, (N + 7) // 8 * 8
+        a = torch.randn(K, mp, device="cuda", generator=g).to(torch.bfloat16)
+        b = torch.randn(K, np_, device="cuda", generator=g).to(torch.bfloat16)
+        nsl = (K + ks - 1) // ks
+        s_tn = torch.full((nsl, M, N), float("nan"), device="cuda")
+        s_nt = torch.full((nsl, M, N), float("nan"), device="cuda")
+        at, bt = a.t().contiguous(), b.t().contiguous()
+        kp = (K + 7) // 8 * 8
+        if kp != K:  # the NT path needs k padded to 8 (zeros)
+            at = torch.nn.functional.pad(at, (0, kp - K))
+            bt = torch.nn.functional.pad(bt, (0, kp - K))
+        mfma_mlp._gemm(mfma_mlp.EPI_PARTIAL_TN, [dict(A=a, B=b, M=M, N=N, K=K, cf=s_tn)], ksplit=ks)
+        mfma_mlp._gemm(mfma_mlp.EPI_PARTIAL, [dict(A=at, B=bt, M=M, N=N, K=kp, cf=s_nt)], ksplit=ks)
+        torch.cuda.synchronize()
+        assert torch.isfinite(s_tn).all(), (M, N)
+        assert torch.equal(s_tn, s_nt), (M, N, float((s_tn - s_nt).abs().max()))
+        ref = a[:, :M].float().t() @ b[:, :N].float()
+        err = float((s_tn.sum(0) - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, (M, N, err)
+
+
+def test_fused_update_tn_is_bitwise_transposed_copies(monkeypatch):
+    """The whole fused update with row-major-only activations (PMLP_TN=1, the default)
+    equals the transposed-copy dataflow (PMLP_TN=0) bitwise: losses and parameters."""
+    torch.manual_seed(0)
+    N, T, O, A = 2048, 8, 48, 12
+    ac = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda()
+    algs = []
+    for tn in ("1", "0"):
+        monkeypatch.setenv("PMLP_TN", tn)
+        alg = PPO(copy.deepcopy(ac), num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3,
+                  schedule="adaptive", device="cuda")
+        alg.use_graph = False
+        alg.init_storage(N, T, [O], [None], [A])
+        assert alg._fused.tn == (tn == "1")
+        algs.append(alg)
+    for u in range(2):
+        data = _fill_storage(algs[1], T, N, O, A, seed=20 + u)
+        for k, v in data.items():
+            getattr(algs[0].storage, k).copy_(v)
+        algs[0].storage.step = T
+        torch.manual_seed(200 + u)
+        l0 = algs[0].update()
+        torch.manual_seed(200 + u)
+        l1 = algs[1].update()
+        assert l0 == l1
+        for a, b in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
+            assert torch.equal(a, b)

@@ -1,6 +1,10 @@
-"""A/B of one PPO update (20 fused optimizer steps replayed as a HIP graph) with the
-weight-gradient GEMMs on a side stream (overlapping the input-gradient GEMMs) or
-serial, interleaved in one process (Go2 MLPs, 4096 envs x 24 steps)."""
+"""A/B of one PPO update (20 fused optimizer steps replayed as a HIP graph) under two
+values of an environment switch read when the fused step is built, interleaved in one
+process (Go2 MLPs, 4096 envs x 24 steps).
+
+    python tools/probes/update_env_ab.py PMLP_TN 1 0
+    python tools/probes/update_env_ab.py PMLP_DW_SIDE_STREAM 0 1
+"""
 import os
 import sys
 
@@ -14,8 +18,11 @@ from rsl_rl.modules import ActorCritic  # noqa: E402
 N, T, O, A = 4096, 24, 48, 12
 
 
-def make(side):
-    os.environ["PMLP_DW_SIDE_STREAM"] = "1" if side else "0"
+VAR, VALS = sys.argv[1], sys.argv[2:]
+
+
+def make(val):
+    os.environ[VAR] = val
     torch.manual_seed(0)
     ac = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda()
     alg = PPO(ac, num_learning_epochs=5, num_mini_batches=4, device="cuda")
@@ -33,7 +40,7 @@ def make(side):
     return alg
 
 
-algs = {"serial": make(False), "side": make(True)}
+algs = {f"{VAR}={v}": make(v) for v in VALS}
 res = {k: [] for k in algs}
 for rnd in range(5):
     for k, alg in algs.items():
@@ -48,4 +55,4 @@ for rnd in range(5):
         res[k].append(e0.elapsed_time(e1) / 5)
 for k, v in res.items():
     v = sorted(v)
-    print(f"{k:7s} update ms: median {v[len(v) // 2]:.3f}  min {v[0]:.3f}  all {[round(x, 3) for x in v]}")
+    print(f"{k:24s} update ms: median {v[len(v) // 2]:.3f}  min {v[0]:.3f}  all {[round(x, 3) for x in v]}")

@@ -30,6 +30,9 @@
 typedef __bf16 bf16;
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 static thread_local std::string g_err;
@@ -67,13 +70,28 @@ struct GemmBatch {
     int slabs;  // PARTIAL: slabs per job (grid.z = njobs * slabs)
 };
 
+// ds_read_b64_tr_b16 (guide T10): per 16-lane group, lane 4q+p addresses row q,
+// columns 4p..4p+3 of a 4 x 16 block; lane i receives column i, rows 0..3
+__device__ __forceinline__ shortx4 lds_read_tr(const bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)p);
+}
+
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     const int job = blockIdx.z / gb.slabs, slice = blockIdx.z % gb.slabs;
     const GemmArgs& g = gb.j[job];
     if ((int)blockIdx.x * BM >= g.M || (int)blockIdx.y * BN >= g.N) return;  // grid covers the largest job
+    // PARTIAL_TN: A[K,M] and B[K,N] (m / n contiguous: the row-major activations and
+    // gradients), staged k-major in LDS and fed to the MFMAs by transposed reads
+    constexpr bool TNL = EPI == PMLP_EPI_PARTIAL_TN;
+    constexpr bool PART = EPI == PMLP_EPI_PARTIAL || TNL;
+    static_assert(!TNL || PMLP_NBUF == 1, "PARTIAL_TN stages one k-tile");
     constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
     constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
+    // TN images [BK][BM + 32]: a row stride of 16 (mod 64) dwords puts the four rows of
+    // one transposed read on disjoint banks (conflict-free for BM, BN multiples of 64)
+    constexpr int SA = TNL ? BM + 32 : LS, SB = TNL ? BN + 32 : LS;
+    constexpr int ATILE = TNL ? BK * SA : BM * LS, BTILE = TNL ? BK * SB : BN * LS;
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 32, FN = TN / 32;
@@ -82,17 +100,18 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
     constexpr int CS = BN + 8;  // row-major epilogue tile [BM][CS] (bf16)
     constexpr int TS = BM + 8;  // transposed epilogue tile [BN][TS]: 16-B aligned rows, 2-way b64 writes
-    constexpr int STAGE = (BM + BN) * LS * PMLP_NBUF, CTILE = BM * CS, TTILE = BN * TS;
-    constexpr int SMEM = STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE);
+    constexpr int STAGE = (ATILE + BTILE) * PMLP_NBUF, CTILE = BM * CS, TTILE = BN * TS;
+    constexpr int SMEM = PART ? STAGE
+                              : (STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE));
     __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
     bf16* As = smem;
-    bf16* Bs = smem + BM * LS;
+    bf16* Bs = smem + ATILE;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     int kb = 0, ke = g.K;
-    if (EPI == PMLP_EPI_PARTIAL) {
+    if (PART) {
         kb = slice * g.ksplit;
         ke = min(g.K, kb + g.ksplit);
     }
@@ -106,6 +125,27 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 
     uint4 ra[AL], rb[BL];
     auto gload = [&](int k0) {
+        if constexpr (TNL) {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int c = tid + i * NT;
+                const int r = c / (BM / 8), mc = (c % (BM / 8)) * 8;  // k row, m chunk
+                const int gk = k0 + r, gm = m0 + mc;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (c < ACH && gk < ke && gm < g.M) v = *(const uint4*)(g.A + (size_t)gk * g.lda + gm);
+                ra[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < BL; ++i) {
+                const int c = tid + i * NT;
+                const int r = c / (BN / 8), nc = (c % (BN / 8)) * 8;
+                const int gk = k0 + r, gn = n0 + nc;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (c < BCH && gk < ke && gn < g.N) v = *(const uint4*)(g.B + (size_t)gk * g.ldb + gn);
+                rb[i] = v;
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
             const int c = tid + i * NT;
@@ -126,6 +166,19 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         }
     };
     auto lstore = [&]() {
+        if constexpr (TNL) {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int c = tid + i * NT;
+                if (c < ACH) *(uint4*)(As + (c / (BM / 8)) * SA + (c % (BM / 8)) * 8) = ra[i];
+            }
+#pragma unroll
+            for (int i = 0; i < BL; ++i) {
+                const int c = tid + i * NT;
+                if (c < BCH) *(uint4*)(Bs + (c / (BN / 8)) * SB + (c % (BN / 8)) * 8) = rb[i];
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
             const int c = tid + i * NT;
@@ -138,7 +191,35 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         }
     };
 
+    // TN operand fragments: lane l (row/col 16*((l>>4)&1) + (l&15) of its 32-block,
+    // k = 8(l>>5)..+7) = two transposed reads of k rows 8(l>>5) + {0..3, 4..7}
+    const int tr_off = 8 * (lane >> 5) + ((lane >> 2) & 3);  // k row within a 16-step
+    const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
     auto compute = [&]() {
+        if constexpr (TNL) {
+#pragma unroll
+            for (int s = 0; s < BK / 16; ++s) {
+                bf16x8 af[FM], bfr[FN];
+#pragma unroll
+                for (int i = 0; i < FM; ++i) {
+                    const bf16* p = As + (s * 16 + tr_off) * SA + wm * TM + i * 32 + tr_col;
+                    const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SA);
+                    af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const bf16* p = Bs + (s * 16 + tr_off) * SB + wn * TN + j * 32 + tr_col;
+                    const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SB);
+                    bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             bf16x8 af[FM], bfr[FN];
@@ -222,8 +303,8 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         for (int j = 0; j < FN; ++j) {
             const int col = n0 + wn * TN + j * 32 + (lane & 31);
             const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
-            if (col >= g.N && (EPI == PMLP_EPI_PARTIAL || EPI == PMLP_EPI_FWD_OUT)) continue;
-            if (EPI == PMLP_EPI_PARTIAL) {
+            if (col >= g.N && (PART || EPI == PMLP_EPI_FWD_OUT)) continue;
+            if (PART) {
                 float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
@@ -327,7 +408,7 @@ struct CvtJob {
     bf16* y;
     bf16* yt;
     const int64_t* rows;  // optional gather: row m of the output is row rows[m] of x
-    int M, K, ldx, Kp, ldyt;
+    int M, K, ldx, Kp, ldyt, one_col;
 };
 struct CvtJobs {
     CvtJob j[PMLP_MAX_JOBS];
@@ -359,7 +440,7 @@ __global__ __launch_bounds__(256) void k_convert_jobs(CvtJobs jobs) {
     for (int u = 0; u < 16; ++u) {
         const int r = ty + 4 * u, m = m0 + r;
         tile[r][tx] = v[u];
-        if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)v[u];
+        if (J.y && m < J.M && k < J.Kp) J.y[(size_t)m * J.Kp + k] = (bf16)(k == J.one_col ? 1.f : v[u]);
     }
     if (!J.yt) return;
     __syncthreads();
@@ -653,7 +734,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
                 g = dlogp * d / (sg * sg);
             }
             o.dmu_b[(size_t)i * o.Ap + k] = (bf16)g;
-            o.dmu_t[(size_t)k * a.M + i] = (bf16)g;
+            if (o.dmu_t) o.dmu_t[(size_t)k * a.M + i] = (bf16)g;
         }
         const float v = a.value[i], r = a.ret[si];
         float dv;
@@ -671,7 +752,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
         }
         for (int k = 0; k < o.Vp; ++k) {
             o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
-            o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+            if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
         }
     }
     auto wsum = [](float x) {
@@ -754,7 +835,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
                 for (int kk = 0; kk < AM; ++kk)
                     if (kk == k + u && kk < A) gv = dlogp * d[kk] * c_i2[kk];
                 g[u] = (bf16)gv;
-                o.dmu_t[(size_t)(k + u) * a.M + i] = (bf16)gv;
+                if (o.dmu_t) o.dmu_t[(size_t)(k + u) * a.M + i] = (bf16)gv;
             }
             *(bf16x8*)(o.dmu_b + (size_t)i * o.Ap + k) = g;
         }
@@ -775,7 +856,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
         }
         for (int k = 0; k < o.Vp; ++k) {
             o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
-            o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+            if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
         }
     } else {
 #pragma unroll
@@ -1203,7 +1284,8 @@ static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, 
     case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, gb); break;
     case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, gb); break;
     case PMLP_EPI_BWD_DX: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, gb); break;
-    default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, gb); break;
+    case PMLP_EPI_PARTIAL: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, gb); break;
+    default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4>), grid, block, 0, st, gb); break;
     }
 }
 
@@ -1220,9 +1302,11 @@ PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* str
     int nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_convert_job& J = jobs[i];
-        if (!J.x || J.M <= 0 || J.K <= 0 || J.Kp < J.K || J.ldx < J.K || (!J.y && !J.yt) || (J.yt && J.ldyt < J.M))
+        if (!J.x || J.M <= 0 || J.K <= 0 || J.Kp < J.K || J.ldx < J.K || (!J.y && !J.yt) || (J.yt && J.ldyt < J.M) ||
+            J.one_col < 0 || J.one_col >= J.Kp || (J.one_col > 0 && (J.one_col < J.K || J.yt)))
             return fail(-1, "pmlp_convert: bad job " + std::to_string(i));
-        cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.rows, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0};
+        cj.j[i] = CvtJob{J.x, (bf16*)J.y, (bf16*)J.yt, J.rows, J.M, J.K, J.ldx, J.Kp, J.yt ? J.ldyt : 0,
+                         J.one_col > 0 ? J.one_col : -1};
         const int mext = std::max(J.M, J.yt ? J.ldyt : 0);
         cj.gm[i] = (mext + 63) / 64;
         cj.start[i] = nb;
@@ -1235,7 +1319,8 @@ PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* str
 }
 
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream) {
-    if (epi < 0 || epi > 3) return fail(-1, "pmlp_gemm: unknown epilogue");
+    if (epi < 0 || epi > 4) return fail(-1, "pmlp_gemm: unknown epilogue");
+    const bool part = epi == PMLP_EPI_PARTIAL || epi == PMLP_EPI_PARTIAL_TN;
     if (njobs <= 0 || njobs > PMLP_MAX_GEMM_JOBS || !jobs) return fail(-1, "pmlp_gemm: 1..PMLP_MAX_GEMM_JOBS jobs");
     GemmBatch gb{};
     gb.slabs = 1;
@@ -1244,9 +1329,15 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         const pmlp_gemm_job& J = jobs[i];
         const std::string w = "pmlp_gemm job " + std::to_string(i) + ": ";
         if (!J.A || !J.B || J.M <= 0 || J.N <= 0 || J.K <= 0) return fail(-1, w + "null operand or empty shape");
-        if (J.K % 8 || J.lda % 8 || J.ldb % 8 || J.lda < J.K || J.ldb < J.K || !al16(J.A) || !al16(J.B))
+        if (epi == PMLP_EPI_PARTIAL_TN) {
+            // A[K,M], B[K,N]: whole 16-byte chunks along m and n are read
+            if (J.lda % 8 || J.ldb % 8 || J.lda < (J.M + 7) / 8 * 8 || J.ldb < (J.N + 7) / 8 * 8 || !al16(J.A) ||
+                !al16(J.B))
+                return fail(-1, w + "PARTIAL_TN: lda >= ceil8(M), ldb >= ceil8(N), multiples of 8, 16-byte aligned");
+        } else if (J.K % 8 || J.lda % 8 || J.ldb % 8 || J.lda < J.K || J.ldb < J.K || !al16(J.A) || !al16(J.B)) {
             return fail(-1, w + "K, lda, ldb must be multiples of 8 with 16-byte aligned operands");
-        if ((epi == PMLP_EPI_FWD_OUT || epi == PMLP_EPI_PARTIAL) && (!J.cf || J.ldcf < J.N))
+        }
+        if ((epi == PMLP_EPI_FWD_OUT || part) && (!J.cf || J.ldcf < J.N))
             return fail(-1, w + "fp32 output missing or ldcf < N");
         if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) &&
             ((!J.cb && !J.ct) || (J.cb && J.ldcb < J.N) || (J.ct && (J.ldct < J.M || J.ldct % 4))))
@@ -1259,7 +1350,7 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         g.M = J.M; g.N = J.N; g.K = J.K; g.ksplit = ksplit;
         maxm = std::max(maxm, J.M); maxn = std::max(maxn, J.N); maxk = std::max(maxk, J.K);
     }
-    if (epi == PMLP_EPI_PARTIAL) {
+    if (part) {
         if (ksplit <= 0 || ksplit % 32) return fail(-1, "pmlp_gemm: ksplit must be a positive multiple of 32");
         for (int i = 0; i < njobs; ++i)
             if ((jobs[i].K + ksplit - 1) / ksplit != (maxk + ksplit - 1) / ksplit)
@@ -1270,7 +1361,7 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
     if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, st);
     else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, st);
     else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, st);
-    else if (epi != PMLP_EPI_PARTIAL && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
+    else if (!part && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
         launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, st);  // small grids: 4x the blocks hide the k-loop latency
     else {
         // 128x128 output tiles: 8 waves of 64x32 (accumulators in 32 VGPRs, no AGPRs:
@@ -1485,7 +1576,7 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
     if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
                           clipped_value, vcoef, ecoef))
         return e;
-    if (!partial || !stats || !dstd || !dmu || !dmu_t || !dvalue || !dvalue_t || Ap < A || Vp < 1)
+    if (!partial || !stats || !dstd || !dmu || !dvalue || Ap < A || Vp < 1)
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
     const int nb = (M + 63) / 64;

@@ -78,10 +78,14 @@ class FusedPPOStep:
         self.stats = self.grad[n:n + 4]
         self._side = None  # side stream of the weight-gradient GEMMs (run())
         # dW_l beside dX_l on a second stream: measured SLOWER (one update 6.44 -> 6.77 ms,
-        # tools/probes/update_graph_ab.py), the two latency-bound GEMMs contend; off by default
+        # tools/probes/update_env_ab.py), the two latency-bound GEMMs contend; off by default
         self.dw_side_stream = os.environ.get("PMLP_DW_SIDE_STREAM", "0") == "1"
         # the bf16 weight copies (wb) lag the fp32 weights after an optimizer step
         self.weights_changed = True
+        # weight gradients read the row-major activations through LDS-transposed MFMA
+        # operands (PARTIAL_TN), so no transposed copy is ever written; PMLP_TN=0 keeps
+        # the transposed copies and the k-contiguous PARTIAL GEMM (A/B comparisons)
+        self.tn = os.environ.get("PMLP_TN", "1") != "0"
         self.sync_optimizer_state(alg.optimizer)
         self._alloc()
 
@@ -91,16 +95,22 @@ class FusedPPOStep:
         L = len(self.lins[0])
         self.L = L
         self.k0p = [_ceil8(ls[0].in_features) for ls in self.lins]
-        self.xb = [torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
-        # transposed activations carry 8 extra rows: a row of ones (then zeros) makes the
-        # weight-gradient GEMM's extra column the bias gradient (no separate row sums)
-        self.xt = [self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k) for k in self.k0p]
+        tn = self.tn
+        # Activations carry 8 extra columns (tn: row-major) or rows (transposed copies): a
+        # column of ones (then zeros) makes the weight-gradient GEMM's extra output column
+        # the bias gradient (no separate row sums).  The forward reads only the first K.
+        self.xb = [self._ones_col(torch.empty(M, k + 8, dtype=bf, device=dev), k) if tn else
+                   torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
+        self.xt = [None if tn else self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k)
+                   for k in self.k0p]
         self.wb = [[torch.empty(lin.out_features, self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
                     for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
         self.wt = [[torch.empty(lin.in_features, _ceil8(lin.out_features), dtype=bf, device=dev) if l > 0 else None
                     for l, lin in enumerate(ls)] for ls in self.lins]
-        self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
-        self.yt = [[self._ones_row(torch.empty(lin.out_features + 8, M, dtype=bf, device=dev), lin.out_features)
+        self.y = [[self._ones_col(torch.empty(M, lin.out_features + 8, dtype=bf, device=dev), lin.out_features) if tn
+                   else torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
+        self.yt = [[None if tn else
+                    self._ones_row(torch.empty(lin.out_features + 8, M, dtype=bf, device=dev), lin.out_features)
                     for lin in ls[:-1]] for ls in self.lins]
         self.out = [torch.empty(M, ls[-1].out_features, device=dev) for ls in self.lins]
         A = self.lins[0][-1].out_features
@@ -109,10 +119,11 @@ class FusedPPOStep:
         self.loss_partial = torch.empty(mm.load().pmlp_ppo_loss_step_parts(M, A), device=dev)
         # output gradients (bf16, both layouts) and the hidden-layer input gradients
         self.dz_out = [torch.empty(M, _ceil8(ls[-1].out_features), dtype=bf, device=dev) for ls in self.lins]
-        self.dzt_out = [torch.empty(_ceil8(ls[-1].out_features), M, dtype=bf, device=dev) for ls in self.lins]
-        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 1 else None
+        self.dzt_out = [None if tn else torch.empty(_ceil8(ls[-1].out_features), M, dtype=bf, device=dev)
+                        for ls in self.lins]
+        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 1 or (tn and l > 0) else None
                     for l, lin in enumerate(ls)] for ls in self.lins]
-        self.dzt = [[torch.empty(lin.in_features, M, dtype=bf, device=dev) if l > 0 else None
+        self.dzt = [[torch.empty(lin.in_features, M, dtype=bf, device=dev) if l > 0 and not tn else None
                      for l, lin in enumerate(ls)] for ls in self.lins]
         # split-K weight-gradient slabs; layers whose padded width differs from the
         # parameter's get a staging buffer (copied into the flat gradient)
@@ -128,6 +139,12 @@ class FusedPPOStep:
             self.dw_stage.append([None if kps[n] == self.lins[n][l].in_features else
                                   torch.empty(self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
         self.opt_partial = torch.empty(mm.load().pmlp_opt_parts(), device=dev)
+
+    @staticmethod
+    def _ones_col(t, k):
+        t[:, k:].zero_()
+        t[:, k].fill_(1.0)
+        return t
 
     @staticmethod
     def _ones_row(t, k):
@@ -164,9 +181,15 @@ class FusedPPOStep:
         shared = cobs is obs and self.k0p[0] == self.k0p[1]
         lib = mm.load()
         # 1. gathered observations + weights -> bf16
-        jobs = [(obs, self.k0p[0], self.xb[0], self.xt[0], rows)]
-        if not shared:
-            jobs.append((cobs, self.k0p[1], self.xb[1], self.xt[1], rows))
+        tn = self.tn
+        if tn:  # row-major [M, k0p + 8] with the ones column at k0p
+            jobs = [(obs, self.k0p[0] + 8, self.xb[0], None, rows, self.k0p[0])]
+            if not shared:
+                jobs.append((cobs, self.k0p[1] + 8, self.xb[1], None, rows, self.k0p[1]))
+        else:
+            jobs = [(obs, self.k0p[0], self.xb[0], self.xt[0], rows)]
+            if not shared:
+                jobs.append((cobs, self.k0p[1], self.xb[1], self.xt[1], rows))
         for n in range(2):
             for l, lin in enumerate(self.lins[n]):
                 W = lin.weight.detach()
@@ -201,8 +224,8 @@ class FusedPPOStep:
                                       P(sigma_old), P(adv), P(ret), P(values), P(rows), M, A, float(alg.clip_param),
                                       int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
                                       float(alg.entropy_coef), P(self.loss_partial), P(self.stats),
-                                      P(self._gview[id(ac.std)]), P(self.dz_out[0]), P(self.dzt_out[0]),
-                                      self.dz_out[0].shape[1], P(self.dz_out[1]), P(self.dzt_out[1]),
+                                      P(self._gview[id(ac.std)]), P(self.dz_out[0]), mm._p(self.dzt_out[0]),
+                                      self.dz_out[0].shape[1], P(self.dz_out[1]), mm._p(self.dzt_out[1]),
                                       self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
         #    dW_l (split-K slabs) and dX_l both read only dz_l; with dw_side_stream dW_l runs
@@ -218,10 +241,14 @@ class FusedPPOStep:
             gj = []
             for n in range(2):
                 lin = self.lins[n][l]
-                B = xt[n] if l == 0 else self.yt[n][l - 1]
                 kp = self.k0p[n] if l == 0 else lin.in_features
                 slab = self.slab[l][n]
-                gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
+                if tn:  # A = dz [M, out], B = activations [M, kp + 8] (row-major)
+                    B = xb[n] if l == 0 else self.y[n][l - 1]
+                    gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
+                else:
+                    B = xt[n] if l == 0 else self.yt[n][l - 1]
+                    gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
                 dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
                 red.append((slab, dw, lin.out_features * (kp + 8), slab.shape[0], self._gview[id(lin.bias)],
                             kp + 8, kp))
@@ -229,15 +256,14 @@ class FusedPPOStep:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
             side.wait_stream(main)  # dz_l is ready
             with torch.cuda.stream(side):
-                mm._gemm(mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
+                mm._gemm(mm.EPI_PARTIAL_TN if tn else mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
             if l > 0:
                 gj = []
                 for n in range(2):
                     lin = self.lins[n][l]
                     # the input layer's gradient is only consumed transposed (its weight gradient)
                     gj.append(dict(A=dz[n], B=self.wt[n][l], M=M, N=lin.in_features, K=dz[n].shape[1],
-                                   yprev=self.y[n][l - 1], cb=self.dz[n][l] if l > 1 else None,
-                                   ct=self.dzt[n][l]))
+                                   yprev=self.y[n][l - 1], cb=self.dz[n][l], ct=self.dzt[n][l]))
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
                 dzt = [self.dzt[n][l] for n in range(2)]

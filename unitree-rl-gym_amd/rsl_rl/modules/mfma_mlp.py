@@ -17,7 +17,7 @@ import os
 import torch
 import torch.nn as nn
 
-EPI_FWD_HIDDEN, EPI_FWD_OUT, EPI_BWD_DX, EPI_PARTIAL = 0, 1, 2, 3
+EPI_FWD_HIDDEN, EPI_FWD_OUT, EPI_BWD_DX, EPI_PARTIAL, EPI_PARTIAL_TN = 0, 1, 2, 3, 4
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
@@ -31,7 +31,8 @@ def lib_path():
 
 class ConvertJob(C.Structure):
     _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("yt", C.c_void_p), ("rows", C.c_void_p), ("M", C.c_int32),
-                ("K", C.c_int32), ("ldx", C.c_int32), ("Kp", C.c_int32), ("ldyt", C.c_int32)]
+                ("K", C.c_int32), ("ldx", C.c_int32), ("Kp", C.c_int32), ("ldyt", C.c_int32),
+                ("one_col", C.c_int32)]
 
 
 class GemmJob(C.Structure):
@@ -129,14 +130,16 @@ def supported(seq):
 
 
 def _convert(jobs):
-    """jobs: (x fp32 [*,K], Kp, y bf16 [M,Kp] | None, yt bf16 [Kp,ld] | None[, rows int64 [M]]);
-    without rows M = x.shape[0], with rows output row m is x[rows[m]]."""
+    """jobs: (x fp32 [*,K], Kp, y bf16 [M,Kp] | None, yt bf16 [Kp,ld] | None[, rows int64 [M]
+    | None[, one_col]]); without rows M = x.shape[0], with rows output row m is x[rows[m]];
+    one_col > 0: that column of y is 1.0 (the bias column of a weight-gradient operand)."""
     def mk(j):
         x, kp, y, yt = j[:4]
         rows = j[4] if len(j) > 4 else None
+        one = j[5] if len(j) > 5 else 0
         M = x.shape[0] if rows is None else rows.shape[0]
         return ConvertJob(_p(x), _p(y), _p(yt), _p(rows), M, x.shape[1], x.stride(0), kp,
-                          0 if yt is None else yt.shape[1])
+                          0 if yt is None else yt.shape[1], one)
     for i in range(0, len(jobs), MAX_JOBS):
         chunk = jobs[i:i + MAX_JOBS]
         arr = (ConvertJob * len(chunk))(*[mk(j) for j in chunk])
