@@ -49,7 +49,8 @@ def wrap(name, fn, keyf):
     return w
 
 
-EPI = {mm.EPI_FWD_HIDDEN: "FWD", mm.EPI_FWD_OUT: "FWD_OUT", mm.EPI_PARTIAL: "PARTIAL", mm.EPI_BWD_DX: "BWD_DX"}
+EPI = {mm.EPI_FWD_HIDDEN: "FWD", mm.EPI_FWD_OUT: "FWD_OUT", mm.EPI_PARTIAL: "PARTIAL", mm.EPI_BWD_DX: "BWD_DX",
+       mm.EPI_PARTIAL_TN: "PART_TN"}
 mm._gemm = wrap("gemm", mm._gemm, lambda epi, jobs, ksplit=0: f"gemm {EPI.get(epi, epi):8s} M={jobs[0]['M']:6d} "
                 f"N={jobs[0]['N']:4d} K={jobs[0]['K']:6d} x{len(jobs)}")
 mm._convert = wrap("convert", mm._convert, lambda jobs: "convert")

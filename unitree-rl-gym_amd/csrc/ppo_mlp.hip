@@ -63,7 +63,13 @@ struct GemmArgs {
     int M, N, K, ksplit;
 };
 
+#ifdef PMLP_EXACT_ELU
 __device__ __forceinline__ float elu(float v) { return v > 0.f ? v : expm1f(v); }
+#else
+// exp(v) - 1 on v_exp_f32 (a few instructions instead of expm1f's ~20): the absolute
+// error stays within a few ulp of 1.0, far below the bf16 rounding every ELU output gets
+__device__ __forceinline__ float elu(float v) { return v > 0.f ? v : __expf(v) - 1.f; }
+#endif
 
 struct GemmBatch {
     GemmArgs j[PMLP_MAX_GEMM_JOBS];
@@ -76,7 +82,7 @@ __device__ __forceinline__ shortx4 lds_read_tr(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)p);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4>
 __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     const int job = blockIdx.z / gb.slabs, slice = blockIdx.z % gb.slabs;
     const GemmArgs& g = gb.j[job];
@@ -195,45 +201,39 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     // k = 8(l>>5)..+7) = two transposed reads of k rows 8(l>>5) + {0..3, 4..7}
     const int tr_off = 8 * (lane >> 5) + ((lane >> 2) & 3);  // k row within a 16-step
     const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-    auto compute = [&]() {
+    auto kstep = [&](int s) {
+        bf16x8 af[FM], bfr[FN];
         if constexpr (TNL) {
 #pragma unroll
-            for (int s = 0; s < BK / 16; ++s) {
-                bf16x8 af[FM], bfr[FN];
-#pragma unroll
-                for (int i = 0; i < FM; ++i) {
-                    const bf16* p = As + (s * 16 + tr_off) * SA + wm * TM + i * 32 + tr_col;
-                    const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SA);
-                    af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-                }
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const bf16* p = Bs + (s * 16 + tr_off) * SB + wn * TN + j * 32 + tr_col;
-                    const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SB);
-                    bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-                }
-#pragma unroll
-                for (int i = 0; i < FM; ++i)
-#pragma unroll
-                    for (int j = 0; j < FN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < FM; ++i) {
+                const bf16* p = As + (s * 16 + tr_off) * SA + wm * TM + i * 32 + tr_col;
+                const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SA);
+                af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
-            return;
-        }
 #pragma unroll
-        for (int s = 0; s < BK / 16; ++s) {
-            bf16x8 af[FM], bfr[FN];
+            for (int j = 0; j < FN; ++j) {
+                const bf16* p = Bs + (s * 16 + tr_off) * SB + wn * TN + j * 32 + tr_col;
+                const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SB);
+                bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+        } else {
             const int ko = s * 16 + (lane >> 5) * 8;
 #pragma unroll
             for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(As + (wm * TM + i * 32 + (lane & 31)) * LS + ko);
 #pragma unroll
             for (int j = 0; j < FN; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * TN + j * 32 + (lane & 31)) * LS + ko);
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    // NKS < 4: a single short k-tile (K <= 16 NKS: 48 for the first layer's forward, 16
+    // for the last layer's input gradient), so the k-steps of zero operands are not issued
+    auto compute = [&](int) {
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) kstep(s);
     };
 
     gload(kb);
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     for (int k0 = kb; k0 < ke; k0 += BK) {
         const bool more = k0 + BK < ke;
         if (more) gload(k0 + BK);
-        compute();
+        compute(k0);
         if (more) {
             As = (As == smem) ? smem + (BM + BN) * LS : smem;
             Bs = As + BM * LS;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         lstore();
         __syncthreads();
         if (k0 + BK < ke) gload(k0 + BK);
-        compute();
+        compute(k0);
     }
 #endif
 
@@ -1278,8 +1278,17 @@ __global__ __launch_bounds__(64 * MLP4_WAVES) void k_mlp4_fwd(Mlp4Jobs jobs, int
 }
 
 template <int BM, int BN, int WM, int WN>
-static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, hipStream_t st) {
+static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
+    // one short k-tile: only the k-steps that carry data (K = 48 forward, K = 16 input gradient)
+    if (epi == PMLP_EPI_FWD_HIDDEN && maxk <= 48 && maxk > 32) {
+        hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 3>), grid, block, 0, st, gb);
+        return;
+    }
+    if (epi == PMLP_EPI_BWD_DX && maxk <= 16) {
+        hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1>), grid, block, 0, st, gb);
+        return;
+    }
     switch (epi) {
     case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, gb); break;
     case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, gb); break;
@@ -1358,11 +1367,11 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         gb.slabs = (maxk + ksplit - 1) / ksplit;
     }
     hipStream_t st = (hipStream_t)stream;
-    if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, st);
-    else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, st);
-    else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, st);
+    if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, maxk, st);
+    else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, maxk, st);
+    else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, maxk, st);
     else if (!part && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
-        launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, st);  // small grids: 4x the blocks hide the k-loop latency
+        launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, maxk, st);  // small grids: 4x the blocks hide the k-loop latency
     else {
         // 128x128 output tiles: 8 waves of 64x32 (accumulators in 32 VGPRs, no AGPRs:
         // 4 waves/SIMD resident instead of 3) for the epilogue-heavy short-K GEMMs; 4 waves
@@ -1374,9 +1383,9 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
             return v ? atoi(v) : -1;
         }();
         const int pick = big >= 0 ? big : ((epi == PMLP_EPI_FWD_HIDDEN && maxk >= 256) ? 0 : 1);
-        if (pick == 1) launch<128, 128, 2, 4>(epi, gb, njobs, maxm, maxn, st);
-        else if (pick == 2) launch<128, 128, 4, 2>(epi, gb, njobs, maxm, maxn, st);
-        else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, st);
+        if (pick == 1) launch<128, 128, 2, 4>(epi, gb, njobs, maxm, maxn, maxk, st);
+        else if (pick == 2) launch<128, 128, 4, 2>(epi, gb, njobs, maxm, maxn, maxk, st);
+        else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, maxk, st);
     }
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
