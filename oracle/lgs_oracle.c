@@ -395,23 +395,34 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         }
         M[(6 + j) * NMAX + 6 + j] += sp->armature;
     }
-    float rhs[NMAX];
-    for (int k = 0; k < 6; ++k) rhs[k] = -C[k];
-    for (int j = 0; j < D; ++j) rhs[6 + j] = tau[j] - C[6 + j];
+    float rhs0[NMAX];
+    for (int k = 0; k < 6; ++k) rhs0[k] = -C[k];
+    for (int j = 0; j < D; ++j) rhs0[6 + j] = tau[j] - C[6 + j];
+    /* The factorisation and every solve run in the LEAVES-FIRST order p = n-1-i of the
+     * natural [base, joints in DFS order] index (each DOF after all of its descendants):
+     * L then has no fill-in, its structural zeros are exact, and the HIP kernel skips
+     * them (leggedsim.hip l_nz) without changing a result bit. */
+    static __thread float Mp[NMAX * NMAX];
+    float rhs[NMAX], qdd[NMAX];
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < n; ++j) Mp[i * NMAX + j] = M[(n - 1 - i) * NMAX + (n - 1 - j)];
+        rhs[i] = rhs0[n - 1 - i];
+    }
     float invd[NMAX];
-    cholesky(M, invd, n);
-    fwd_sub(M, invd, n, rhs);
-    bwd_sub(M, invd, n, rhs); /* rhs = qdd */
+    cholesky(Mp, invd, n);
+    fwd_sub(Mp, invd, n, rhs);
+    bwd_sub(Mp, invd, n, rhs);
+    for (int i = 0; i < n; ++i) qdd[i] = rhs[n - 1 - i];
 
     /* free velocity (classical velocity of the root origin after dt) */
     float qf[NMAX];
     float wxv[3];
     cross3(w0, vO, wxv);
     for (int k = 0; k < 3; ++k) {
-        qf[k] = w0[k] + dt * rhs[k];
-        qf[3 + k] = vO[k] + dt * (rhs[3 + k] + wxv[k]);
+        qf[k] = w0[k] + dt * qdd[k];
+        qf[3 + k] = vO[k] + dt * (qdd[3 + k] + wxv[k]);
     }
-    for (int j = 0; j < D; ++j) qf[6 + j] = dofs[2 * j + 1] + dt * rhs[6 + j];
+    for (int j = 0; j < D; ++j) qf[6 + j] = dofs[2 * j + 1] + dt * qdd[6 + j];
 
     /* ---- constraint rows: contacts (n, t1, t2) first, then joint limits.
      * Gauss-Seidel visits them in this order (the HIP kernel keeps contact c at
@@ -487,12 +498,12 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
             kind[nr++] = 0;
         }
     }
-    /* Y = L^-1 J^T ; A = Y^T Y ; v = J qf */
+    /* Y = L^-1 J^T (leaves-first columns) ; A = Y^T Y ; v = J qf (natural order) */
     static __thread float Y[ROWMAX][NMAX];
     static __thread float A[ROWMAX][ROWMAX];
     for (int r = 0; r < nr; ++r) {
-        memcpy(Y[r], J[r], sizeof(float) * n);
-        fwd_sub(M, invd, n, Y[r]);
+        for (int i = 0; i < n; ++i) Y[r][i] = J[r][n - 1 - i];
+        fwd_sub(Mp, invd, n, Y[r]);
         float s = 0.f;
         for (int i = 0; i < n; ++i) s += J[r][i] * qf[i];
         v[r] = s;
@@ -535,9 +546,9 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         for (int r = 0; r < nr; ++r) s += Y[r][i] * lam[r];
         z[i] = s;
     }
-    bwd_sub(M, invd, n, z);
+    bwd_sub(Mp, invd, n, z);
     float qn[NMAX];
-    for (int i = 0; i < n; ++i) qn[i] = qf[i] + z[i];
+    for (int i = 0; i < n; ++i) qn[i] = qf[i] + z[n - 1 - i];
     if (sp->clamp_joint_velocity)
         for (int j = 0; j < D; ++j) {
             float lim = md->dof_velocity[j];

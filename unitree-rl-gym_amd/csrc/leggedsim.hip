@@ -361,7 +361,19 @@ __device__ __forceinline__ void load_model(Smem<D, B, ROWS>& s, const DevModel& 
 //   broadcast by readlane; A = Y Y^T on the matrix cores
 //   (v_mfma_f32_32x32x2_f32: exact fp32 fma chain over k); PGS with each lane
 //   holding its column of A in registers.
-template <int D, int B, int ROWS>
+// The linear algebra runs in the LEAVES-FIRST order: index p = n-1-i of the natural
+// [base (6), joints in DFS order] order, i.e. every DOF after all of its descendants,
+// so the Cholesky factor has no fill-in.  With CH > 0 every joint chain has CH DOFs
+// hanging from the base (Go2: 4 x 3, G1 / H1_2: 2 x 6, H1: 2 x 5), and column k < D
+// of L is nonzero only at rows k+1 .. k+pos(k) (the joint's ancestors on its chain,
+// pos = its depth in the chain) and at the base rows D..n-1.  Structurally zero
+// entries are exact zeros (no fill-in), so skipping them changes no result bit.
+template <int D, int CH>
+__host__ __device__ constexpr bool l_nz(int i, int k) {  // may L[i][k] (i > k) be nonzero?
+    return CH == 0 || k >= D || i >= D || i <= k + (D - 1 - k) % CH;
+}
+
+template <int D, int B, int ROWS, int CH>
 __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& sp, float added_mass, float shape_mu) {
     constexpr int n = 6 + D;
     const ModelCache<D, B>& mc = s.mc;
@@ -532,56 +544,53 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     __syncthreads();
     STAMP(4);
-    // ---- 5. row `lane` of the mass matrix (lower triangle) into registers, rhs = tau - C
+    // ---- 5. row `lane` of the leaves-first mass matrix (lower triangle) into
+    // registers, rhs = tau - C.  Lane i < D: joint jr = D-1-i (columns: itself and its
+    // descendants); lane i >= D: base row r = n-1-i (columns: every joint, and the
+    // base columns c >= r).
     float m[n];
     float x = 0.f;
 #pragma unroll
     for (int c = 0; c < n; ++c) m[c] = 0.f;
-    if (lane < 6) {
+    if (lane >= D && lane < n) {
+        const int r = n - 1 - lane;
         const float* I = (&s.u.dyn.cpk[0][4]);
         const float* h = (&s.u.dyn.cpk[0][1]);
         const float cm0 = s.u.dyn.cpk[0][0];
-        // [[I, [h]x], [[h]x^T, m 1]]: rows 0-2 need cols 0-2 only (lower triangle)
-        if (lane < 3) {
-            const int r = lane;
-            m[0] = I[r == 0 ? 0 : (r == 1 ? 3 : 4)];
-            m[1] = I[r == 0 ? 3 : (r == 1 ? 1 : 5)];
-            m[2] = I[r == 0 ? 4 : (r == 1 ? 5 : 2)];
-        } else {
-            const int i = lane - 3;  // ([h]x)^T row i = column i of [h]x
-            const float H[9] = {0.f, -h[2], h[1], h[2], 0.f, -h[0], -h[1], h[0], 0.f};
-            m[0] = H[i]; m[1] = H[3 + i]; m[2] = H[6 + i];
-            m[3] = (i == 0) ? cm0 : 0.f;
-            m[4] = (i == 1) ? cm0 : 0.f;
-            m[5] = (i == 2) ? cm0 : 0.f;
-        }
-        x = -(lane < 3 ? s.u.dyn.cpk[0][10 + lane] : s.u.dyn.cpk[0][13 + lane - 3]);
-    } else if (lane < n) {
-        const int j = lane - 6;
-        const int bj = mc.dofbody[j];
-        float cn[3], cf[3];
+        // M[r][6+j] = (F_j)_r
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { cn[k] = s.u.dyn.Fj[j][k]; cf[k] = s.u.dyn.Fj[j][3 + k]; }
-        m[0] = cn[0]; m[1] = cn[1]; m[2] = cn[2];
-        m[3] = cf[0]; m[4] = cf[1]; m[5] = cf[2];
-        const unsigned am = mc.anc[j];
+        for (int cp = 0; cp < D; ++cp) m[cp] = s.u.dyn.Fj[D - 1 - cp][r];
+        // base block [[I, [h]x], [[h]x^T, m 1]], entries c >= r
+        const float H[9] = {0.f, -h[2], h[1], h[2], 0.f, -h[0], -h[1], h[0], 0.f};
+        const float I3[9] = {I[0], I[3], I[4], I[3], I[1], I[5], I[4], I[5], I[2]};
 #pragma unroll
-        for (int c = 6; c < n; ++c) {
-            const int i = c - 6;
-            const float4* q = (const float4*)s.u.dyn.Sd[i];
-            const float4 s0 = q[0], s1 = q[1];
-            const float Si_w[3] = {s0.x, s0.y, s0.z};
-            const float Si_v[3] = {s0.w, s1.x, s1.y};
-            float val = dot3(Si_w, cn) + dot3(Si_v, cf);
-            if (i == j) val += sp.armature;
-            m[c] = ((am >> i) & 1u) ? val : 0.f;
+        for (int c = 0; c < 6; ++c) {  // c compile-time, r per lane: selects, no indexed registers
+            const float* T = c < 3 ? I3 : H;
+            const int cc = c < 3 ? c : c - 3;
+            float val = r == 0 ? T[cc] : (r == 1 ? T[3 + cc] : (r == 2 ? T[6 + cc] : 0.f));
+            if (c >= 3) val = r < 3 ? val : (r == c ? cm0 : 0.f);
+            m[n - 1 - c] = c >= r ? val : 0.f;
         }
+        x = -(r < 3 ? s.u.dyn.cpk[0][10 + r] : s.u.dyn.cpk[0][13 + r - 3]);
+    } else if (lane < D) {
+        const int jr = D - 1 - lane;
+        const int bj = mc.dofbody[jr];
         float Sw[3] = {s.u.dyn.Sw[bj][0], s.u.dyn.Sw[bj][1], s.u.dyn.Sw[bj][2]};
         float Sv[3] = {s.u.dyn.Sv[bj][0], s.u.dyn.Sv[bj][1], s.u.dyn.Sv[bj][2]};
+        // M[jr][jc] = S_jr . F_jc for jc a descendant-or-self of jr
+#pragma unroll
+        for (int cp = 0; cp < D; ++cp) {
+            const int jc = D - 1 - cp;
+            const float* F = s.u.dyn.Fj[jc];
+            const float cn[3] = {F[0], F[1], F[2]}, cf[3] = {F[3], F[4], F[5]};
+            float val = dot3(Sw, cn) + dot3(Sv, cf);
+            if (jc == jr) val += sp.armature;
+            m[cp] = ((mc.anc[jc] >> jr) & 1u) ? val : 0.f;
+        }
         float Fn[3] = {s.u.dyn.cpk[bj][10 + 0], s.u.dyn.cpk[bj][10 + 1], s.u.dyn.cpk[bj][10 + 2]};
         float Ff[3] = {s.u.dyn.cpk[bj][13 + 0], s.u.dyn.cpk[bj][13 + 1], s.u.dyn.cpk[bj][13 + 2]};
         float C = dot3(Sw, Fn) + dot3(Sv, Ff);
-        x = s.tau[j] - C;
+        x = s.tau[jr] - C;
     }
     STAMP(5);
     // ---- 6. Cholesky, right-looking on register rows.  Entry (i,j) receives
@@ -604,6 +613,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         idg = ln == k ? inv : idg;
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
+            if (!l_nz<D, CH>(j, k)) continue;  // L_jk == 0: no update (compile-time after unrolling)
             const float ljk = rl(m[k], j);
             m[j] = ln >= j ? m[j] - m[k] * ljk : m[j];
         }
@@ -640,17 +650,19 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             x = ln < i ? x - lc[i] * xi : x;
         }
     }
-    // free velocity (classical velocity of the root origin after dt)
+    // free velocity (classical velocity of the root origin after dt); lane i holds
+    // qdd of natural index r = n-1-i, s.qf is in the natural order
     {
         float wxv[3];
         cross3(w0, vO, wxv);
-        const int c = lane % 3;
+        const int r = n - 1 - lane;
+        const int c = (r >= 0 ? r : 0) % 3;
         const float wl = c == 0 ? w0[0] : (c == 1 ? w0[1] : w0[2]);
         const float vl = c == 0 ? vO[0] : (c == 1 ? vO[1] : vO[2]);
         const float cl = c == 0 ? wxv[0] : (c == 1 ? wxv[1] : wxv[2]);
-        if (lane < 3) s.qf[lane] = wl + dt * x;
-        else if (lane < 6) s.qf[lane] = vl + dt * (x + cl);
-        else if (lane < n) s.qf[lane] = s.qd[lane - 6] + dt * x;
+        if (lane < D) s.qf[r] = s.qd[r - 6] + dt * x;
+        else if (lane < n - 3) s.qf[r] = vl + dt * (x + cl);
+        else if (lane < n) s.qf[r] = wl + dt * x;
     }
     __syncthreads();
     STAMP(7);
@@ -763,19 +775,28 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int i = 0; i < n; ++i) y[i] = used ? s.u.con.Y[lane][i] : 0.f;
 #pragma unroll
         for (int i = 0; i < n; ++i) v += y[i] * s.qf[i];
-        // row i of L and 1/L_ii as wave-uniform LDS reads (16-byte row loads on the LDS
-        // pipe) instead of ~170 v_readlane broadcasts on the VALU
+        // leaves-first order (register renaming only), then row i of L and 1/L_ii as
+        // wave-uniform LDS reads (16-byte row loads on the LDS pipe) instead of ~170
+        // v_readlane broadcasts on the VALU; structurally zero L entries are skipped
+        float yp[n];
+#pragma unroll
+        for (int i = 0; i < n; ++i) yp[i] = y[n - 1 - i];
 #pragma unroll
         for (int i = 0; i < n; ++i) {
             const float* Li = s.L[i];
-            float t = y[i];
+            float t = yp[i];
 #pragma unroll
-            for (int k = 0; k < i; ++k) t -= Li[k] * y[k];
-            y[i] = t * s.Linv[i];
+            for (int k = 0; k < i; ++k)
+                if (l_nz<D, CH>(i, k)) t -= Li[k] * yp[k];
+            yp[i] = t * s.Linv[i];
+            // pinned per row: with the sparse joint rows independent the scheduler
+            // otherwise runs them all at once and spills at the 128-VGPR (4 waves/SIMD)
+            // budget
+            if (CH > 0) asm volatile("" : "+v"(yp[i]));
         }
         if (lane < ROWS) {
 #pragma unroll
-            for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = y[i];
+            for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = yp[i];
         }
     }
     __syncthreads();
@@ -919,9 +940,10 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             z = ln < i ? z - lc[i] * zi : z;
         }
     }
-    float qn = (lane < n) ? s.qf[lane] + z : 0.f;
-    if (sp.clamp_qd && lane >= 6 && lane < n) {
-        const float lim = mc.vl[lane - 6];
+    // back to the natural order: lane i < n holds qd' of index n-1-i
+    float qn = (lane < n) ? s.qf[n - 1 - lane] + z : 0.f;
+    if (sp.clamp_qd && lane < D) {
+        const float lim = mc.vl[D - 1 - lane];
         if (lim > 0.f) qn = fminf(fmaxf(qn, -lim), lim);
     }
     // contact forces of this substep
@@ -945,11 +967,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     STAMP(13);
     // ---- 13. integrate
-    const float qw0 = rl(qn, 0), qw1 = rl(qn, 1), qw2 = rl(qn, 2);
-    const float qv0 = rl(qn, 3), qv1 = rl(qn, 4), qv2 = rl(qn, 5);
+    const float qw0 = rl(qn, n - 1), qw1 = rl(qn, n - 2), qw2 = rl(qn, n - 3);
+    const float qv0 = rl(qn, n - 4), qv1 = rl(qn, n - 5), qv2 = rl(qn, n - 6);
     __syncthreads();
-    if (lane >= 6 && lane < n) {
-        const int j = lane - 6;
+    if (lane < D) {
+        const int j = D - 1 - lane;
         s.qd[j] = qn;
         s.q[j] = s.q[j] + dt * qn;
     }
@@ -1060,7 +1082,7 @@ __device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState&
 }
 
 // ---------------------------------------------------------- kernels --------
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
@@ -1069,12 +1091,12 @@ __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevSt
     load_state(s, st, e);
     if (threadIdx.x < D) s.tau[threadIdx.x] = st.torques_in[(size_t)D * e + threadIdx.x];
     __syncthreads();
-    substep(s, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
+    substep<D, B, ROWS, CH>(s, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
     store_state(s, st, e);
     if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
 }
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
@@ -1443,7 +1465,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     if (lane < 6) E.last_root_vel[6 * e + lane] = s.root[7 + lane];
 }
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? LGS_WAVES_PER_EU : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step) {
     __shared__ Smem<D, B, ROWS> s;
@@ -1477,7 +1499,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
             s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
         }
         __syncthreads();
-        substep(s, md, sp, am, mu);
+        substep<D, B, ROWS, CH>(s, md, sp, am, mu);
     }
     STAMP(0);
     if (lane < D) E.torques[D * e + lane] = s.tau[lane];
@@ -1493,7 +1515,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     STAMP_FLUSH(e);
 }
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
                                                     lgs_env_buffers E, int N, uint32_t step) {
     __shared__ Smem<D, B, ROWS> s;
@@ -1561,10 +1583,13 @@ struct lgs_sim {
     int16_t* hf_mem = nullptr;
     int has_task = 0;
     int rows = 32;
+    int chain = 0;  // dof_chain_length of the model
 };
 
-// Compiled (dofs, max bodies, constraint-row capacity) variants.  The row
-// capacity sets the LDS footprint (Y, A): the 32-row variant is the Go2 one.
+// Compiled (dofs, max bodies, constraint-row capacity, chain length) variants.  The
+// row capacity sets the LDS footprint (Y, A): the 32-row variant is the Go2 one.  The
+// chain length CH is the sparsity the Cholesky exploits (l_nz); a tree that is not
+// D/CH equal chains hanging from the base takes the dense (CH = 0) variant.
 enum Variant { V_12_19, V_12_13, V_10_11, V_12_19_48, V_NONE };
 
 static Variant pick(const lgs_sim* s) {
@@ -1575,15 +1600,48 @@ static Variant pick(const lgs_sim* s) {
     return V_NONE;
 }
 static int variant_rows(Variant v) { return v == V_12_19 ? 32 : 48; }
+static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 5 : 3); }
 
+#define LGS_LAUNCH(sim, KERNEL, D_, B_, R_, ...)                                                         \
+    do {                                                                                                 \
+        if ((sim)->chain == variant_chain(pick(sim)))                                                    \
+            hipLaunchKernelGGL((KERNEL<D_, B_, R_, (D_ == 10 ? 5 : (B_ == 13 ? 6 : 3))>), dim3((sim)->N), \
+                               dim3(WAVE), 0, (sim)->stream, __VA_ARGS__);                               \
+        else                                                                                             \
+            hipLaunchKernelGGL((KERNEL<D_, B_, R_, 0>), dim3((sim)->N), dim3(WAVE), 0, (sim)->stream,    \
+                               __VA_ARGS__);                                                             \
+    } while (0)
 #define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
     switch (pick(sim)) {                                                                                  \
-    case V_12_19: hipLaunchKernelGGL((KERNEL<12, 19, 32>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
-    case V_12_13: hipLaunchKernelGGL((KERNEL<12, 13, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
-    case V_10_11: hipLaunchKernelGGL((KERNEL<10, 11, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
-    case V_12_19_48: hipLaunchKernelGGL((KERNEL<12, 19, 48>), dim3(sim->N), dim3(WAVE), 0, sim->stream, __VA_ARGS__); break; \
+    case V_12_19: LGS_LAUNCH(sim, KERNEL, 12, 19, 32, __VA_ARGS__); break;                                \
+    case V_12_13: LGS_LAUNCH(sim, KERNEL, 12, 13, 48, __VA_ARGS__); break;                                \
+    case V_10_11: LGS_LAUNCH(sim, KERNEL, 10, 11, 48, __VA_ARGS__); break;                                \
+    case V_12_19_48: LGS_LAUNCH(sim, KERNEL, 12, 19, 48, __VA_ARGS__); break;                             \
     default: return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");                                 \
     }
+
+// Chain length of the DOF tree: CH if the D DOFs are D/CH chains of CH joints, each
+// hanging from the base, in DFS order (DOF j's nearest moving ancestor is DOF j-1, or
+// the base when j % CH == 0); 0 otherwise.
+static int dof_chain_length(const lgs_model_desc* m) {
+    const int D = m->num_dofs;
+    if (D <= 0) return 0;
+    int par[LGS_MAX_DOFS];
+    for (int b = 0; b < m->num_bodies; ++b) {
+        const int j = m->dof[b];
+        if (j < 0) continue;
+        int a = m->parent[b];
+        while (a > 0 && m->dof[a] < 0) a = m->parent[a];
+        par[j] = a > 0 ? m->dof[a] : -1;
+    }
+    for (int ch = 1; ch <= D; ++ch) {
+        if (D % ch) continue;
+        bool ok = true;
+        for (int j = 0; j < D && ok; ++j) ok = par[j] == (j % ch == 0 ? -1 : j - 1);
+        if (ok) return ch;
+    }
+    return 0;
+}
 
 static DevState state_of(lgs_sim* s) {
     DevState st;
@@ -1612,6 +1670,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     lgs_sim* s = new lgs_sim();
     s->N = num_envs; s->B = m->num_bodies; s->D = m->num_dofs; s->P = m->num_points; s->device = device_id;
     s->rows = p->max_rows;
+    s->chain = dof_chain_length(m);
     if (pick(s) == V_NONE) {
         delete s;
         return set_err(LGS_ERR_ARG, "lgs_create_sim: no kernel instantiation for this (dofs, bodies)");
