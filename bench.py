@@ -84,6 +84,27 @@ def load_pmc_traffic():
         return None
 
 
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per
+# SIMD (MI355X_MICROARCH.md: 32 lanes/cycle), at the 2.4 GHz peak engine clock
+VALU_PEAK_GINST_S = 256 * 4 * 2.4 / 2
+
+
+def load_sq_valu(kernel_ms):
+    """VALU-issue roofline of the env-step kernel: instructions per launch from the committed
+    rocprofv3 SQ summary (profiles/sq_k_step.json, tools/sq_summary.py) over the live launch
+    time.  The env step is latency-bound, so this, not GB/s, is its meaningful
+    utilisation figure; reported beside the HBM roofline the contract asks for."""
+    path = os.path.join(ROOT, "profiles", "sq_k_step.json")
+    try:
+        with open(path) as f:
+            sq = json.load(f)
+    except Exception:
+        return None
+    ginst = sq["valu_insts_per_launch"] / (kernel_ms * 1e-3) / 1e9
+    return {"achieved": round(ginst, 1), "peak": VALU_PEAK_GINST_S, "unit": "G VALU inst/s", "frac": ginst / VALU_PEAK_GINST_S,
+            "valu_insts_per_launch": sq["valu_insts_per_launch"], "share_of_wave_time": sq.get("share_of_wave_time")}
+
+
 def cpu_baseline(env, seconds):
     """The CPU oracle (oracle/lgs_oracle.c, OpenMP over envs) on the same Go2 workload."""
     import numpy as np
@@ -243,7 +264,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc_traffic(),
                      "kernel": "k_step<12,19,32> (fused Go2 control step)",
-                     "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms)},
     }
     if world == 1 and not args.no_other_configs:
         # the other BASELINE configs' env step on this GPU (their multi-GPU/LSTM PPO legs are

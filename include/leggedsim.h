@@ -214,6 +214,10 @@ typedef struct lgs_env_buffers {
     float* ep_means;         /* [num_sums] carried extras["episode"] values (rew_* / max_episode_length_s) */
     float* ep_snapshot;      /* [num_sums] this step's copy of ep_means (the step's extras["episode"]) */
     uint8_t* time_outs_carry;/* [N] extras["time_outs"]: time_out of the last step with a reset */
+    /* optional [N,A] policy actions read by lgs_step in place of `actions` (which still
+       receives the clipped copy, legged_robot.py:623-624): the caller's tensor is read
+       directly, with no separate copy launch; NULL: the actions are already in `actions`. */
+    const float* actions_in;
 } lgs_env_buffers;
 
 typedef struct lgs_sim lgs_sim;

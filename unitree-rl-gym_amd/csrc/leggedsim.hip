@@ -1479,7 +1479,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     const int A = T.num_actions;
     float a = 0.f;
     if (lane < A) {
-        a = clipf(E.actions[A * e + lane], -T.clip_actions, T.clip_actions);  // :623-624
+        const float* ain = E.actions_in ? E.actions_in : E.actions;
+        a = clipf(ain[A * e + lane], -T.clip_actions, T.clip_actions);  // :623-624
         E.actions[A * e + lane] = a;
         s.act[lane] = a;
     }

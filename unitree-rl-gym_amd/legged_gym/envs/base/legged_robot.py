@@ -332,11 +332,18 @@ class LeggedRobot(BaseTask):
         self._sync_stream()
         self._buf_idx ^= 1
         i = self._buf_idx
-        self.actions.copy_(actions)
+        E = self._env_structs[i]
+        # the kernel reads the caller's actions in place (clipped copy into self.actions);
+        # anything else is copied first
+        if (actions.is_cuda and actions.dtype == torch.float32 and actions.is_contiguous() and
+                actions.shape == self.actions.shape and actions.device == self.actions.device):
+            E.actions_in = actions.data_ptr()
+        else:
+            self.actions.copy_(actions)
+            E.actions_in = None
         # this step's extras["episode"] values (a fresh buffer per step, like the
         # reference's per-reset tensors; inside a captured rollout, one per step)
         snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
-        E = self._env_structs[i]
         E.ep_snapshot = snap.data_ptr()
         self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
         self._step_mirror += 1
