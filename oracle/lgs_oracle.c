@@ -262,6 +262,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
                      const float* tau, float* cforce, float added_mass, float shape_friction) {
     const int B = md->num_bodies, D = md->num_dofs, n = 6 + D;
     const float dt = sp->dt;
+    const float idt = 1.0f / dt; /* divisions by dt are multiplications by 1/dt (the HIP kernel's) */
     okin K;
     fk(md, root13, dofs, &K);
     const float* O = K.p[0];
@@ -472,7 +473,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
                 row[6 + j] = dot3(d, t);
             }
         }
-        tgt[nr] = sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp->max_depenetration_velocity);
+        tgt[nr] = sep >= 0.f ? -sep * idt : fminf(-beta * sep * idt, sp->max_depenetration_velocity);
         tgt[nr + 1] = tgt[nr + 2] = 0.f;
         kind[nr] = 0; kind[nr + 1] = 1; kind[nr + 2] = 2;
         cb[nc] = b;
@@ -488,13 +489,13 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
             memset(J[nr], 0, sizeof(float) * n);
             J[nr][6 + j] = 1.f;
             float gap = q - lo;
-            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            tgt[nr] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
             kind[nr++] = 0;
         } else if (qn > hi) {
             memset(J[nr], 0, sizeof(float) * n);
             J[nr][6 + j] = -1.f;
             float gap = hi - q;
-            tgt[nr] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            tgt[nr] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
             kind[nr++] = 0;
         }
     }
@@ -560,7 +561,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         int r = 3 * c;
         float* F = cforce + 3 * cb[c];
         for (int t = 0; t < 3; ++t) /* ln n + l1 t1 + l2 t2 */
-            F[t] += (lam[r] * cfr[c][0][t] + lam[r + 1] * cfr[c][1][t] + lam[r + 2] * cfr[c][2][t]) / dt;
+            F[t] += (lam[r] * cfr[c][0][t] + lam[r + 1] * cfr[c][1][t] + lam[r + 2] * cfr[c][2][t]) * idt;
     }
     (void)cpt;
     /* integrate (semi-implicit Euler) */

@@ -383,6 +383,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
     const float dt = sp.dt;
+    const float idt = 1.0f / dt;  // every per-row / per-force division by dt is a multiply (as the oracle)
 
     STAMP(0);
     // ---- 1. forward kinematics: joint rotations lane per DOF, then lane b walks root..b
@@ -734,7 +735,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             float* row = s.u.con.Y[r];
             for (int i = 0; i < n; ++i) row[i] = 0.f;
             row[6 + lane] = lo_act ? 1.f : -1.f;
-            s.tgt[r] = gap >= 0.f ? -gap / dt : -beta * gap / dt;
+            s.tgt[r] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
         }
     }
     __syncthreads();
@@ -762,7 +763,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             row[6 + j] = dot3(d, t);
         }
         const float sep = s.c_sep[cc];
-        s.tgt[lane] = dd != 0 ? 0.f : (sep >= 0.f ? -sep / dt : fminf(-beta * sep / dt, sp.max_depen));
+        s.tgt[lane] = dd != 0 ? 0.f : (sep >= 0.f ? -sep * idt : fminf(-beta * sep * idt, sp.max_depen));
     }
     __syncthreads();
     STAMP(9);
@@ -957,9 +958,9 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                     if (sp.hf) {
                         const float* fr = s.c_fr[c];  // world force = ln n + l1 t1 + l2 t2
 #pragma unroll
-                        for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) / dt;
+                        for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) * idt;
                     } else {  // plane: the same numbers (n = z, t1 = x, t2 = y exactly)
-                        F[0] += l1 / dt; F[1] += l2 / dt; F[2] += ln / dt;
+                        F[0] += l1 * idt; F[1] += l2 * idt; F[2] += ln * idt;
                     }
                 }
             }
