@@ -610,13 +610,16 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         asm volatile("" : "+v"(ln));
         const float d = sqrtf(fmaxf(rl(m[k], k), 1e-12f));
         const float inv = 1.0f / d;
-        m[k] = ln == k ? d : (ln > k ? m[k] * inv : m[k]);
+        // Lanes above the diagonal (i < k, i < j) update their upper-triangle registers
+        // too: nothing reads those (the L store, the solves and the broadcasts take the
+        // lower triangle only), and no lane mask / select is spent per update.
+        m[k] = ln == k ? d : m[k] * inv;
         idg = ln == k ? inv : idg;
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
             if (!l_nz<D, CH>(j, k)) continue;  // L_jk == 0: no update (compile-time after unrolling)
             const float ljk = rl(m[k], j);
-            m[j] = ln >= j ? m[j] - m[k] * ljk : m[j];
+            m[j] = m[j] - m[k] * ljk;
         }
         __builtin_amdgcn_sched_barrier(0);
     }
