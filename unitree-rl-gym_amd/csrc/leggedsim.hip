@@ -773,6 +773,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     const bool used = (lane < 3 * nc) || (lane >= 3 * CM && lane < 3 * CM + nlimit);
     // ---- 9. v = J qf ; Y = L^-1 J^T (lane r; L entries broadcast from their row lanes)
     float v = 0.f;
+    float dg = 0.f;  // A_rr = |Y_r|^2 of this lane's row (the MFMA's fp32 chain, k ascending)
     {
         float y[n];
 #pragma unroll
@@ -798,6 +799,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             // budget
             if (CH > 0) asm volatile("" : "+v"(yp[i]));
         }
+#pragma unroll
+        for (int i = 0; i < n; ++i) dg = fmaf(yp[i], yp[i], dg);
         if (lane < ROWS) {
 #pragma unroll
             for (int i = 0; i < n; ++i) s.u.con.Y[lane][i] = yp[i];
@@ -869,9 +872,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     {
         const float mu = 0.5f * (sp.ground_friction + shape_mu);
         float tg = used ? s.tgt[lane] : 0.f;
-        float dg = 0.f;
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) dg = (lane == r) ? acol[r] : dg;
+        // the diagonal comes from the lane's own row (above), not a 32-way select over
+        // acol (32 lane masks, which spilled SGPRs into VGPR lanes)
         float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
         for (int it = 0; it < sp.iters; ++it) {
             // Opaque per sweep: otherwise LICM hoists ~64 loop-invariant readlanes
@@ -880,6 +882,10 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             asm volatile("" : "+v"(tg), "+v"(inv));
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) asm volatile("" : "+v"(acol[r]));
+            // opaque lane id per sweep: the row masks (lane == r) are recomputed (one v_cmp
+            // each) instead of held across the sweeps in SGPRs, which spilled
+            int lid = lane;
+            asm volatile("" : "+v"(lid));
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
                 if (c < nc) {
@@ -901,7 +907,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                     }
                     const float d1 = l1 - l1o, d2 = l2 - l2o;
                     v += acol[r + 1] * d1 + acol[r + 2] * d2;
-                    lam = lane == r ? ln : (lane == r + 1 ? l1 : (lane == r + 2 ? l2 : lam));
+                    lam = lid == r ? ln : (lid == r + 1 ? l1 : (lid == r + 2 ? l2 : lam));
                 }
             }
 #pragma unroll
@@ -911,7 +917,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                     const float lo = rl(lam, r);
                     const float ln = fmaxf(0.f, lo + (rl(tg, r) - rl(v, r)) * rl(inv, r));
                     v = fmaf(acol[r], ln - lo, v);
-                    lam = lane == r ? ln : lam;
+                    lam = lid == r ? ln : lam;
                 }
             }
         }
