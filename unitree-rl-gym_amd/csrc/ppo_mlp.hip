@@ -1109,6 +1109,77 @@ __global__ __launch_bounds__(256) void k_act(ActArgs a) {
     }
 }
 
+// A <= 16: four lanes per env, lane c drawing and storing actions 4c..4c+3 (the Philox
+// counters of k_act, so the same samples); the env's log-prob terms go through LDS and
+// its first lane sums them in k order (k_act's arithmetic).  4x the sampling lanes of
+// k_act, whose one-lane-per-env loop kept the draw on a handful of CUs.
+__global__ __launch_bounds__(256) void k_act4(ActArgs a) {
+    __shared__ float terms[64][16];
+    const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+    const uint32_t draw = (uint32_t)*a.draw;
+    const uint2 key = make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    const int le = threadIdx.x >> 2, c = threadIdx.x & 3, k0 = 4 * c;
+    const bool vec = (a.A & 3) == 0 &&
+                     ((((uintptr_t)a.mu | (uintptr_t)a.actions_out | (uintptr_t)a.st_actions | (uintptr_t)a.st_mu |
+                        (uintptr_t)a.st_sigma) & 15) == 0);
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)a.N * 4; base += nth) {
+        const int64_t i = (base + threadIdx.x) >> 2;
+        if (i < a.N && k0 < a.A) {
+            const uint4 r = philox4x32(make_uint4(draw, (uint32_t)i, (uint32_t)c, 0x5050u), key);
+            const float rad0 = sqrtf(-2.f * logf(u01(r.x))), rad1 = sqrtf(-2.f * logf(u01(r.z)));
+            float z[4];
+            sincospif(2.f * u01(r.y), &z[1], &z[0]);
+            sincospif(2.f * u01(r.w), &z[3], &z[2]);
+            z[0] *= rad0; z[1] *= rad0; z[2] *= rad1; z[3] *= rad1;
+            const size_t o = (size_t)i * a.A + k0;
+            float act[4], mu[4], sg[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u;
+                if (k >= a.A) break;
+                sg[u] = a.stdv[k];
+                mu[u] = a.mu[o + u];
+                act[u] = mu[u] + sg[u] * z[u];
+                const float d = act[u] - mu[u];
+                terms[le][k] = -(d * d) / (2.f * sg[u] * sg[u]) - logf(sg[u]) - kHalfLog2Pi;
+            }
+            if (vec) {
+                const float4 av = make_float4(act[0], act[1], act[2], act[3]);
+                *(float4*)(a.actions_out + o) = av;
+                *(float4*)(a.st_actions + o) = av;
+                *(float4*)(a.st_mu + o) = make_float4(mu[0], mu[1], mu[2], mu[3]);
+                *(float4*)(a.st_sigma + o) = make_float4(sg[0], sg[1], sg[2], sg[3]);
+            } else {
+                for (int u = 0; u < 4 && k0 + u < a.A; ++u) {
+                    a.actions_out[o + u] = act[u];
+                    a.st_actions[o + u] = act[u];
+                    a.st_mu[o + u] = mu[u];
+                    a.st_sigma[o + u] = sg[u];
+                }
+            }
+        }
+        __syncthreads();
+        if (c == 0 && i < a.N) {
+            float logp = 0.f;
+            for (int k = 0; k < a.A; ++k) logp += terms[le][k];
+            a.st_logp[i] = logp;
+            a.st_value[i] = a.value[i];
+        }
+        __syncthreads();
+    }
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t no = (int64_t)a.N * a.O;
+    if ((no & 3) == 0 && (((uintptr_t)a.obs | (uintptr_t)a.st_obs) & 15) == 0) {
+        for (int64_t j = tid; j < no / 4; j += nth) ((float4*)a.st_obs)[j] = ((const float4*)a.obs)[j];
+    } else {
+        for (int64_t j = tid; j < no; j += nth) a.st_obs[j] = a.obs[j];
+    }
+    if (a.st_cobs) {
+        const int64_t nc = (int64_t)a.N * a.CO;
+        for (int64_t j = tid; j < nc; j += nth) a.st_cobs[j] = a.cobs[j];
+    }
+}
+
 // rewards[i] + gamma * (value[i] * time_out[i]) and dones into the storage row;
 // then the policy-noise draw counter advances (one thread, after k_act)
 __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ rew, const uint8_t* __restrict__ dones,
@@ -1532,9 +1603,15 @@ PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, co
         return fail(-1, "pmlp_act: null buffer or empty shape");
     ActArgs a{mu, stdv, value, obs, cobs, actions_out, st_actions, st_logp, st_mu, st_sigma, st_value, st_obs,
               st_cobs, draw, seed, N, A, O, CO};
-    const int64_t work = std::max<int64_t>(N, (int64_t)N * O / 4);
-    const int blocks = (int)std::min<int64_t>(1024, (work + 255) / 256);
-    hipLaunchKernelGGL(k_act, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (A <= 16) {
+        const int64_t work = std::max<int64_t>(4 * (int64_t)N, (int64_t)N * O / 4);
+        const int blocks = (int)std::min<int64_t>(1024, (work + 255) / 256);
+        hipLaunchKernelGGL(k_act4, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    } else {
+        const int64_t work = std::max<int64_t>(N, (int64_t)N * O / 4);
+        const int blocks = (int)std::min<int64_t>(1024, (work + 255) / 256);
+        hipLaunchKernelGGL(k_act, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    }
     PMLP_CHECK_LAUNCH("pmlp_act");
     return 0;
 }
