@@ -45,6 +45,27 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args):
+    """`bench.py --gpus N` (N > 1) outside a launcher: start N ranks of this script under
+    torch.distributed.run, one process per GPU, and exit with their status.  Runs before
+    anything touches the GPU (no HIP call in this parent process)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def setup_dist(args):
     import torch
     import torch.distributed as dist
@@ -165,8 +186,12 @@ def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     import torch
     world, rank, local = setup_dist(args)
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     import isaacgym  # noqa: F401
     from legged_gym.envs import task_registry  # noqa: F401
     from legged_gym.utils import get_args

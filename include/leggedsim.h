@@ -258,8 +258,24 @@ LGS_API int lgs_set_dof_state_indexed(lgs_sim* sim, const float* dof_src, const 
 /* task setup + the fused control step (LeggedRobot.step + post_physics_step) */
 LGS_API int lgs_set_task(lgs_sim* sim, const lgs_task_params* task);
 LGS_API int lgs_step(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* The two halves of lgs_step, for callers that act between them (a task's Python reward
+ * terms) and for parity tests that check each half on its own.  lgs_step is bit-for-bit
+ * lgs_step_physics followed by lgs_post_physics with the same step_counter.
+ *  - lgs_step_physics: clip actions (legged_robot.py:623-624), decimation x (_compute_torques
+ *    :649-671 + one substep :628-639), torques of the last substep, rigid_body_states for tasks
+ *    that read them (h1_env.py:49).  No post-physics, no extras, no step-counter advance.
+ *  - lgs_post_physics: post_physics_step (:673-709) + extras on the bound state, reading the
+ *    clipped actions from env->actions, the last substep's torques from env->torques and the
+ *    contact forces from the bound net_contact_forces; advances env->step_counter like lgs_step. */
+LGS_API int lgs_step_physics(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+LGS_API int lgs_post_physics(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(all) as used by BaseTask.reset (base_task.py:82-86) */
 LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* reset_idx(env_ids) (legged_robot.py:723-768) for an arbitrary subset: env_mask is a DEVICE
+ * byte per env (nonzero = reset).  Resets dofs/root/commands/buffers of those envs, sets their
+ * reset byte, and fills the extras like lgs_step (episode means over the reset envs, carried
+ * time-outs); the step counter is not advanced. */
+LGS_API int lgs_reset_idx(lgs_sim* sim, const lgs_env_buffers* env, const uint8_t* env_mask, int64_t step_counter);
 
 /* gym.add_heightfield -- the rough-terrain ground of legged_gym (utils/terrain.py builds
  * height_field_raw; the reference's create_sim only ever adds the plane, legged_robot.py:240-257).

@@ -154,6 +154,15 @@ PMLP_API int32_t pmlp_gae_parts(int32_t num_envs);
 PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
                       float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
                       double* partial, void* stream);
+/* The same in two halves for data-parallel training (rsl_rl v1.0.2 normalises with the
+ * statistics of the whole batch; across ranks that is the all-reduced moments):
+ * pmlp_gae_local writes returns/advantages and this rank's moments[3] = {sum, sum of
+ * squares, count} (doubles); the caller all-reduces moments (sum) and pmlp_adv_normalize
+ * normalises the n local advantages with the global mean and unbiased std. */
+PMLP_API int pmlp_gae_local(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                            float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
+                            double* partial, double* moments, void* stream);
+PMLP_API int pmlp_adv_normalize(float* advantages, int64_t n, const double* moments, void* stream);
 
 /* Rollout step of PPO (rsl_rl v1.0.2 PPO.act + RolloutStorage.add_transitions):
  * from the policy mean mu[N,A], std[A] and value[N] (the MLP outputs) draw

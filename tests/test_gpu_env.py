@@ -1,11 +1,7 @@
-"""HIP product path vs the CPU oracle, through the C ABI (the env calls lgs_step).
-
-Parity bar: the post-physics outputs (obs, rewards, resets, time-outs,
-commands, episode bookkeeping) within 1e-4 (fp32; SURVEY §7 / north star); the
-physics state within 1e-3.  One control step is compared from identical
-states; a contact that is within fp32 rounding of the 1 cm activation
-threshold can legitimately flip between the two implementations, so up to 1 %
-of envs may exceed the physics tolerance (never the reset/episode logic).
+"""The env through its Python API (LeggedRobot on the C ABI): reset/push/time-out
+semantics against the oracle, the VecEnv drop-in contract, the gymapi-style substep,
+long rollouts, and the PPO paths on top of it.  The step-level bitwise parity of
+the HIP kernel with the oracle (every robot, size and ground) is tests/test_gpu_parity.py.
 """
 import numpy as np
 import pytest
@@ -33,7 +29,7 @@ def make(task, n, **edits):
     return env
 
 
-def compare(env, ref, keys, atol, frac_ok=0.0):
+def compare(env, ref, keys, atol):
     n = env.num_envs
     got = {"root": env.root_states, "dofs": env.dof_state, "cforce": env._contact_forces, "obs": env.obs_buf,
            "priv_obs": env.privileged_obs_buf, "rew": env.rew_buf, "reset": env.reset_buf,
@@ -48,84 +44,9 @@ def compare(env, ref, keys, atol, frac_ok=0.0):
         if g.dtype == np.bool_:
             g = g.astype(np.uint8)
         bad = ~np.isclose(g.astype(np.float64), r.astype(np.float64), rtol=atol, atol=atol)
-        frac = bad.reshape(n, -1).any(axis=1).mean()
+        nbad = int(bad.reshape(n, -1).any(axis=1).sum())
         assert np.isfinite(g).all(), k
-        assert frac <= frac_ok, f"{k}: {frac:.2%} of envs outside {atol} (max |d| {np.abs(g - r).max():.3e})"
-
-
-@pytest.mark.parametrize("task", TASKS)
-def test_fused_step_matches_oracle(task):
-    env = make(task, 512)
-    env.reset()
-    g = torch.Generator(device="cuda").manual_seed(0)
-    for _ in range(30):
-        env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
-    for _ in range(3):
-        snap = bridge.snapshot(env)
-        a = 0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g)
-        ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
-        env.step(a)
-        torch.cuda.synchronize()
-        compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
-        compare(env, ref, ["obs", "rew", "commands", "feet_air_time", "last_contacts", "episode_sums"] +
-                (["priv_obs"] if env.num_privileged_obs else []), 1e-4, frac_ok=0.01)
-        compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=0.01)
-
-
-@pytest.mark.parametrize("task,n", [("go2", 1), ("go2", 37), ("h1_2", 65), ("go2", 4096), ("h1", 8192)])
-def test_step_matches_oracle_at_edge_and_full_sizes(task, n):
-    """Ragged env counts (1, 37, 65: partial waves of XCD-mapped workgroups) and the BASELINE
-    per-GPU sizes (Go2 4096, H1 8192): one fused step from identical states == the oracle."""
-    env = make(task, n)
-    env.reset()
-    g = torch.Generator(device="cuda").manual_seed(n)
-    for _ in range(8):
-        env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
-    snap = bridge.snapshot(env)
-    a = 0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g)
-    ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
-    env.step(a)
-    torch.cuda.synchronize()
-    compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
-    # the 1 % allowance for a contact flipping at the activation threshold, but at least one
-    # env for the ragged counts (65 envs: 1 % would allow none); reset logic stays exact
-    ok = 0.01 if n < 32 else max(0.01, 1.0 / n)
-    compare(env, ref, ["obs", "rew", "commands", "feet_air_time", "last_contacts", "episode_sums"] +
-            (["priv_obs"] if env.num_privileged_obs else []), 1e-4, frac_ok=ok)
-    compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=ok)
-
-
-@pytest.mark.parametrize("task", ["go2", "g1_rough"])
-def test_heightfield_step_matches_oracle(task):
-    """Rough terrain (lgs_set_heightfield: the utils/terrain.py curriculum map, envs on
-    its tiles): one fused control step vs the oracle on the same heightfield, with the
-    tile-origin resets (custom_origins xy jitter) included."""
-    env = make(task, 512, terrain__mesh_type="heightfield", terrain__num_rows=5, terrain__num_cols=8)
-    assert env.terrain is not None and env.custom_origins
-    env.reset()
-    g = torch.Generator(device="cuda").manual_seed(0)
-    for _ in range(30):
-        env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
-    for _ in range(3):
-        snap = bridge.snapshot(env)
-        a = 0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g)
-        ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
-        env.step(a)
-        torch.cuda.synchronize()
-        compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
-        compare(env, ref, ["obs", "rew", "commands", "feet_air_time", "last_contacts", "episode_sums"] +
-                (["priv_obs"] if env.num_privileged_obs else []), 1e-4, frac_ok=0.01)
-        compare(env, ref, ["root", "dofs", "torques", "rbs"], 1e-3, frac_ok=0.01)
-    # the robots stand on the terrain, not on z = 0: feet above the local ground
-    hs = env.cfg.terrain.horizontal_scale
-    b = env.cfg.terrain.border_size
-    root = env.root_states[:, :3]
-    hf = env.height_samples
-    i = ((root[:, 0] + b) / hs).long().clamp(0, hf.shape[0] - 1)
-    j = ((root[:, 1] + b) / hs).long().clamp(0, hf.shape[1] - 1)
-    ground = hf[i, j].float() * env.cfg.terrain.vertical_scale
-    assert float((root[:, 2] - ground).median()) > 0.1
-    bridge.set_ground(bridge.ensure_built())
+        assert nbad == 0, f"{k}: {nbad}/{n} envs outside {atol} (max |d| {np.abs(g - r).max():.3e})"
 
 
 @pytest.mark.parametrize("task", ["go2", "h1"])
@@ -143,10 +64,8 @@ def test_timeouts_reset_push_match_oracle_exactly(task):
     torch.cuda.synchronize()
     assert env.reset_buf.all() and env.time_out_buf.all()
     assert (env.episode_length_buf == 0).all()
-    compare(env, ref, ["reset", "time_out", "episode_length"], 0.0)
-    compare(env, ref, ["commands"], 1e-6)  # FMA contraction of (hi-lo)*u+lo on the GPU
-    compare(env, ref, ["root", "dofs", "episode_sums"], 1e-5)
-    compare(env, ref, ["obs"], 1e-4, frac_ok=0.01)
+    compare(env, ref, ["reset", "time_out", "episode_length", "commands", "root", "dofs", "episode_sums", "obs"],
+            0.0)  # bit-exact (tests/test_gpu_parity.py)
     q = env.dof_pos / env.default_dof_pos
     m = env.default_dof_pos.abs().expand_as(q) > 1e-6
     assert ((q[m] >= 0.5 - 1e-6) & (q[m] <= 1.5 + 1e-6)).all()
@@ -164,8 +83,8 @@ def test_timeouts_reset_push_match_oracle_exactly(task):
     acc = ref["episode_acc"]
     means = acc[:nsum] / max(float(acc[nsum]), 1.0) / env.max_episode_length_s
     got = torch.stack([ep["rew_" + k] for k in env._sum_names]).cpu().numpy()
-    # the step's reward terms inherit the physics tolerance (dof_acc/torque terms)
-    np.testing.assert_allclose(got, means, rtol=2e-2, atol=1e-5)
+    # float atomics over the reset envs: the sum order is not fixed
+    np.testing.assert_allclose(got, means, rtol=1e-5, atol=1e-8)
     assert float(env._episode_acc.abs().sum()) == 0.0  # zeroed for the next step
 
 
@@ -214,8 +133,8 @@ def test_gymapi_style_substep_matches_oracle():
     p = lambda a: a.ctypes.data  # noqa: E731
     lib.orc_simulate(C.byref(mh.desc), C.byref(env._lgs_params), 128, p(root), p(dofs), p(t), p(cf), p(rbs),
                      p(snap["added_mass"]), p(snap["friction"]))
-    np.testing.assert_allclose(env.root_states.cpu().numpy(), root, rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(env.dof_state.cpu().numpy(), dofs, rtol=1e-3, atol=1e-3)
+    np.testing.assert_array_equal(env.root_states.cpu().numpy(), root)  # bit-exact
+    np.testing.assert_array_equal(env.dof_state.cpu().numpy(), dofs)
 
 
 @pytest.mark.parametrize("task", TASKS)

@@ -25,6 +25,7 @@
 #include <string>
 
 #include "../../include/leggedsim.h"
+#include "lgs_detmath.h"
 
 // Diagnostic build only (-DLGS_PHASE_STAMPS): lane 0 accumulates s_memtime
 // deltas per phase into a global [N][LGS_NPHASE] buffer.  Never in the real build.
@@ -174,7 +175,7 @@ __device__ __forceinline__ void mat_to_quat(const float* R, float* q) {
 }
 __device__ __forceinline__ void axis_angle(const float* a, float ang, float* R) {
     float s, c;
-    sincosf(ang, &s, &c);
+    lgs_sincosf(ang, &s, &c);  // deterministic: the oracle's bits (lgs_detmath.h)
     float t = 1.f - c;
     float x = a[0], y = a[1], z = a[2];
     R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
@@ -1032,8 +1033,10 @@ __device__ void body_states(Smem<D, B, ROWS>& s, float* rbs_out) {
         const float O[3] = {p[0], p[1], p[2]};
         float c0[3];
         matvec(R, mc.com[0], c0);
+        // the root COM offset as (O + R c) - O, the oracle's (and substep()'s) arithmetic
+        float rc[3] = {(O[0] + c0[0]) - O[0], (O[1] + c0[1]) - O[1], (O[2] + c0[2]) - O[2]};
         float w[3] = {s.root[10], s.root[11], s.root[12]}, t[3];
-        cross3(w, c0, t);
+        cross3(w, rc, t);
         float Vw[3] = {w[0], w[1], w[2]};
         float Vv[3] = {s.root[7] - t[0], s.root[8] - t[1], s.root[9] - t[2]};
         const int d = mc.depth[lane];
@@ -1209,11 +1212,11 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
         r = sum; break;
     case LGS_REW_TRACKING_LIN_VEL: {
         float e0 = cmd[0] - bl[0], e1 = cmd[1] - bl[1];
-        r = expf(-(e0 * e0 + e1 * e1) / T.tracking_sigma);
+        r = lgs_expf(-(e0 * e0 + e1 * e1) / T.tracking_sigma);
     } break;
     case LGS_REW_TRACKING_ANG_VEL: {
         float d = cmd[2] - ba[2];
-        r = expf(-(d * d) / T.tracking_sigma);
+        r = lgs_expf(-(d * d) / T.tracking_sigma);
     } break;
     case LGS_REW_FEET_AIR_TIME: {
         int filt[LGS_MAX_FEET];
@@ -1300,12 +1303,12 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
             float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
             float sinr = 2.0f * (qw * qx + qy * qz);
             float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
-            rpy[0] = atan2f(sinr, cosr);
+            rpy[0] = lgs_atan2f(sinr, cosr);
             float sinp = 2.0f * (qw * qy - qz * qx);
-            rpy[1] = fabsf(sinp) >= 1.f ? copysignf(3.14159265358979323846f / 2.0f, sinp) : asinf(sinp);
+            rpy[1] = fabsf(sinp) >= 1.f ? copysignf(3.14159265358979323846f / 2.0f, sinp) : lgs_asinf(sinp);
             float siny = 2.0f * (qw * qz + qx * qy);
             float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
-            rpy[2] = atan2f(siny, cosy);
+            rpy[2] = lgs_atan2f(siny, cosy);
         }
         float phase = 0.f, leg_phase[2] = {0.f, 0.f};
         if (T.obs_layout == LGS_OBS_HUMANOID) {
@@ -1325,7 +1328,7 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
             cross3(q, t, u);
             float fwd0 = fx[0] + q[3] * t[0] + u[0];
             float fwd1 = fx[1] + q[3] * t[1] + u[1];
-            float heading = atan2f(fwd1, fwd0);
+            float heading = lgs_atan2f(fwd1, fwd0);
             const float tp = 2.0f * 3.14159265358979323846f;
             float wv = fmod_pos(cmd[3] - heading, tp);
             if (wv > 3.14159265358979323846f) wv -= tp;
@@ -1379,12 +1382,18 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
     }
 }
 
+// reset modes of post_physics: the control step (reset decided by check_termination),
+// BaseTask.reset (every env, no episode extras), reset_idx(env_ids) (the masked envs:
+// episode sums into the extras accumulator, reset_buf set, legged_robot.py:723-768)
+enum { RESET_STEP = 0, RESET_ALL = 1, RESET_IDS = 2 };
+
 template <int D, int B, int ROWS>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
-                             const float* rbs, int N, int e, uint32_t step, bool force_reset) {
+                             const float* rbs, int N, int e, uint32_t step, int reset_mode) {
     const int lane = threadIdx.x;
     const int A = T.num_actions;
     const uint64_t seed = T.seed;
+    const bool force_reset = reset_mode != RESET_STEP;
     if (!force_reset) {
         post_physics_scalar(s, T, E, rbs, N, e, step);
     } else {
@@ -1414,7 +1423,8 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         }
         __syncthreads();
         if (lane < 6) s.root[7 + lane] = rv;
-        if (!force_reset) {
+        if (reset_mode == RESET_IDS && lane == 0) E.reset[e] = 1;  // reset_buf[env_ids] = 1 (:758)
+        if (reset_mode != RESET_ALL) {
             const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
             if (lane < nsum) {
                 atomicAdd(E.episode_acc + lane, E.episode_sums[(size_t)lane * N + e]);
@@ -1454,8 +1464,10 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         for (int j = 0; j < A; ++j) tmp[k++] = act[j];
         if (T.obs_layout == LGS_OBS_HUMANOID) {
             float ph = 2.0f * 3.14159265358979323846f * s.u.post.misc[9];
-            tmp[k++] = sinf(ph);
-            tmp[k++] = cosf(ph);
+            float sp_, cp_;
+            lgs_sincosf(ph, &sp_, &cp_);
+            tmp[k++] = sp_;
+            tmp[k++] = cp_;
         }
     }
     __syncthreads();
@@ -1475,9 +1487,15 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     if (lane < 6) E.last_root_vel[6 * e + lane] = s.root[7 + lane];
 }
 
+// k_step modes: the fused control step (lgs_step), or its two halves -- the physics
+// (clip, decimation x (PD + substep), torques, body states: lgs_step_physics) and the
+// post-physics stack on the bound state (lgs_post_physics).  STEP == PHYSICS then POST,
+// bit for bit: the post half reads back exactly what the physics half stored.
+enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2 };
+
 template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? LGS_WAVES_PER_EU : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
-                                               lgs_env_buffers E, int N, uint32_t step) {
+                                               lgs_env_buffers E, int N, uint32_t step, int mode) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
@@ -1487,38 +1505,44 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     load_model(s, md);
     load_state(s, st, e);
     const int A = T.num_actions;
-    float a = 0.f;
-    if (lane < A) {
-        const float* ain = E.actions_in ? E.actions_in : E.actions;
-        a = clipf(ain[A * e + lane], -T.clip_actions, T.clip_actions);  // :623-624
-        E.actions[A * e + lane] = a;
-        s.act[lane] = a;
-    }
-    const float lqd = (lane < D) ? E.last_dof_vel[D * e + lane] : 0.f;
-    const float am = st.added_mass ? st.added_mass[e] : 0.f;
-    const float mu = st.friction ? st.friction[e] : 1.f;
-    STAMP_INIT();
-    __syncthreads();
-    for (int it = 0; it < T.decimation; ++it) {  // :627-639
-        if (lane < D) {  // _compute_torques :649-671
-            const float as = a * T.action_scale;
-            const float q = s.q[lane], qd = s.qd[lane];
-            float t;
-            if (T.control_type == 0) t = T.p_gains[lane] * (as + T.default_dof_pos[lane] - q) - T.d_gains[lane] * qd;
-            else if (T.control_type == 1) t = T.p_gains[lane] * (as - qd) - T.d_gains[lane] * (qd - lqd) / sp.dt;
-            else t = as;
-            s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
-        }
-        __syncthreads();
-        substep<D, B, ROWS, CH>(s, md, sp, am, mu);
-    }
-    STAMP(0);
-    if (lane < D) E.torques[D * e + lane] = s.tau[lane];
     float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * B * e : nullptr;
-    if (rbs) body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
+    STAMP_INIT();
+    if (mode != MODE_POST) {
+        float a = 0.f;
+        if (lane < A) {
+            const float* ain = E.actions_in ? E.actions_in : E.actions;
+            a = clipf(ain[A * e + lane], -T.clip_actions, T.clip_actions);  // :623-624
+            E.actions[A * e + lane] = a;
+            s.act[lane] = a;
+        }
+        const float lqd = (lane < D) ? E.last_dof_vel[D * e + lane] : 0.f;
+        const float am = st.added_mass ? st.added_mass[e] : 0.f;
+        const float mu = st.friction ? st.friction[e] : 1.f;
+        __syncthreads();
+        for (int it = 0; it < T.decimation; ++it) {  // :627-639
+            if (lane < D) {  // _compute_torques :649-671
+                const float as = a * T.action_scale;
+                const float q = s.q[lane], qd = s.qd[lane];
+                float t;
+                if (T.control_type == 0) t = T.p_gains[lane] * (as + T.default_dof_pos[lane] - q) - T.d_gains[lane] * qd;
+                else if (T.control_type == 1) t = T.p_gains[lane] * (as - qd) - T.d_gains[lane] * (qd - lqd) / sp.dt;
+                else t = as;
+                s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
+            }
+            __syncthreads();
+            substep<D, B, ROWS, CH>(s, md, sp, am, mu);
+        }
+        STAMP(0);
+        if (lane < D) E.torques[D * e + lane] = s.tau[lane];
+        if (rbs) body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
+    } else {  // the physics half's outputs, as it stored them
+        if (lane < A) s.act[lane] = E.actions[A * e + lane];
+        if (lane < D) s.tau[lane] = E.torques[D * e + lane];
+        for (int i = lane; i < 3 * B; i += WAVE) (&s.cf[0][0])[i] = st.cforce[(size_t)3 * B * e + i];
+    }
     __syncthreads();
     STAMP(15);
-    post_physics(s, T, E, rbs, N, e, step, false);
+    if (mode != MODE_PHYSICS) post_physics(s, T, E, rbs, N, e, step, RESET_STEP);
     __syncthreads();
     STAMP(16);
     store_state(s, st, e);
@@ -1526,18 +1550,20 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     STAMP_FLUSH(e);
 }
 
+// reset_idx: every env (mask == NULL, BaseTask.reset) or the envs whose mask byte is set
 template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
-                                                    lgs_env_buffers E, int N, uint32_t step) {
+                                                    lgs_env_buffers E, int N, uint32_t step, const uint8_t* mask) {
     __shared__ Smem<D, B, ROWS> s;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
+    if (mask && !mask[e]) return;
     if (E.step_counter) step = (uint32_t)*E.step_counter;
     load_model(s, md);
     load_state(s, st, e);
     if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
     __syncthreads();
-    post_physics(s, *Tp, E, nullptr, N, e, step, true);
+    post_physics(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
     __syncthreads();
     store_state(s, st, e);
     if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
@@ -1548,7 +1574,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
 // carried time-out flags — then episode_acc zeroed for the next step and the
 // device step counter advanced (the Philox key of graph-replayed steps).
 __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
-                                                      int N) {
+                                                      int N, int advance) {
     const lgs_task_params& T = *Tp;
     const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
     const float cnt = E.episode_acc[nsum];
@@ -1564,7 +1590,7 @@ __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const l
         for (int e = t; e < N; e += blockDim.x) E.time_outs_carry[e] = E.time_out[e];
     __syncthreads();
     if (t <= nsum) E.episode_acc[t] = 0.f;
-    if (t == 0 && E.step_counter) *E.step_counter += 1;
+    if (t == 0 && E.step_counter && advance) *E.step_counter += 1;
 }
 
 __global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, int n, int width) {
@@ -1872,22 +1898,48 @@ LGS_API int lgs_set_task(lgs_sim* s, const lgs_task_params* t) {
     return LGS_OK;
 }
 
-LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
-    if (!s || !env) return set_err(LGS_ERR_ARG, "null argument");
-    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_step: state not bound or task not set");
+static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter, int mode, const char* what) {
+    if (!s || !env) return set_err(LGS_ERR_ARG, std::string(what) + ": null argument");
+    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, std::string(what) + ": state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
+    LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N);
-    HIP_TRY(hipGetLastError());
+    if (mode != MODE_PHYSICS) {  // extras of the step's resets, episode_acc zeroed, step counter advanced
+        hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1);
+        HIP_TRY(hipGetLastError());
+    }
     return LGS_OK;
+}
+
+LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_STEP, "lgs_step");
+}
+
+LGS_API int lgs_step_physics(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_PHYSICS, "lgs_step_physics");
+}
+
+LGS_API int lgs_post_physics(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_POST, "lgs_post_physics");
 }
 
 LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
     if (!s || !env) return set_err(LGS_ERR_ARG, "null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_reset_all: state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter);
+    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, (const uint8_t*)nullptr);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t* env_mask, int64_t step_counter) {
+    if (!s || !env || !env_mask) return set_err(LGS_ERR_ARG, "lgs_reset_idx: null argument");
+    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_reset_idx: state not bound or task not set");
+    DevState st = state_of(s);
+    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, env_mask);
+    HIP_TRY(hipGetLastError());
+    // extras["episode"] over the reset envs and extras["time_outs"]; no step-counter advance
+    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0);
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }

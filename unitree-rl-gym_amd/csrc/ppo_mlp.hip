@@ -1018,22 +1018,31 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_gae(const float* __restric
     }
 }
 
-// adv = (adv - mean) / (std + 1e-8), unbiased std over all T*N advantages
+// adv = (adv - mean) / (std + 1e-8), unbiased std over all T*N advantages.  gstats
+// (data-parallel): the all-reduced {sum, sum of squares, count} of every rank's
+// advantages replace this rank's partials, so each rank normalises by the global moments.
 __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adv_norm(float* __restrict__ adv, int64_t n,
-                                                               const double* __restrict__ partial, int nparts) {
-    __shared__ double sh[2];
+                                                               const double* __restrict__ partial, int nparts,
+                                                               const double* __restrict__ gstats) {
+    __shared__ double sh[3];
     if (threadIdx.x == 0) {
-        double a = 0.0, b = 0.0;
-        for (int i = 0; i < nparts; ++i) {
-            a += partial[2 * i];
-            b += partial[2 * i + 1];
+        double a = 0.0, b = 0.0, c = (double)n;
+        if (gstats) {
+            a = gstats[0]; b = gstats[1]; c = gstats[2];
+        } else {
+            for (int i = 0; i < nparts; ++i) {
+                a += partial[2 * i];
+                b += partial[2 * i + 1];
+            }
         }
         sh[0] = a;
         sh[1] = b;
+        sh[2] = c;
     }
     __syncthreads();
-    const double mean = sh[0] / (double)n;
-    const double var = (sh[1] - (double)n * mean * mean) / (double)(n - 1);
+    const double cnt = sh[2];
+    const double mean = sh[0] / cnt;
+    const double var = (sh[1] - cnt * mean * mean) / (cnt - 1.0);
     const float meanf = (float)mean, den = (float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f;
     for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * PMLP_OPT_THREADS)
@@ -1589,8 +1598,45 @@ PMLP_API int pmlp_gae(const float* rewards, const uint8_t* dones, const float* v
     const int64_t n = (int64_t)T * N;
     const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
     hipLaunchKernelGGL(k_adv_norm, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, advantages, n,
-                       partial, nb);
+                       partial, nb, (const double*)nullptr);
     PMLP_CHECK_LAUNCH("pmlp_gae");
+    return 0;
+}
+
+// this rank's {sum, sum of squares, count} of the advantages from the GAE partials
+__global__ void k_gae_moments(const double* __restrict__ partial, int nparts, int64_t n, double* __restrict__ out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int i = 0; i < nparts; ++i) {
+            a += partial[2 * i];
+            b += partial[2 * i + 1];
+        }
+        out[0] = a;
+        out[1] = b;
+        out[2] = (double)n;
+    }
+}
+
+PMLP_API int pmlp_gae_local(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                            float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam,
+                            double* partial, double* moments, void* stream) {
+    if (!rewards || !dones || !values || !last_values || !returns || !advantages || !partial || !moments || T <= 0 ||
+        N <= 0)
+        return fail(-1, "pmlp_gae_local: null buffer or empty rollout");
+    const int nb = pmlp_gae_parts(N);
+    hipLaunchKernelGGL(k_gae, dim3(nb), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, rewards, dones, values,
+                       last_values, returns, advantages, T, N, gamma, lam, partial);
+    hipLaunchKernelGGL(k_gae_moments, dim3(1), dim3(64), 0, (hipStream_t)stream, partial, nb, (int64_t)T * N, moments);
+    PMLP_CHECK_LAUNCH("pmlp_gae_local");
+    return 0;
+}
+
+PMLP_API int pmlp_adv_normalize(float* advantages, int64_t n, const double* moments, void* stream) {
+    if (!advantages || !moments || n <= 0) return fail(-1, "pmlp_adv_normalize: null buffer or empty");
+    const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    hipLaunchKernelGGL(k_adv_norm, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, advantages, n,
+                       (const double*)nullptr, 0, moments);
+    PMLP_CHECK_LAUNCH("pmlp_adv_normalize");
     return 0;
 }
 

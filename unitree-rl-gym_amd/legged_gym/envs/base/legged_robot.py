@@ -357,17 +357,22 @@ class LeggedRobot(BaseTask):
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
     def reset_idx(self, env_ids):
-        """Reset the given envs.  The native kernel resets every env of the batch
-        (BaseTask.reset's use); arbitrary subsets go through reset_buf masks in step()."""
+        """reset_idx (legged_robot.py:723-768) for any subset of envs: one masked launch
+        (lgs_reset_idx) resets dofs, root states and commands, zeroes the actions and
+        buffers, sets reset_buf[env_ids] = 1 and fills extras["episode"] (means of the
+        reset envs' episode sums / episode_length_s) and extras["time_outs"]."""
         if len(env_ids) == 0:
             return
-        if len(env_ids) != self.num_envs:
-            raise NotImplementedError("reset_idx of a subset: resets happen inside step() from reset_buf")
         self._sync_stream()
-        self.sim.reset_all(self._env_structs[self._buf_idx], self.common_step_counter)
-        self.extras["episode"] = {"rew_" + k: self._ep_means[i].clone() for i, k in enumerate(self._sum_names)}
+        ids = torch.as_tensor(env_ids, device=self.device).long().view(-1)
+        mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        mask[ids] = 1
+        E = self._env_structs[self._buf_idx]
+        snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
+        E.ep_snapshot = snap.data_ptr()
+        self.sim.reset_idx(E, mask, self.common_step_counter)
+        self.extras["episode"] = {"rew_" + k: snap[i] for i, k in enumerate(self._sum_names)}
         if self.cfg.env.send_timeouts:
-            self._time_outs.copy_(self.time_out_buf)
             self.extras["time_outs"] = self._time_outs
 
     def post_physics_step(self):

@@ -194,6 +194,10 @@ def load_oracle():
     lib.orc_simulate.argtypes = [C.POINTER(ModelDesc), C.POINTER(SimParams), C.c_int, vp, vp, vp, vp, vp, vp, vp]
     lib.orc_step.argtypes = [C.POINTER(ModelDesc), C.POINTER(SimParams), C.POINTER(TaskParams), C.c_int,
                              vp, vp, vp, vp, vp, vp, C.POINTER(EnvBuffers), C.c_int64]
+    lib.orc_step_physics.argtypes = [C.POINTER(ModelDesc), C.POINTER(SimParams), C.POINTER(TaskParams), C.c_int,
+                                     vp, vp, vp, vp, vp, vp, C.POINTER(EnvBuffers)]
+    lib.orc_reset_idx.argtypes = [C.POINTER(ModelDesc), C.POINTER(TaskParams), C.c_int, vp, vp,
+                                  C.POINTER(EnvBuffers), vp, C.c_int64]
     lib.orc_post_physics.argtypes = [C.POINTER(ModelDesc), C.POINTER(TaskParams), C.c_int, vp, vp, vp, vp,
                                      C.POINTER(EnvBuffers), C.c_int64]
     lib.orc_compute_torques.argtypes = [C.POINTER(TaskParams), C.c_int, C.c_int, vp, vp, vp, C.c_float, vp]

@@ -62,12 +62,16 @@ def load():
     lib.lgs_set_task.argtypes = [vp, C.POINTER(cabi.TaskParams)]
     lib.lgs_step.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_reset_all.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_step_physics.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_post_physics.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_reset_idx.argtypes = [vp, C.POINTER(cabi.EnvBuffers), vp, C.c_int64]
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
                  "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
-                 "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield"):
+                 "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield",
+                 "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx"):
         getattr(lib, name).restype = C.c_int
     _LIB = lib
     return lib
@@ -83,6 +87,7 @@ EXPORTED_SYMBOLS = [
     "lgs_set_env_properties", "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
+    "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx",
 ]
 
 
@@ -137,6 +142,17 @@ class Sim:
 
     def step(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_step(self.handle, C.byref(env_bufs), step_counter), "lgs_step")
+
+    def step_physics(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_step_physics(self.handle, C.byref(env_bufs), step_counter), "lgs_step_physics")
+
+    def post_physics(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_post_physics(self.handle, C.byref(env_bufs), step_counter), "lgs_post_physics")
+
+    def reset_idx(self, env_bufs: cabi.EnvBuffers, mask_u8, step_counter: int):
+        assert mask_u8.is_cuda and mask_u8.numel() == self.num_envs and mask_u8.element_size() == 1
+        check(self.lib, self.lib.lgs_reset_idx(self.handle, C.byref(env_bufs), mask_u8.data_ptr(), step_counter),
+              "lgs_reset_idx")
 
     def reset_all(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_reset_all(self.handle, C.byref(env_bufs), step_counter), "lgs_reset_all")

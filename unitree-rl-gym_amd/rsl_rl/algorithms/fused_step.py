@@ -387,16 +387,28 @@ class FusedRollout:
                                                                          ok(time_outs, torch.bool))
 
 
-def gae(storage, last_values, gamma, lam):
+def gae(storage, last_values, gamma, lam, world_size=1):
     """RolloutStorage.compute_returns on the GPU in two launches (pmlp_gae): GAE
-    backwards over T per env, then advantage normalisation."""
+    backwards over T per env, then advantage normalisation.  world_size > 1: the
+    normalisation uses the moments of every rank's advantages (one fp64 all-reduce of
+    {sum, sum of squares, count} between the two halves), i.e. the whole batch's, as a
+    single-GPU run over all ranks' envs would."""
     lib = mm.load()
     T, N = storage.num_transitions_per_env, storage.num_envs
     key = (T, N)
     if getattr(storage, "_gae_partial_key", None) != key:
         storage._gae_partial = torch.empty(2 * lib.pmlp_gae_parts(N), dtype=torch.float64, device=storage.device)
+        storage._gae_moments = torch.empty(3, dtype=torch.float64, device=storage.device)
         storage._gae_partial_key = key
     lv = last_values.reshape(N).contiguous()
-    mm._ok(lib.pmlp_gae(mm._p(storage.rewards), mm._p(storage.dones), mm._p(storage.values), mm._p(lv),
-                        mm._p(storage.returns), mm._p(storage.advantages), T, N, float(gamma), float(lam),
-                        mm._p(storage._gae_partial), mm._stream()), "pmlp_gae")
+    if world_size == 1:
+        mm._ok(lib.pmlp_gae(mm._p(storage.rewards), mm._p(storage.dones), mm._p(storage.values), mm._p(lv),
+                            mm._p(storage.returns), mm._p(storage.advantages), T, N, float(gamma), float(lam),
+                            mm._p(storage._gae_partial), mm._stream()), "pmlp_gae")
+        return
+    mom = storage._gae_moments
+    mm._ok(lib.pmlp_gae_local(mm._p(storage.rewards), mm._p(storage.dones), mm._p(storage.values), mm._p(lv),
+                              mm._p(storage.returns), mm._p(storage.advantages), T, N, float(gamma), float(lam),
+                              mm._p(storage._gae_partial), mm._p(mom), mm._stream()), "pmlp_gae_local")
+    dist.all_reduce(mom)
+    mm._ok(lib.pmlp_adv_normalize(mm._p(storage.advantages), T * N, mm._p(mom), mm._stream()), "pmlp_adv_normalize")

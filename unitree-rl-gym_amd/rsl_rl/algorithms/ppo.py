@@ -174,8 +174,8 @@ class PPO:
 
     def compute_returns(self, last_critic_obs):
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
-        if self._fused is not None and self.world_size == 1:  # GAE + normalisation: two launches
-            fused_step.gae(self.storage, last_values, self.gamma, self.lam)
+        if self._fused is not None:  # GAE + normalisation: two launches (+ a moments all-reduce)
+            fused_step.gae(self.storage, last_values, self.gamma, self.lam, self.world_size)
             return
         stats = self._global_adv_stats if self.world_size > 1 else None
         self.storage.compute_returns(last_values, self.gamma, self.lam, adv_stats=stats)

@@ -86,6 +86,8 @@ def load():
         L.pmlp_gae_parts.argtypes = [i32]
         L.pmlp_gae_parts.restype = i32
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
+        L.pmlp_gae_local.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp, vp]
+        L.pmlp_adv_normalize.argtypes = [vp, i64, vp, vp]
         L.pmlp_mlp4_forward.argtypes = [i32, C.POINTER(Mlp4Job), i32, i32, i32, i32, vp]
         L.pmlp_ppo_loss_step_parts.argtypes = [i32, i32]
         L.pmlp_ppo_loss_step_parts.restype = i32
