@@ -126,18 +126,38 @@ def load_sq_valu(kernel_ms):
             "valu_insts_per_launch": sq["valu_insts_per_launch"], "share_of_wave_time": sq.get("share_of_wave_time")}
 
 
-def cpu_baseline(env, seconds):
-    """The CPU oracle (oracle/lgs_oracle.c, OpenMP over envs) on the same Go2 workload."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_rate(env, bridge, lib, n_envs, seconds, threads):
+    """env-steps/s of the oracle's fused step (PD + substeps + post-physics) over n_envs
+    copies of the env's state, with `threads` OpenMP threads."""
+    import ctypes
     import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import bridge
-    lib = bridge.ensure_built()
+    gomp = ctypes.CDLL("libgomp.so.1")
+    gomp.omp_set_num_threads(int(threads))
     snap = bridge.snapshot(env)
-    n_envs = env.num_envs
+    reps = -(-n_envs // env.num_envs)
+    b = {}
+    for k, v in snap.items():
+        if v is None:
+            b[k] = None
+        elif k in ("episode_sums",):
+            b[k] = np.ascontiguousarray(np.tile(v, (1, reps))[:, :n_envs])
+        elif k in ("episode_acc",):
+            b[k] = v.copy()
+        else:
+            rows = v.reshape(env.num_envs, -1)
+            b[k] = np.ascontiguousarray(np.tile(rows, (reps, 1))[:n_envs].reshape((-1,) + v.shape[1:]))
     rng = np.random.default_rng(0)
     acts = [rng.normal(0, 0.5, (n_envs, env.num_actions)).astype(np.float32) for _ in range(4)]
-    b = {k: (None if v is None else v.copy()) for k, v in snap.items()}
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     steps, t0 = 0, time.time()
     while True:
         b["actions"][:] = acts[steps % 4]
@@ -147,9 +167,104 @@ def cpu_baseline(env, seconds):
         el = time.time() - t0
         if el >= seconds and steps >= 2:
             break
-    return {"value": n_envs * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"Go2 {n_envs} envs x {steps} fused control steps (PD + 4 physics substeps + post-physics), "
-                      f"oracle/lgs_oracle.c with OpenMP over envs, no policy; {el:.1f} s"}
+    return n_envs * steps / el, steps, el
+
+
+def _cpu_ppo_iter_s(num_envs, obs_dim, num_actions, threads, env_step_rate, sample_steps=2):
+    """PPO iteration on the host: 24 x (policy inference on CPU torch + the oracle env step
+    at env_step_rate) + the update (5 epochs x 4 mini-batches; `sample_steps` optimizer steps
+    timed and scaled to the 20).  Go2 MLP actor-critic 512-256-128, fp32 CPU torch."""
+    import torch
+    from rsl_rl.modules import ActorCritic
+    torch.set_num_threads(int(threads))
+    T, epochs, mbs = 24, 5, 4
+    ac = ActorCritic(obs_dim, obs_dim, num_actions, [512, 256, 128], [512, 256, 128], mixed_precision=False)
+    opt = torch.optim.Adam(ac.parameters(), lr=1e-3)
+    obs = torch.randn(num_envs, obs_dim)
+    with torch.no_grad():
+        ac.act_and_value(obs, obs)
+        t0 = time.time()
+        for _ in range(T):
+            ac.act_and_value(obs, obs)
+        infer = time.time() - t0
+    rows = num_envs * T // mbs
+    xb = torch.randn(rows, obs_dim)
+    ab = torch.randn(rows, num_actions)
+    t0 = time.time()
+    for _ in range(sample_steps):
+        ac.update_distribution(xb)
+        loss = -ac.get_actions_log_prob(ab).mean() + ac.evaluate(xb).pow(2).mean()
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(ac.parameters(), 1.0)
+        opt.step()
+    upd = (time.time() - t0) / sample_steps * epochs * mbs
+    return T * num_envs / env_step_rate + infer + upd, infer, upd
+
+
+def cpu_baseline(env, seconds):
+    """The CPU oracle (oracle/lgs_oracle.c, OpenMP over envs) on the same Go2 workload, plus
+    the policy and the PPO update on CPU torch: Go2 4096 and 4 envs,
+    all host threads of this job and 1 thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bridge
+    lib = bridge.ensure_built()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    n = env.num_envs
+    half = max(2.0, seconds / 4)
+    rate_all, st_all, el_all = _oracle_rate(env, bridge, lib, n, half, threads)
+    rate_one, st_one, el_one = _oracle_rate(env, bridge, lib, n, half, 1)
+    rate4_all, _, _ = _oracle_rate(env, bridge, lib, 4, 1.0, threads)
+    rate4_one, _, _ = _oracle_rate(env, bridge, lib, 4, 1.0, 1)
+    it_all, inf_all, upd_all = _cpu_ppo_iter_s(n, env.num_obs, env.num_actions, threads, rate_all)
+    it4, _, _ = _cpu_ppo_iter_s(4, env.num_obs, env.num_actions, threads, rate4_all, sample_steps=5)
+    import torch
+    torch.set_num_threads(threads)
+    return {"value": round(24 * n / it_all, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": (f"Go2 {n} envs: oracle fused step (PD + 4 substeps + post-physics) {st_all} steps in "
+                       f"{el_all:.1f} s on {threads} threads; PPO iteration = 24 x (oracle step + CPU torch "
+                       f"MLP policy) + update (2 optimizer steps of 24,576 rows timed, scaled to 5 x 4)"),
+            "ppo_iter_ms": round(it_all * 1e3, 1),
+            "ppo_iter_breakdown_ms": {"env": round(24 * n / rate_all * 1e3, 1), "inference": round(inf_all * 1e3, 1),
+                                      "update": round(upd_all * 1e3, 1)},
+            "env_only_env_steps_per_s": round(rate_all, 1),
+            "env_only_env_steps_per_s_1_thread": round(rate_one, 1),
+            "go2_4_envs": {"env_only_env_steps_per_s": round(rate4_all, 1),
+                           "env_only_env_steps_per_s_1_thread": round(rate4_one, 1),
+                           "ppo_iter_ms": round(it4 * 1e3, 2)},
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count(),
+            "build": "gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (oracle/Makefile; the .so is built "
+                     "in the container and travels to the GPU box)"}
+
+
+def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
+    """PPO iterations (OnPolicyRunner.learn: captured rollout + GAE + captured update) of
+    another BASELINE config with its own policy (G1 / H1 / H1_2: ActorCriticRecurrent,
+    LSTM 64, on the HIP sequence kernels): ms per iteration and env-steps/s."""
+    import torch
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    gargs = get_args(["--task", task, "--num_envs", str(n), "--headless", "--sim_device", dev, "--rl_device", dev])
+    with contextlib.redirect_stdout(sys.stderr):
+        env, env_cfg = task_registry.make_env(name=task, args=gargs)
+        _, train_cfg = task_registry.get_cfgs(task)
+        runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device=dev)
+        runner.learn(num_learning_iterations=warmup, init_at_random_ep_len=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.time()
+    with contextlib.redirect_stdout(sys.stderr):
+        runner.learn(num_learning_iterations=iters)
+    torch.cuda.synchronize(dev)
+    el = time.time() - t0
+    T = runner.num_steps_per_env
+    out = {"num_envs": n, "policy": runner.cfg["policy_class_name"], "decimation": env_cfg.control.decimation,
+           "ppo_iter_ms": round(el / iters * 1e3, 3), "env_steps_per_s": round(n * T * iters / el, 1),
+           "rollout_graph": runner._rollout_graph is not None,
+           "update_graph": getattr(runner.alg, "_graph", None) is not None,
+           "domain_rand": bool(env_cfg.domain_rand.randomize_friction or env_cfg.domain_rand.randomize_base_mass),
+           "terrain": env_cfg.terrain.mesh_type, "iters_timed": iters}
+    env.close()
+    return out
 
 
 def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
@@ -292,13 +407,20 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms)},
     }
     if world == 1 and not args.no_other_configs:
-        # the other BASELINE configs' env step on this GPU (their multi-GPU/LSTM PPO legs are
-        # not this line's metric): G1 rough heightfield 4096, H1 8192, H1_2 8192 (+DR)
+        # the other BASELINE configs on this GPU (not this line's metric): G1 rough heightfield
+        # 4096, H1 8192, H1_2 8192 (+DR, decimation 8) -- the fused env step alone, and the
+        # whole PPO iteration with their recurrent (LSTM) policies
         line["other_configs_env_only"] = {
             "g1_rough_heightfield_4096": env_kernel_rate("g1_rough", 4096, dev, 50, get_args, task_registry),
             "h1_8192": env_kernel_rate("h1", 8192, dev, 50, get_args, task_registry),
             "h1_2_8192": env_kernel_rate("h1_2", 8192, dev, 50, get_args, task_registry),
         }
+        line["other_configs_ppo_iter"] = {
+            "g1_rough_heightfield_4096": ppo_iter_rate("g1_rough", 4096, dev, 3, 2, get_args, task_registry),
+            "h1_8192": ppo_iter_rate("h1", 8192, dev, 3, 2, get_args, task_registry),
+            "h1_2_8192": ppo_iter_rate("h1_2", 8192, dev, 3, 2, get_args, task_registry),
+        }
+        line["h1_2_8192_ppo_iter_ms"] = line["other_configs_ppo_iter"]["h1_2_8192"]["ppo_iter_ms"]
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(env, args.cpu_seconds)
     print(json.dumps(line), flush=True)

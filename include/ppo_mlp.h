@@ -213,4 +213,24 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
                                 float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
                                 pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
 
+/* ---- recurrent memory: rsl_rl v1.0.2 Memory (one-layer LSTM, gate order i, f, g, o)
+ * for ActorCriticRecurrent (the G1 / H1 / H1_2 policies: g1_config.py:92-108,
+ * h1_config.py:103-118, h1_2_config.py:115-130).  Dense form of the padded-trajectory
+ * update: the [T, B] reset mask zeroes (h, c) before step t when the env was done at t-1.
+ *  gx      [T,B,4H]  x W_ih^T + b_ih + b_hh (one GEMM over T*B rows, by the caller)
+ *  whh     [4H,H]    weight_hh_l0 (16-byte aligned)
+ *  h0, c0  [B,H]     state before step 0 (NULL: zeros); reset [T,B] bytes or NULL
+ *  h_out, c_out [T,B,H], gact [T,B,4H] (activated gates): outputs, each may be NULL
+ *  h_last, c_last [B,H]: state after step T-1 (may alias h0/c0: rollout mode, T = 1)
+ * pmlp_lstm_bwd: dh_out [T,B,H] -> dgx [T,B,4H] (gradient of the gate pre-activations);
+ * the caller forms dW_ih = dgx^T x, dW_hh = dgx^T h_prev, db = sum(dgx).
+ * H = 32, 64 or 128 (pmlp_lstm_supported). */
+PMLP_API const char* pmlp_lstm_last_error(void);
+PMLP_API int pmlp_lstm_supported(int32_t hidden);
+PMLP_API int pmlp_lstm_fwd(int32_t T, int32_t B, int32_t H, const float* gx, const float* whh, const float* h0,
+                           const float* c0, const uint8_t* reset, float* h_out, float* c_out, float* gact,
+                           float* h_last, float* c_last, void* stream);
+PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0, const uint8_t* reset,
+                           const float* c_out, const float* gact, const float* dh_out, float* dgx, void* stream);
+
 #endif

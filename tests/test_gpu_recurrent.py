@@ -1,0 +1,205 @@
+"""The recurrent (LSTM) policy leg of BASELINE configs[2..4] (G1 / H1 / H1_2 train
+ActorCriticRecurrent, LSTM 64): the HIP sequence kernels (csrc/lstm_seq.hip) against torch,
+one recurrent PPO update at H1_2 scale against the same update in fp32 on the CPU (rsl_rl's
+padded-trajectory form), and the captured rollout/update graphs against eager."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from rsl_rl.algorithms import PPO  # noqa: E402
+from rsl_rl.modules import ActorCriticRecurrent  # noqa: E402
+from rsl_rl.modules import lstm_seq  # noqa: E402
+
+
+@pytest.mark.parametrize("H", [32, 64, 128])
+def test_lstm_kernels_match_torch(H):
+    """Forward outputs and the four parameter gradients of the dense LSTM (resets inside
+    the sequence, a carried initial state) vs the same recurrence in torch fp32 ops."""
+    torch.manual_seed(H)
+    T, B, I = 24, 1000, 47
+    rnn = torch.nn.LSTM(I, H).cuda()
+    x = torch.randn(T, B, I, device="cuda")
+    h0 = 0.5 * torch.randn(1, B, H, device="cuda")
+    c0 = 0.5 * torch.randn(1, B, H, device="cuda")
+    reset = (torch.rand(T, B, device="cuda") < 0.1).to(torch.uint8)
+    reset[0] = 0
+    y = lstm_seq.lstm_dense(rnn, x, h0, c0, reset)
+    y_ref = lstm_seq.lstm_dense_reference(rnn, x, h0, c0, reset)
+    torch.testing.assert_close(y, y_ref, rtol=1e-5, atol=2e-6)
+    g = torch.randn_like(y)
+    params = [rnn.weight_ih_l0, rnn.weight_hh_l0, rnn.bias_ih_l0, rnn.bias_hh_l0]
+    gk = torch.autograd.grad(y, params, g)
+    gr = torch.autograd.grad(y_ref, params, g)
+    for name, a, b in zip(("w_ih", "w_hh", "b_ih", "b_hh"), gk, gr):
+        rel = float((a - b).norm() / b.norm())
+        assert rel < 1e-5, (name, rel)
+    # without resets and from zeros, the reference statement is nn.LSTM itself
+    y0 = lstm_seq.lstm_dense(rnn, x, None, None, None)
+    torch.testing.assert_close(y0, rnn(x)[0], rtol=1e-5, atol=2e-6)
+
+
+def test_lstm_rollout_step_in_place_matches_nn_lstm():
+    torch.manual_seed(0)
+    B, I, H = 8192, 47, 64
+    rnn = torch.nn.LSTM(I, H).cuda()
+    h = 0.3 * torch.randn(1, B, H, device="cuda")
+    c = 0.3 * torch.randn(1, B, H, device="cuda")
+    x = torch.randn(B, I, device="cuda")
+    out_ref, (h_ref, c_ref) = rnn(x.unsqueeze(0), (h.clone(), c.clone()))
+    ptr = h.data_ptr()
+    out = lstm_seq.lstm_step_(rnn, x, h, c)
+    assert out.data_ptr() == ptr  # in place: static state buffers
+    torch.testing.assert_close(h, h_ref, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(c, c_ref, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(out, out_ref, rtol=1e-5, atol=2e-6)
+
+
+def _synthetic_storage(alg, T, N, O, P, A, H, seed):
+    """A rollout with dones and the saved hidden states of a real recurrent rollout: the
+    state at t = 0 is carried (nonzero); after a done it is zero."""
+    g = torch.Generator().manual_seed(seed)
+    st = alg.storage
+    st.observations.copy_(torch.randn(T, N, O, generator=g))
+    st.privileged_observations.copy_(torch.randn(T, N, P, generator=g))
+    mu = 0.3 * torch.randn(T, N, A, generator=g)
+    sigma = 0.8 * (1 + 0.1 * torch.rand(T, N, A, generator=g))
+    act = mu + sigma * torch.randn(T, N, A, generator=g)
+    st.mu.copy_(mu)
+    st.sigma.copy_(sigma)
+    st.actions.copy_(act)
+    st.actions_log_prob.copy_(torch.distributions.Normal(mu, sigma).log_prob(act).sum(-1, keepdim=True))
+    st.values.copy_(0.5 * torch.randn(T, N, 1, generator=g))
+    st.rewards.copy_(0.2 * torch.randn(T, N, 1, generator=g))
+    dones = (torch.rand(T, N, 1, generator=g) < 0.04)
+    st.dones.copy_(dones.to(st.dones.dtype))
+    hs = []
+    for _ in range(2):  # (h, c)
+        s = 0.5 * torch.randn(T, 1, N, H, generator=g)
+        s[1:] *= (~dones[:-1, :, 0]).float().view(T - 1, 1, N, 1)
+        hs.append(s)
+    dev = st.observations.device
+    st.saved_hidden_states_a = [s.to(dev) for s in hs]
+    st.saved_hidden_states_c = [(0.7 * s).to(dev) for s in hs]
+    st.step = T
+    return torch.randn(N, P, generator=g)
+
+
+def test_recurrent_ppo_update_matches_fp32_cpu_update():
+    """One PPO update (5 epochs x 4 mini-batches, adaptive LR) of the H1_2 recurrent policy at
+    BASELINE scale (obs 47, priv 50, 8192 envs, T = 24, LSTM 64, MLP [32]) on the GPU (dense
+    form, LSTM kernels, GAE kernel) vs the same update on the CPU in fp32 with rsl_rl's padded
+    trajectories and torch's LSTM."""
+    T, N, O, P, A, H = 24, 8192, 47, 50, 12, 64
+    torch.manual_seed(0)
+    kw = dict(actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm", rnn_hidden_size=H,
+              rnn_num_layers=1, init_noise_std=0.8)
+    ac_cpu = ActorCriticRecurrent(O, P, A, **kw)
+    ac_gpu = copy.deepcopy(ac_cpu).cuda()
+    akw = dict(num_learning_epochs=5, num_mini_batches=4, learning_rate=1e-3, schedule="adaptive", gamma=0.99,
+               lam=0.95, entropy_coef=0.01)
+    cpu = PPO(ac_cpu, device="cpu", **akw)
+    cpu._dense_recurrent = False  # rsl_rl's own padded-trajectory generator
+    gpu = PPO(ac_gpu, device="cuda", **akw)
+    assert gpu._dense_recurrent and gpu.use_graph
+    for alg in (cpu, gpu):
+        alg.init_storage(N, T, [O], [P], [A])
+    last = _synthetic_storage(cpu, T, N, O, P, A, H, seed=1)
+    _synthetic_storage(gpu, T, N, O, P, A, H, seed=1)
+    cpu.compute_returns(last)
+    gpu.compute_returns(last.cuda())
+    torch.testing.assert_close(gpu.storage.advantages.cpu(), cpu.storage.advantages, rtol=1e-4, atol=1e-4)
+    p0 = [p.detach().clone() for p in ac_cpu.parameters()]
+    l_cpu = cpu.update()
+    l_gpu = gpu.update()  # eager (first call)
+    np.testing.assert_allclose(l_gpu, l_cpu, rtol=1e-3, atol=1e-5)
+    assert gpu.learning_rate == pytest.approx(cpu.learning_rate, rel=1e-6)
+    lr = 1e-3
+    for (name, a), b, c in zip(ac_cpu.named_parameters(), ac_gpu.parameters(), p0):
+        da, db = a.detach() - c, b.detach().cpu() - c
+        assert da.abs().max() > 0, name
+        # Adam turns a sign flip of a ~0 gradient into a ~lr move: a few entries may differ
+        bad = ((da - db).abs() > 0.1 * lr).float().mean().item()
+        assert bad < 0.02, (name, bad)
+        assert (da - db).abs().max() <= 2 * 20 * 1.5 * lr, name
+
+
+def test_recurrent_update_graph_matches_eager():
+    """The captured recurrent update (dense generator, LSTM kernels, capturable Adam) replays
+    the eager update: same losses and parameters from the same starting point."""
+    T, N, O, P, A, H = 24, 2048, 47, 50, 12, 64
+    torch.manual_seed(0)
+    kw = dict(actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm", rnn_hidden_size=H,
+              rnn_num_layers=1, init_noise_std=0.8)
+    ac = ActorCriticRecurrent(O, P, A, **kw).cuda()
+    alg = PPO(ac, device="cuda", num_learning_epochs=2, num_mini_batches=4, learning_rate=3e-4, schedule="fixed")
+    alg.init_storage(N, T, [O], [P], [A])
+    last = _synthetic_storage(alg, T, N, O, P, A, H, seed=2).cuda()
+    alg.compute_returns(last)
+    alg.update()  # eager warm-up
+    assert alg._graph is None
+    saved = {k: v.clone() for k, v in alg.storage.__dict__.items() if torch.is_tensor(v) and not k.startswith("_")}
+    params = list(ac.parameters())
+    p0 = [p.detach().clone() for p in params]
+    st0 = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in alg.optimizer.state[p].items()}
+           for p in params}
+    alg.storage.step = T
+    g_loss = alg.update()  # captured + replayed
+    assert alg._graph is not None
+    p_graph = [p.detach().clone() for p in params]
+    with torch.no_grad():
+        for p, v in zip(params, p0):
+            p.copy_(v)
+        for p in params:
+            for k, v in alg.optimizer.state[p].items():
+                if torch.is_tensor(v):
+                    v.copy_(st0[id(p)][k])
+        for k, v in saved.items():
+            getattr(alg.storage, k).copy_(v)
+    alg.storage.step = T
+    alg.use_graph = False
+    e_loss = alg.update()
+    np.testing.assert_allclose(g_loss, e_loss, rtol=1e-5, atol=1e-7)
+    for a, b in zip(params, p_graph):
+        assert (a.detach() - b).abs().max() <= 8 * 3e-4
+
+
+def test_recurrent_rollout_graph_matches_eager(tmp_path):
+    """OnPolicyRunner on H1 (recurrent policy): the captured collection loop (LSTM state
+    stepped in place, masked resets) replays the eager loop's rollouts."""
+    import isaacgym  # noqa: F401
+    from legged_gym.envs import task_registry
+    from legged_gym.utils import get_args
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    out = {}
+    for graph in (False, True):
+        args = get_args(["--task", "h1", "--num_envs", "512", "--headless"])
+        env_cfg, train_cfg = task_registry.get_cfgs("h1")
+        env_cfg = copy.deepcopy(env_cfg)
+        env_cfg.env.episode_length_s = 0.5  # resets inside every rollout
+        env, _ = task_registry.make_env(name="h1", args=args, env_cfg=env_cfg)
+        cfg = class_to_dict(train_cfg)
+        cfg["runner"]["rollout_graph"] = graph
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        runner = OnPolicyRunner(env, cfg, log_dir=None, device="cuda:0")
+        runner.alg.use_graph = False  # compare the rollouts, not the update paths
+        runner.learn(3, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+        st = runner.alg.storage
+        out[graph] = dict(root=env.root_states.clone(), st_obs=st.observations.clone(), st_act=st.actions.clone(),
+                          st_rew=st.rewards.clone(), hid=st.saved_hidden_states_a[0].clone(),
+                          mem=runner.alg.actor_critic.memory_a.hidden_states[0].clone(),
+                          params=[p.detach().clone() for p in runner.alg.actor_critic.parameters()],
+                          captured=runner._rollout_graph is not None)
+        env.close()
+    e, g = out[False], out[True]
+    assert g["captured"] and not e["captured"]
+    for k in ("root", "st_obs", "st_act", "st_rew", "hid", "mem"):
+        assert torch.equal(e[k], g[k]), k
+    for a, b in zip(e["params"], g["params"]):
+        assert torch.equal(a, b)

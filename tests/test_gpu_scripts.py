@@ -1,0 +1,70 @@
+"""The reference's entry points run unmodified on the GPU build (scripts/train.py:11-14,
+scripts/play.py:15-44): train a few iterations from the CLI, then play the last checkpoint,
+which exports the policy; the exported TorchScript actor reproduces the checkpoint's actor."""
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from conftest import ROOT  # noqa: E402
+
+PKG = os.path.join(ROOT, "unitree-rl-gym_amd")
+
+
+def run(script, *argv, timeout=300, steps=None):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
+    if steps is not None:
+        env["LEGGED_GYM_PLAY_STEPS"] = str(steps)
+    r = subprocess.run([sys.executable, os.path.join(PKG, "legged_gym", "scripts", script), *argv], cwd=PKG, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, f"{script} failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    return r.stdout
+
+
+@pytest.mark.parametrize("task,n_obs,recurrent", [("go2", 48, False), ("h1", 41, True)])
+def test_train_then_play_export(task, n_obs, recurrent):
+    exp = f"pytest_{task}"
+    out = run("train.py", "--task", task, "--num_envs", "512", "--max_iterations", "2", "--headless",
+              "--experiment_name", exp, "--run_name", "cli")
+    assert "Learning iteration 1/2" in out
+    from legged_gym import LEGGED_GYM_ROOT_DIR
+    runs = sorted(glob.glob(os.path.join(LEGGED_GYM_ROOT_DIR, "logs", exp, "*_cli")))
+    assert runs, "train.py wrote no run directory"
+    ck = os.path.join(runs[-1], "model_2.pt")
+    assert os.path.exists(ck)
+    run("play.py", "--task", task, "--headless", "--experiment_name", exp, "--load_run", os.path.basename(runs[-1]),
+        steps=30)
+    pol = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", exp, "exported", "policies",
+                       "policy_lstm_1.pt" if recurrent else "policy_1.pt")
+    assert os.path.exists(pol)
+    m = torch.jit.load(pol)
+    sd = torch.load(ck, map_location="cpu", weights_only=True)["model_state_dict"]
+    actor = {k[len("actor."):]: v for k, v in sd.items() if k.startswith("actor.")}
+    x = torch.randn(3, n_obs, generator=torch.Generator().manual_seed(0))
+    if recurrent:  # the exported LSTM policy == memory_a.rnn + actor of the checkpoint
+        rnn = torch.nn.LSTM(n_obs, 64)
+        rnn.load_state_dict({k[len("memory_a.rnn."):]: v for k, v in sd.items() if k.startswith("memory_a.rnn.")})
+        m.reset_memory()
+        h = None
+        for i in range(3):
+            y, h = rnn(x[i:i + 1].unsqueeze(0), h)
+            want = _mlp(actor, y[0])
+            torch.testing.assert_close(m(x[i:i + 1]), want, rtol=1e-5, atol=1e-6)
+    else:
+        torch.testing.assert_close(m(x), _mlp(actor, x), rtol=1e-5, atol=1e-6)
+
+
+def _mlp(sd, x):
+    """Linear/ELU stack from a state dict {'0.weight', '0.bias', '2.weight', ...}."""
+    idx = sorted({int(k.split(".")[0]) for k in sd})
+    for j, i in enumerate(idx):
+        x = torch.nn.functional.linear(x, sd[f"{i}.weight"], sd[f"{i}.bias"])
+        if j < len(idx) - 1:
+            x = torch.nn.functional.elu(x)
+    return x

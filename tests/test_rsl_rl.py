@@ -136,6 +136,7 @@ def test_lstm_export_matches_pretrained_policy(robot, tmp_path):
     """Golden: deploy/pre_train/<robot>/motion.pt (the reference's own exported
     PolicyExporterLSTM).  Our ActorCriticRecurrent + PolicyExporterLSTM with the
     same weights must reproduce its outputs and its reset_memory semantics."""
+    import legged_gym.envs  # noqa: F401  (train.py's import order: envs before utils)
     from legged_gym.utils.helpers import export_policy_as_jit
     g = np.load(os.path.join(GOLDEN, f"lstm_policy_{robot}.npz"))
     n_in = g["w.memory.weight_ih_l0"].shape[1]
@@ -176,3 +177,65 @@ def test_splitk_linear_matches_linear_grads():
     assert torch.allclose(dw, dw2, rtol=1e-10, atol=1e-10)
     # state_dict keys identical to nn.Linear (checkpoints interchange)
     assert set(skl.SplitKLinear(48, 32).state_dict()) == set(lin.state_dict())
+
+
+def test_dense_recurrent_update_equals_padded_trajectories():
+    """The dense recurrent update (recurrent_dense_mini_batch_generator: every env's T steps with
+    the LSTM state zeroed after dones) computes exactly rsl_rl v1.0.2's padded-trajectory update
+    (reccurent_mini_batch_generator + split_and_pad_trajectories): same losses, same gradients."""
+    torch.manual_seed(0)
+    env = FakeEnv(num_envs=8, num_privileged_obs=9, ep_len=5)
+    ac = ActorCriticRecurrent(6, 9, 3, actor_hidden_dims=[16], critic_hidden_dims=[16], rnn_type="lstm",
+                              rnn_hidden_size=8, rnn_num_layers=1, init_noise_std=0.8)
+    ppo = PPO(ac, num_learning_epochs=1, num_mini_batches=2, device="cpu")
+    ppo.init_storage(8, 12, [6], [9], [3])
+    obs, priv = env.reset()
+    with torch.inference_mode():
+        for it in range(2):  # two rollouts: the second starts from a carried (nonzero) state
+            ppo.storage.clear()
+            for _ in range(12):
+                a = ppo.act(obs, priv)
+                obs, priv, r, d, info = env.step(a)
+                ppo.process_env_step(r, d, info)
+            ppo.compute_returns(priv)
+    st = ppo.storage
+    assert st.dones.any() and st.saved_hidden_states_a[0][0].abs().sum() > 0
+    params = list(ac.parameters())
+    for (padded, dense) in zip(st.reccurent_mini_batch_generator(2, 1), st.recurrent_dense_mini_batch_generator(2, 1)):
+        out = []
+        for flag, batch in ((False, padded), (True, dense)):
+            ppo._dense_recurrent = flag
+            loss, surr, vl = ppo._reference_loss(*batch)
+            out.append((loss.detach(), surr.detach(), vl.detach(), torch.autograd.grad(loss, params)))
+        (l1, s1, v1, g1), (l2, s2, v2, g2) = out
+        torch.testing.assert_close(l2, l1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(s2, s1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(v2, v1, rtol=1e-5, atol=1e-6)
+        for a, b in zip(g2, g1):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+    ppo._dense_recurrent = True
+
+
+def test_recurrent_rollout_saves_pre_step_hidden_states():
+    """The hidden state stored for step t is the state BEFORE step t (reset after dones)."""
+    torch.manual_seed(1)
+    env = FakeEnv(num_envs=4, ep_len=3)
+    ac = ActorCriticRecurrent(6, 6, 3, actor_hidden_dims=[8], critic_hidden_dims=[8], rnn_type="lstm",
+                              rnn_hidden_size=8, rnn_num_layers=1)
+    ppo = PPO(ac, device="cpu")
+    ppo.init_storage(4, 6, [6], [None], [3])
+    obs, _ = env.reset()
+    states = []
+    with torch.inference_mode():
+        for _ in range(6):
+            hs = ac.get_hidden_states()
+            states.append(None if hs[0] is None else hs[0][0].clone())
+            a = ppo.act(obs, obs)
+            obs, _, r, d, info = env.step(a)
+            ppo.process_env_step(r, d, info)
+    saved = ppo.storage.saved_hidden_states_a[0]  # [T, layers, N, H]
+    for t in range(1, 6):
+        torch.testing.assert_close(saved[t, 0], states[t][0])
+    d = ppo.storage.dones[:, :, 0].bool()
+    for t in range(1, 6):  # after a done the stored state is zero
+        assert saved[t, 0][d[t - 1]].abs().sum() == 0

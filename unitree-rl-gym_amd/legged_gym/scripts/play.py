@@ -37,4 +37,6 @@ def play(args, num_steps=None):
 
 
 if __name__ == "__main__":
-    play(get_args())
+    # LEGGED_GYM_PLAY_STEPS bounds the roll-out (the reference plays 10 episodes' worth)
+    n = os.environ.get("LEGGED_GYM_PLAY_STEPS")
+    play(get_args(), num_steps=int(n) if n else None)

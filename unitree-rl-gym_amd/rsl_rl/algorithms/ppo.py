@@ -68,7 +68,12 @@ class PPO:
         # whole-update HIP graph (MLP policies on a GPU): set use_graph=False to disable
         # (library bf16 GEMMs under autocast drift inside a captured graph on this ROCm;
         #  the MFMA MLP kernels are deterministic and capture cleanly)
-        self.use_graph = on_gpu and not getattr(self.actor_critic, "is_recurrent", False) and \
+        # recurrent policies train in the dense form (storage.recurrent_dense_mini_batch_generator,
+        # modules/lstm_seq.py): fixed shapes and no host sync, so their update captures too
+        self._dense_recurrent = getattr(self.actor_critic, "is_recurrent", False) and \
+            hasattr(self.actor_critic, "act_dense")
+        self.use_graph = on_gpu and (not getattr(self.actor_critic, "is_recurrent", False) or
+                                     self._dense_recurrent) and \
             self.optimizer.defaults.get("capturable", False) and \
             (self.world_size == 1 or dist.get_backend() == "nccl")
         self._graph = None
@@ -131,7 +136,10 @@ class PPO:
             self._stored_t = t
             return actions
         if self.actor_critic.is_recurrent:
-            self.transition.hidden_states = self.actor_critic.get_hidden_states()
+            # the state BEFORE this step, copied into the storage slot now: on the GPU the
+            # memory updates its state buffers in place during act()
+            self.storage._save_hidden_states(self.actor_critic.get_hidden_states())
+            self.transition.hidden_states = None
         if not self.actor_critic.is_recurrent and hasattr(self.actor_critic, "act_and_value"):  # shared launches
             actions, values = self.actor_critic.act_and_value(obs, critic_obs)
             self.transition.actions, self.transition.values = actions.detach(), values.detach()
@@ -174,7 +182,8 @@ class PPO:
 
     def compute_returns(self, last_critic_obs):
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
-        if self._fused is not None:  # GAE + normalisation: two launches (+ a moments all-reduce)
+        if self._fused is not None or (str(self.device).startswith("cuda") and last_values.is_cuda):
+            # GAE + normalisation: two launches (+ a moments all-reduce across ranks)
             fused_step.gae(self.storage, last_values, self.gamma, self.lam, self.world_size)
             return
         stats = self._global_adv_stats if self.world_size > 1 else None
@@ -194,13 +203,28 @@ class PPO:
     def _reference_loss(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
                         returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
                         masks_batch):
-        """The loss exactly as rsl_rl v1.0.2 PPO.update states it (torch ops)."""
-        if self.actor_critic.is_recurrent:
-            self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
-        else:  # v1.0.2 calls act() here and discards the sample; only the distribution is used
-            self.actor_critic.update_distribution(obs_batch)
-        actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
-        value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
+        """The loss exactly as rsl_rl v1.0.2 PPO.update states it (torch ops).  Recurrent
+        policies in the dense form (masks_batch is the [T, envs] reset mask of
+        recurrent_dense_mini_batch_generator): every [T, envs, .] tensor is flattened to
+        T*envs rows, the rows the padded form's unpad_trajectories produces."""
+        if self.actor_critic.is_recurrent and self._dense_recurrent:
+            ac = self.actor_critic
+            ac.act_dense(obs_batch, hid_states_batch[0], masks_batch)
+            value_batch = ac.evaluate_dense(critic_obs_batch, hid_states_batch[1], masks_batch)
+            flat = lambda t: t.reshape(-1, t.shape[-1])  # noqa: E731
+            actions_batch, target_values_batch, advantages_batch = (flat(actions_batch), flat(target_values_batch),
+                                                                     flat(advantages_batch))
+            returns_batch, old_actions_log_prob_batch = flat(returns_batch), flat(old_actions_log_prob_batch)
+            old_mu_batch, old_sigma_batch = flat(old_mu_batch), flat(old_sigma_batch)
+            actions_log_prob_batch = ac.get_actions_log_prob(actions_batch)
+        else:
+            if self.actor_critic.is_recurrent:
+                self.actor_critic.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+            else:  # v1.0.2 calls act() here and discards the sample; only the distribution is used
+                self.actor_critic.update_distribution(obs_batch)
+            actions_log_prob_batch = self.actor_critic.get_actions_log_prob(actions_batch)
+            value_batch = self.actor_critic.evaluate(critic_obs_batch, masks=masks_batch,
+                                                     hidden_states=hid_states_batch[1])
         mu_batch = self.actor_critic.action_mean
         sigma_batch = self.actor_critic.action_std
         entropy_batch = self.actor_critic.entropy
@@ -293,7 +317,9 @@ class PPO:
             acc = self._update_graphed()
         else:
             acc = torch.zeros(2, device=self.device)
-            if self.actor_critic.is_recurrent:
+            if self.actor_critic.is_recurrent and self._dense_recurrent:
+                gen = self.storage.recurrent_dense_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+            elif self.actor_critic.is_recurrent:
                 gen = self.storage.reccurent_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
             else:
                 gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
@@ -353,7 +379,8 @@ class PPO:
         batch = st.num_envs * st.num_transitions_per_env
         mb = batch // self.num_mini_batches
         if self._graph is None:
-            self._perm = torch.randperm(self.num_mini_batches * mb, device=self.device)
+            self._perm = None if self._dense_recurrent else \
+                torch.randperm(self.num_mini_batches * mb, device=self.device)
             self._acc = torch.zeros(2, device=self.device)
             flat = [st.observations.flatten(0, 1),
                     st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None
@@ -364,6 +391,11 @@ class PPO:
 
             def body():
                 self._acc.zero_()
+                if self._dense_recurrent:  # contiguous env slices, no permutation (rsl_rl recurrent)
+                    for batch in st.recurrent_dense_mini_batch_generator(self.num_mini_batches,
+                                                                         self.num_learning_epochs):
+                        self._minibatch_step(*batch, self._acc)
+                    return
                 adv = st.advantages.flatten(0, 1)
                 for _ in range(self.num_learning_epochs):
                     for i in range(self.num_mini_batches):
@@ -399,6 +431,7 @@ class PPO:
         if st.advantages.data_ptr() != self._adv_static.data_ptr():
             self._adv_static.copy_(st.advantages)
             st.advantages = self._adv_static
-        self._perm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
+        if not self._dense_recurrent:  # one randperm per update (mini_batch_generator's rule)
+            self._perm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
         self._graph.replay()
         return self._acc

@@ -88,7 +88,11 @@ class ActorCritic(nn.Module):
 
     def act(self, observations, **kwargs):
         self.update_distribution(observations)
-        return self.distribution.sample()
+        # = distribution.sample() (mean + std * N(0, 1) draws) through randn_like: torch.normal
+        # with tensor mean/std is not capturable on this ROCm, randn is (graph-safe RNG)
+        d = self.distribution
+        with torch.no_grad():
+            return d.mean + d.stddev * torch.randn_like(d.mean)
 
     def get_actions_log_prob(self, actions):
         return self.distribution.log_prob(actions).sum(dim=-1)

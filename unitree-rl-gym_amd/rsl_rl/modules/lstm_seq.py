@@ -1,0 +1,139 @@
+"""The recurrent memory of ActorCriticRecurrent on hand-written HIP sequence kernels
+(csrc/lstm_seq.hip through include/ppo_mlp.h, "recurrent memory").
+
+rsl_rl v1.0.2 trains the LSTM on trajectories split at dones and zero-padded
+(``split_and_pad_trajectories``): the trajectory count depends on the data, so every
+mini-batch costs a device->host sync and nothing can be captured in a graph.  The
+dense form computes the same outputs with fixed shapes: every env's T steps run in
+order and (h, c) is zeroed before step t when the env was done at t-1, which is the
+zero state a padded trajectory that starts there begins from.  (The trajectory that
+starts at t = 0 begins from the hidden state saved at t = 0, in both forms.)
+
+``lstm_dense`` is differentiable w.r.t. the four LSTM parameters (autograd Function
+around pmlp_lstm_fwd / pmlp_lstm_bwd plus three GEMMs for the weight gradients);
+``lstm_dense_reference`` is the same recurrence in plain torch ops (CPU, tests).
+"""
+import ctypes as C
+
+import torch
+
+from . import mfma_mlp as mm
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = mm.load()
+    if not _bound:
+        vp, i32 = C.c_void_p, C.c_int32
+        L.pmlp_lstm_last_error.restype = C.c_char_p
+        L.pmlp_lstm_supported.argtypes = [i32]
+        L.pmlp_lstm_fwd.argtypes = [i32, i32, i32] + [vp] * 10 + [vp]
+        L.pmlp_lstm_bwd.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
+        _bound = True
+    return L
+
+
+def _ok(status, what):
+    if status != 0:
+        raise RuntimeError(f"{what} failed: {_lib().pmlp_lstm_last_error().decode(errors='replace')}")
+
+
+def usable(rnn, x):
+    """The kernels cover a one-layer LSTM with hidden 32/64/128 on a GPU, fp32."""
+    return (x.is_cuda and isinstance(rnn, torch.nn.LSTM) and rnn.num_layers == 1 and rnn.bias
+            and x.dtype == torch.float32 and rnn.hidden_size in (32, 64, 128) and not rnn.batch_first)
+
+
+def _gx(x, w_ih, b_ih, b_hh):
+    T, B, I = x.shape
+    return torch.addmm(b_ih + b_hh, x.reshape(T * B, I), w_ih.t()).view(T, B, w_ih.shape[0])
+
+
+class _LSTMDense(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, h0, c0, reset, w_ih, w_hh, b_ih, b_hh):
+        T, B, _ = x.shape
+        H = w_hh.shape[1]
+        whh = w_hh.detach().contiguous()
+        gx = _gx(x.detach(), w_ih.detach(), b_ih.detach(), b_hh.detach())
+        h_out = torch.empty(T, B, H, device=x.device)
+        c_out = torch.empty(T, B, H, device=x.device)
+        gact = torch.empty(T, B, 4 * H, device=x.device)
+        p = mm._p
+        _ok(_lib().pmlp_lstm_fwd(T, B, H, p(gx), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out), p(gact), None,
+                                 None, mm._stream()), "pmlp_lstm_fwd")
+        ctx.save_for_backward(x, h0, c0, reset, whh, h_out, c_out, gact)
+        return h_out
+
+    @staticmethod
+    def backward(ctx, dh_out):
+        x, h0, c0, reset, whh, h_out, c_out, gact = ctx.saved_tensors
+        T, B, I = x.shape
+        H = whh.shape[1]
+        dgx = torch.empty(T, B, 4 * H, device=x.device)
+        p = mm._p
+        _ok(_lib().pmlp_lstm_bwd(T, B, H, p(whh), p(c0), p(reset), p(c_out), p(gact), p(dh_out.contiguous()), p(dgx),
+                                 mm._stream()), "pmlp_lstm_bwd")
+        g = dgx.view(T * B, 4 * H)
+        dw_ih = g.t().mm(x.reshape(T * B, I))
+        hprev = torch.empty(T, B, H, device=x.device)
+        if h0 is None:
+            hprev[0].zero_()
+        else:
+            hprev[0].copy_(h0)
+        hprev[1:].copy_(h_out[:-1])
+        if reset is not None:
+            hprev.masked_fill_(reset.bool().unsqueeze(-1), 0.0)
+        dw_hh = g.t().mm(hprev.view(T * B, H))
+        db = g.sum(0)
+        return None, None, None, None, dw_ih, dw_hh, db, db
+
+
+def lstm_dense(rnn, x, h0, c0, reset):
+    """[T,B,I] -> [T,B,H] through rnn (nn.LSTM, one layer) with resets before step t where
+    reset[t] != 0; h0/c0 [B,H] (detached: the saved rollout state) or None."""
+    def state(s):
+        if s is None:
+            return None
+        s = s.detach().reshape(x.shape[1], -1)
+        return s.clone() if s.is_inference() else s.contiguous()
+
+    h0, c0 = state(h0), state(c0)
+    reset = None if reset is None else reset.to(torch.uint8).contiguous()
+    return _LSTMDense.apply(x.contiguous(), h0, c0, reset, rnn.weight_ih_l0, rnn.weight_hh_l0, rnn.bias_ih_l0,
+                            rnn.bias_hh_l0)
+
+
+def lstm_dense_reference(rnn, x, h0, c0, reset):
+    """The same recurrence in torch ops (any device): the statement the kernels are checked against."""
+    T, B, _ = x.shape
+    H = rnn.hidden_size
+    h = x.new_zeros(B, H) if h0 is None else h0.reshape(B, H)
+    c = x.new_zeros(B, H) if c0 is None else c0.reshape(B, H)
+    gx = _gx(x, rnn.weight_ih_l0, rnn.bias_ih_l0, rnn.bias_hh_l0)
+    out = []
+    for t in range(T):
+        if reset is not None:
+            keep = (reset[t] == 0).to(x.dtype).unsqueeze(-1)
+            h, c = h * keep, c * keep
+        g = gx[t] + h.mm(rnn.weight_hh_l0.t())
+        i, f, gg, o = g.chunk(4, dim=-1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        out.append(h)
+    return torch.stack(out)
+
+
+def lstm_step_(rnn, x, h, c):
+    """One rollout step in place: h, c [1,B,H] static buffers (the policy's memory) are read
+    and overwritten by the kernel (capturable); returns h (the step's output, [1,B,H])."""
+    B = x.shape[0]
+    H = rnn.hidden_size
+    gx = torch.addmm(rnn.bias_ih_l0 + rnn.bias_hh_l0, x, rnn.weight_ih_l0.t())
+    p = mm._p
+    with torch.no_grad():
+        _ok(_lib().pmlp_lstm_fwd(1, B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), None, None,
+                                 None, None, p(h), p(c), mm._stream()), "pmlp_lstm_fwd")
+    return h

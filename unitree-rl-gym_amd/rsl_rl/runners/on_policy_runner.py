@@ -219,11 +219,14 @@ class OnPolicyRunner:
 
     def _rollout_graph_ok(self):
         """The whole collection loop replays as one HIP graph when nothing in it needs
-        the host: a CUDA device, a feed-forward policy, and an env whose step keys its
-        noise on a device-side counter (LeggedRobot.account_replayed_steps)."""
+        the host: a CUDA device, a feed-forward policy or a recurrent one whose memory
+        steps in place on the LSTM kernels (static state buffers, masked resets), and an
+        env whose step keys its noise on a device-side counter
+        (LeggedRobot.account_replayed_steps)."""
+        ac = self.alg.actor_critic
         return (bool(self.cfg.get("rollout_graph", True)) and str(self.device).startswith("cuda")
-                and not self.alg.actor_critic.is_recurrent and hasattr(self.env, "account_replayed_steps")
-                and self.alg.storage is not None)
+                and (not ac.is_recurrent or (hasattr(ac, "rollout_capturable") and ac.rollout_capturable()))
+                and hasattr(self.env, "account_replayed_steps") and self.alg.storage is not None)
 
     def log(self, locs, width=80, pad=35):
         ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1

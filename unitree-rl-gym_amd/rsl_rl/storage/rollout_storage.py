@@ -70,8 +70,12 @@ class RolloutStorage:
         hid_a = hidden_states[0] if isinstance(hidden_states[0], tuple) else (hidden_states[0],)
         hid_c = hidden_states[1] if isinstance(hidden_states[1], tuple) else (hidden_states[1],)
         if self.saved_hidden_states_a is None:
-            self.saved_hidden_states_a = [torch.zeros(self.observations.shape[0], *h.shape, device=self.device) for h in hid_a]
-            self.saved_hidden_states_c = [torch.zeros(self.observations.shape[0], *h.shape, device=self.device) for h in hid_c]
+            # ordinary (not inference-mode) tensors: the update saves slices of them for backward
+            with torch.inference_mode(False):
+                self.saved_hidden_states_a = [torch.zeros(self.observations.shape[0], *h.shape, device=self.device)
+                                              for h in hid_a]
+                self.saved_hidden_states_c = [torch.zeros(self.observations.shape[0], *h.shape, device=self.device)
+                                              for h in hid_c]
         for i in range(len(hid_a)):
             self.saved_hidden_states_a[i][self.step].copy_(hid_a[i])
             self.saved_hidden_states_c[i][self.step].copy_(hid_c[i])
@@ -164,3 +168,24 @@ class RolloutStorage:
                 yield (obs_batch, critic_obs_batch, actions_batch, values_batch, advantages_batch, returns_batch,
                        old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, (hid_a, hid_c), masks_batch)
                 first_traj = last_traj
+
+    def recurrent_dense_mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        """The recurrent mini-batches of reccurent_mini_batch_generator (contiguous env
+        slices, every epoch in the same order) in the dense form: [T, envs, .] tensors,
+        the hidden states saved at t = 0, and reset[t] = dones[t-1] (the memory zeroes its
+        state there, which is where a padded trajectory would start from zeros).  Fixed
+        shapes and no device->host sync (the padded form counts trajectories on the host)."""
+        mb = self.num_envs // num_mini_batches
+        if not hasattr(self, "_dense_reset") or self._dense_reset.shape != self.dones.shape[:2]:
+            self._dense_reset = torch.zeros(self.dones.shape[:2], dtype=torch.uint8, device=self.device)
+        reset = self._dense_reset
+        reset[1:].copy_(self.dones[:-1, :, 0])  # in place: a captured update reads this buffer
+        cobs = self.privileged_observations if self.privileged_observations is not None else self.observations
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                sl = slice(i * mb, (i + 1) * mb)
+                hid_a = tuple(h[0][:, sl] for h in self.saved_hidden_states_a)
+                hid_c = tuple(h[0][:, sl] for h in self.saved_hidden_states_c)
+                yield (self.observations[:, sl], cobs[:, sl], self.actions[:, sl], self.values[:, sl],
+                       self.advantages[:, sl], self.returns[:, sl], self.actions_log_prob[:, sl], self.mu[:, sl],
+                       self.sigma[:, sl], (hid_a, hid_c), reset[:, sl])
