@@ -177,6 +177,14 @@ typedef struct lgs_task_params {
     /* 1: env origins are terrain tiles (legged_robot.py:582-585, custom_origins): reset_idx adds a
      * U[-1,1] xy offset to the root position (LGS_STREAM_RESET_ROOT draws 6, 7) */
     int32_t custom_origins;
+    /* a task's reward terms written in Python (subclass _reward_* methods, legged_robot.py:817-840)
+     * run between lgs_post_physics_rewards and lgs_post_physics_finish.  defer_reward_total = 1:
+     * the kernel writes the raw sum of its own terms to rew (no only_positive_rewards clip, no
+     * termination term; the caller adds its terms, clips and adds the termination term).
+     * num_extra_sums: episode-sum rows after the native ones (and termination) that the caller
+     * fills; they join the reset-time extras like the native sums. */
+    int32_t defer_reward_total;
+    int32_t num_extra_sums;
 } lgs_task_params;
 
 /* ---- per-env buffers of the VecEnv (device pointers; torch owns them) ---- */
@@ -269,6 +277,14 @@ LGS_API int lgs_step(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_coun
  *    contact forces from the bound net_contact_forces; advances env->step_counter like lgs_step. */
 LGS_API int lgs_step_physics(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 LGS_API int lgs_post_physics(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* lgs_post_physics in two parts around a caller's reward terms (compute_reward, :770-787):
+ *  - _rewards: episode length, base-frame state, commands (:681-698), check_termination (:711-721)
+ *    and the native reward terms (rew, per-term episode sums, reset/time_out); nothing is reset;
+ *  - _finish: reset_idx of the envs whose reset byte is set, push, observations, bookkeeping,
+ *    extras (:697-709), reading the base-frame state and commands the first part wrote.
+ * lgs_post_physics == _rewards then _finish (without deferred rewards).                        */
+LGS_API int lgs_post_physics_rewards(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+LGS_API int lgs_post_physics_finish(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(all) as used by BaseTask.reset (base_task.py:82-86) */
 LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(env_ids) (legged_robot.py:723-768) for an arbitrary subset: env_mask is a DEVICE

@@ -227,18 +227,19 @@ static void fk(const lgs_model_desc* md, const float* root13, const float* dofq,
 /* dense Cholesky in place (lower), n <= NMAX.  The reciprocal of each pivot is taken
  * once (IEEE 1/d) and every division by L_kk -- here and in the triangular solves --
  * is a multiplication by it: the HIP kernel's arithmetic, operation for operation
- * (one division per pivot instead of five on its serial chain). */
+ * (one division per pivot instead of five on its serial chain).  Every update is one
+ * fused multiply-add (fmaf), as in the kernel (both build with -ffp-contract=off). */
 static void cholesky(float* M, float* invd, int n) {
     for (int k = 0; k < n; ++k) {
         float d = M[k * NMAX + k];
-        for (int s = 0; s < k; ++s) d -= M[k * NMAX + s] * M[k * NMAX + s];
+        for (int s = 0; s < k; ++s) d = fmaf(-M[k * NMAX + s], M[k * NMAX + s], d);
         d = sqrtf(fmaxf(d, 1e-12f));
         const float inv = 1.0f / d;
         M[k * NMAX + k] = d;
         invd[k] = inv;
         for (int i = k + 1; i < n; ++i) {
             float v = M[i * NMAX + k];
-            for (int s = 0; s < k; ++s) v -= M[i * NMAX + s] * M[k * NMAX + s];
+            for (int s = 0; s < k; ++s) v = fmaf(-M[i * NMAX + s], M[k * NMAX + s], v);
             M[i * NMAX + k] = v * inv;
         }
     }
@@ -246,7 +247,7 @@ static void cholesky(float* M, float* invd, int n) {
 static void fwd_sub(const float* L, const float* invd, int n, float* x) {
     for (int i = 0; i < n; ++i) {
         float v = x[i];
-        for (int s = 0; s < i; ++s) v -= L[i * NMAX + s] * x[s];
+        for (int s = 0; s < i; ++s) v = fmaf(-L[i * NMAX + s], x[s], v);
         x[i] = v * invd[i];
     }
 }
@@ -254,7 +255,7 @@ static void bwd_sub(const float* L, const float* invd, int n, float* x) {
     /* subtraction order s = n-1 .. i+1 (the order a column sweep produces) */
     for (int i = n - 1; i >= 0; --i) {
         float v = x[i];
-        for (int s = n - 1; s > i; --s) v -= L[s * NMAX + i] * x[s];
+        for (int s = n - 1; s > i; --s) v = fmaf(-L[s * NMAX + i], x[s], v);
         x[i] = v * invd[i];
     }
 }
@@ -509,7 +510,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         for (int i = 0; i < n; ++i) Y[r][i] = J[r][n - 1 - i];
         fwd_sub(Mp, invd, n, Y[r]);
         float s = 0.f;
-        for (int i = 0; i < n; ++i) s += J[r][i] * qf[i];
+        for (int i = 0; i < n; ++i) s = fmaf(J[r][i], qf[i], s);
         v[r] = s;
         lam[r] = 0.f;
     }
@@ -539,7 +540,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
                 }
                 float d1 = l1 - lam[r], d2 = l2 - lam[r + 1];
                 lam[r] = l1; lam[r + 1] = l2;
-                for (int s = 0; s < nr; ++s) v[s] += A[s][r] * d1 + A[s][r + 1] * d2;
+                for (int s = 0; s < nr; ++s) v[s] = fmaf(A[s][r + 1], d2, fmaf(A[s][r], d1, v[s]));
             }
         }
     }
@@ -547,7 +548,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     float z[NMAX];
     for (int i = 0; i < n; ++i) {
         float s = 0.f;
-        for (int r = 0; r < nr; ++r) s += Y[r][i] * lam[r];
+        for (int r = 0; r < nr; ++r) s = fmaf(Y[r][i], lam[r], s);
         z[i] = s;
     }
     bwd_sub(Mp, invd, n, z);

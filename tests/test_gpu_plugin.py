@@ -1,0 +1,93 @@
+"""Task plugin API: a task registered with task_registry.register may add
+reward terms as Python ``_reward_<name>`` methods (legged_robot.py:817-840 looks them up by
+name), and reset_idx may be called on any subset of envs (:723).  A Python copy of a native
+term must give the native term's rewards, sums and extras."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import isaacgym  # noqa: F401,E402
+from legged_gym.envs import task_registry  # noqa: E402
+from legged_gym.envs.base.legged_robot import LeggedRobot  # noqa: E402
+from legged_gym.utils import get_args  # noqa: E402
+
+
+class Go2WithPythonTerms(LeggedRobot):
+    """Go2 whose lin_vel_z and feet_air_time terms are Python methods (the reference's own
+    formulas, legged_robot.py:843-845, 912-923) instead of kernel terms."""
+
+    def _reward_lin_vel_z_py(self):
+        return torch.square(self.base_lin_vel[:, 2])
+
+    def _reward_action_rate_py(self):
+        return torch.sum(torch.square(self.last_actions - self.actions), dim=1)
+
+
+def _make(name, cls, edit):
+    env_cfg, train_cfg = task_registry.get_cfgs("go2")
+    cfg = copy.deepcopy(env_cfg)
+    edit(cfg)
+    task_registry.register(name, cls, cfg, copy.deepcopy(train_cfg))
+    args = get_args(["--task", name, "--num_envs", "256", "--headless"])
+    env, _ = task_registry.make_env(name=name, args=args)
+    return env
+
+
+def test_python_reward_terms_match_native_terms():
+    def native(cfg):
+        pass
+
+    def python(cfg):
+        cfg.rewards.scales.lin_vel_z_py = cfg.rewards.scales.lin_vel_z
+        cfg.rewards.scales.action_rate_py = cfg.rewards.scales.action_rate
+        cfg.rewards.scales.lin_vel_z = 0.0
+        cfg.rewards.scales.action_rate = 0.0
+
+    envs = [_make("go2_native", LeggedRobot, native), _make("go2_pyterms", Go2WithPythonTerms, python)]
+    nat, py = envs
+    assert not nat._py_rewards and [n for n, _ in py._py_rewards] == ["action_rate_py", "lin_vel_z_py"]
+    assert py.task_params.defer_reward_total == 1 and py.task_params.num_extra_sums == 2
+    for e in envs:
+        e.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    rename = {"lin_vel_z": "lin_vel_z_py", "action_rate": "action_rate_py"}
+    for step in range(60):
+        a = 0.6 * torch.randn(256, 12, device="cuda", generator=g)
+        if step == 30:  # a batch of time-outs: resets, extras
+            for e in envs:
+                e.episode_length_buf = torch.full_like(e.episode_length_buf, int(e.max_episode_length))
+        outs = [e.step(a) for e in envs]
+        (o1, _, r1, d1, x1), (o2, _, r2, d2, x2) = outs
+        assert torch.equal(o1, o2) and torch.equal(d1, d2)  # the state never depends on the rewards
+        # only the summation order of the terms differs (native terms first, then Python ones)
+        torch.testing.assert_close(r2, r1, rtol=1e-5, atol=1e-6)
+        for k in nat._sum_names:
+            torch.testing.assert_close(py.episode_sums[rename.get(k, k)], nat.episode_sums[k], rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(x2["episode"]["rew_" + rename.get(k, k)], x1["episode"]["rew_" + k],
+                                       rtol=1e-4, atol=1e-7)
+    assert d1.any()
+
+
+def test_reset_idx_subset_through_the_python_api():
+    env = _make("go2_subset", LeggedRobot, lambda cfg: None)
+    env.reset()
+    for _ in range(20):
+        env.step(0.5 * torch.randn(256, 12, device="cuda"))
+    ids = torch.tensor([3, 17, 200], device="cuda")
+    sums = env._episode_sums[:, ids].clone()
+    keep = torch.ones(256, dtype=torch.bool, device="cuda")
+    keep[ids] = False
+    root_keep = env.root_states[keep].clone()
+    env.reset_idx(ids)
+    assert (env.episode_length_buf[ids] == 0).all() and (env.actions[ids] == 0).all()
+    assert env.reset_buf[ids].all()
+    assert torch.equal(env.root_states[keep], root_keep)
+    assert (env._episode_sums[:, ids] == 0).all()
+    want = (sums.mean(dim=1) / env.max_episode_length_s).cpu().numpy()
+    got = np.array([float(env.extras["episode"]["rew_" + k]) for k in env._sum_names])
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
+    env.step(torch.zeros(256, 12, device="cuda"))  # the env keeps stepping normally

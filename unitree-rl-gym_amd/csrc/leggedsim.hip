@@ -620,7 +620,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int j = k + 1; j < n; ++j) {
             if (!l_nz<D, CH>(j, k)) continue;  // L_jk == 0: no update (compile-time after unrolling)
             const float ljk = rl(m[k], j);
-            m[j] = m[j] - m[k] * ljk;
+            m[j] = fmaf(-m[k], ljk, m[j]);  // fused, as the oracle's cholesky()
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -639,7 +639,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         asm volatile("" : "+v"(ln));
         x = ln == i ? x * idg : x;
         const float xi = rl(x, i);
-        x = ln > i ? x - m[i] * xi : x;
+        x = ln > i ? fmaf(-m[i], xi, x) : x;
     }
     __syncthreads();
     {
@@ -652,7 +652,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             asm volatile("" : "+v"(ln));
             x = ln == i ? x * idg : x;
             const float xi = rl(x, i);
-            x = ln < i ? x - lc[i] * xi : x;
+            x = ln < i ? fmaf(-lc[i], xi, x) : x;
         }
     }
     // free velocity (classical velocity of the root origin after dt); lane i holds
@@ -780,7 +780,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int i = 0; i < n; ++i) y[i] = used ? s.u.con.Y[lane][i] : 0.f;
 #pragma unroll
-        for (int i = 0; i < n; ++i) v += y[i] * s.qf[i];
+        for (int i = 0; i < n; ++i) v = fmaf(y[i], s.qf[i], v);
         // leaves-first order (register renaming only), then row i of L and 1/L_ii as
         // wave-uniform LDS reads (16-byte row loads on the LDS pipe) instead of ~170
         // v_readlane broadcasts on the VALU; structurally zero L entries are skipped
@@ -793,7 +793,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             float t = yp[i];
 #pragma unroll
             for (int k = 0; k < i; ++k)
-                if (l_nz<D, CH>(i, k)) t -= Li[k] * yp[k];
+                if (l_nz<D, CH>(i, k)) t = fmaf(-Li[k], yp[k], t);
             yp[i] = t * s.Linv[i];
             // pinned per row: with the sparse joint rows independent the scheduler
             // otherwise runs them all at once and spills at the 128-VGPR (4 waves/SIMD)
@@ -907,7 +907,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                         l1 *= sc; l2 *= sc;
                     }
                     const float d1 = l1 - l1o, d2 = l2 - l2o;
-                    v += acol[r + 1] * d1 + acol[r + 2] * d2;
+                    v = fmaf(acol[r + 2], d2, fmaf(acol[r + 1], d1, v));
                     lam = lid == r ? ln : (lid == r + 1 ? l1 : (lid == r + 2 ? l2 : lam));
                 }
             }
@@ -930,13 +930,13 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
-                z += s.u.con.Y[3 * c][lane] * rl(lam, 3 * c);
-                z += s.u.con.Y[3 * c + 1][lane] * rl(lam, 3 * c + 1);
-                z += s.u.con.Y[3 * c + 2][lane] * rl(lam, 3 * c + 2);
+                z = fmaf(s.u.con.Y[3 * c][lane], rl(lam, 3 * c), z);
+                z = fmaf(s.u.con.Y[3 * c + 1][lane], rl(lam, 3 * c + 1), z);
+                z = fmaf(s.u.con.Y[3 * c + 2][lane], rl(lam, 3 * c + 2), z);
             }
 #pragma unroll
         for (int l = 0; l < LM; ++l)
-            if (l < nlimit) z += s.u.con.Y[3 * CM + l][lane] * rl(lam, 3 * CM + l);
+            if (l < nlimit) z = fmaf(s.u.con.Y[3 * CM + l][lane], rl(lam, 3 * CM + l), z);
     }
     {
         float lc[n];
@@ -948,7 +948,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             asm volatile("" : "+v"(ln));
             z = ln == i ? z * idg : z;
             const float zi = rl(z, i);
-            z = ln < i ? z - lc[i] * zi : z;
+            z = ln < i ? fmaf(-lc[i], zi, z) : z;
         }
     }
     // back to the natural order: lane i < n holds qd' of index n-1-i
@@ -1370,8 +1370,8 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
         const int reset = s.flags[0], timeout = s.flags[1];
         float rew = 0.f;
         for (int k = 0; k < T.num_rewards; ++k) rew += s.u.post.terms[k];
-        if (T.only_positive_rewards) rew = fmaxf(rew, 0.f);
-        if (T.has_termination_reward) {
+        if (T.only_positive_rewards && !T.defer_reward_total) rew = fmaxf(rew, 0.f);
+        if (T.has_termination_reward && !T.defer_reward_total) {
             float r = ((reset && !timeout) ? 1.f : 0.f) * T.termination_scale;
             rew += r;
             E.episode_sums[(size_t)T.num_rewards * N + e] += r;
@@ -1382,22 +1382,44 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
     }
 }
 
+// episode-sum rows: native terms, termination, then the caller's (Python) terms
+__device__ __forceinline__ int num_sums(const lgs_task_params& T) {
+    return T.num_rewards + (T.has_termination_reward ? 1 : 0) + T.num_extra_sums;
+}
+
 // reset modes of post_physics: the control step (reset decided by check_termination),
 // BaseTask.reset (every env, no episode extras), reset_idx(env_ids) (the masked envs:
 // episode sums into the extras accumulator, reset_buf set, legged_robot.py:723-768)
 enum { RESET_STEP = 0, RESET_ALL = 1, RESET_IDS = 2 };
 
+// post_physics parts: everything, only up to the rewards (lgs_post_physics_rewards), or
+// the rest from the state the first part left in the env buffers (lgs_post_physics_finish)
+enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
+
 template <int D, int B, int ROWS>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
-                             const float* rbs, int N, int e, uint32_t step, int reset_mode) {
+                             const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL) {
     const int lane = threadIdx.x;
     const int A = T.num_actions;
     const uint64_t seed = T.seed;
     const bool force_reset = reset_mode != RESET_STEP;
-    if (!force_reset) {
-        post_physics_scalar(s, T, E, rbs, N, e, step);
-    } else {
+    if (force_reset) {
         if (lane == 0) s.flags[0] = 1;
+    } else if (part != PART_FINISH) {
+        post_physics_scalar(s, T, E, rbs, N, e, step);
+        if (part == PART_REWARDS) return;
+    } else if (lane == 0) {  // the first part's results: reset decision, base-frame state, commands
+        s.flags[0] = E.reset[e];
+        s.flags[1] = E.time_out[e];
+        for (int i = 0; i < 3; ++i) {
+            s.u.post.misc[i] = E.base_lin_vel[3 * e + i];
+            s.u.post.misc[3 + i] = E.base_ang_vel[3 * e + i];
+            s.u.post.misc[6 + i] = E.projected_gravity[3 * e + i];
+        }
+        s.u.post.misc[9] = E.phase ? E.phase[e] : 0.f;
+        s.u.post.misc[10] = E.leg_phase ? E.leg_phase[2 * e] : 0.f;
+        s.u.post.misc[11] = E.leg_phase ? E.leg_phase[2 * e + 1] : 0.f;
+        for (int i = 0; i < 4; ++i) s.u.post.misc[12 + i] = E.commands[4 * e + i];
     }
     __syncthreads();
     const int reset = s.flags[0];
@@ -1425,14 +1447,14 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         if (lane < 6) s.root[7 + lane] = rv;
         if (reset_mode == RESET_IDS && lane == 0) E.reset[e] = 1;  // reset_buf[env_ids] = 1 (:758)
         if (reset_mode != RESET_ALL) {
-            const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+            const int nsum = num_sums(T);
             if (lane < nsum) {
                 atomicAdd(E.episode_acc + lane, E.episode_sums[(size_t)lane * N + e]);
                 E.episode_sums[(size_t)lane * N + e] = 0.f;
             }
             if (lane == 0) atomicAdd(E.episode_acc + nsum, 1.f);
         } else {
-            const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+            const int nsum = num_sums(T);
             if (lane < nsum) E.episode_sums[(size_t)lane * N + e] = 0.f;
         }
         if (lane == 0) {
@@ -1491,7 +1513,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
 // (clip, decimation x (PD + substep), torques, body states: lgs_step_physics) and the
 // post-physics stack on the bound state (lgs_post_physics).  STEP == PHYSICS then POST,
 // bit for bit: the post half reads back exactly what the physics half stored.
-enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2 };
+enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MODE_POST_FINISH = 4 };
 
 template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? LGS_WAVES_PER_EU : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
@@ -1507,7 +1529,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     const int A = T.num_actions;
     float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * B * e : nullptr;
     STAMP_INIT();
-    if (mode != MODE_POST) {
+    if (mode == MODE_STEP || mode == MODE_PHYSICS) {
         float a = 0.f;
         if (lane < A) {
             const float* ain = E.actions_in ? E.actions_in : E.actions;
@@ -1542,7 +1564,9 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
     }
     __syncthreads();
     STAMP(15);
-    if (mode != MODE_PHYSICS) post_physics(s, T, E, rbs, N, e, step, RESET_STEP);
+    if (mode != MODE_PHYSICS)
+        post_physics(s, T, E, rbs, N, e, step, RESET_STEP,
+                     mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL));
     __syncthreads();
     STAMP(16);
     store_state(s, st, e);
@@ -1576,7 +1600,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
 __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
                                                       int N, int advance) {
     const lgs_task_params& T = *Tp;
-    const int nsum = T.num_rewards + (T.has_termination_reward ? 1 : 0);
+    const int nsum = num_sums(T);
     const float cnt = E.episode_acc[nsum];
     const bool any = cnt > 0.f;
     const int t = threadIdx.x;
@@ -1881,7 +1905,8 @@ LGS_API int lgs_set_dof_state_indexed(lgs_sim* s, const float* src, const int32_
 LGS_API int lgs_set_task(lgs_sim* s, const lgs_task_params* t) {
     if (!s || !t) return set_err(LGS_ERR_ARG, "null argument");
     if (t->num_actions != s->D) return set_err(LGS_ERR_ARG, "lgs_set_task: num_actions must equal num_dofs");
-    if (t->num_obs > LGS_MAX_OBS || t->num_privileged_obs > LGS_MAX_OBS || t->num_rewards > LGS_MAX_REWARDS)
+    if (t->num_obs > LGS_MAX_OBS || t->num_privileged_obs > LGS_MAX_OBS || t->num_rewards > LGS_MAX_REWARDS ||
+        t->num_extra_sums < 0 || t->num_rewards + 1 + t->num_extra_sums > WAVE - 1)
         return set_err(LGS_ERR_ARG, "lgs_set_task: obs/reward counts exceed limits");
     if (t->num_feet > LGS_MAX_FEET || t->resample_interval <= 0 || t->push_interval <= 0 || t->decimation <= 0)
         return set_err(LGS_ERR_ARG, "lgs_set_task: invalid feet count / intervals / decimation");
@@ -1904,7 +1929,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     DevState st = state_of(s);
     LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     HIP_TRY(hipGetLastError());
-    if (mode != MODE_PHYSICS) {  // extras of the step's resets, episode_acc zeroed, step counter advanced
+    if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1);
         HIP_TRY(hipGetLastError());
     }
@@ -1921,6 +1946,14 @@ LGS_API int lgs_step_physics(lgs_sim* s, const lgs_env_buffers* env, int64_t ste
 
 LGS_API int lgs_post_physics(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
     return launch_step(s, env, step_counter, MODE_POST, "lgs_post_physics");
+}
+
+LGS_API int lgs_post_physics_rewards(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_POST_REWARDS, "lgs_post_physics_rewards");
+}
+
+LGS_API int lgs_post_physics_finish(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_POST_FINISH, "lgs_post_physics_finish");
 }
 
 LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {

@@ -247,14 +247,23 @@ class LeggedRobot(BaseTask):
         return torch.tensor(self.spec.noise_scale_vec, device=self.device)
 
     def _prepare_reward_function(self):
-        """Drop zero scales, multiply the rest by dt; dict order = alphabetical (:817-840)."""
+        """Drop zero scales, multiply the rest by dt; dict order = alphabetical (:817-840).
+
+        Terms the kernel knows run inside the fused step.  A term it does not know is looked
+        up as ``self._reward_<name>`` like the reference does (a task subclass may define it);
+        such Python terms run between the two halves of the post-physics stack, on the same
+        pre-reset state the reference's compute_reward sees (step() then takes the split path:
+        lgs_step_physics, lgs_post_physics_rewards, the Python terms, lgs_post_physics_finish)."""
         self.reward_scales = dict(self.spec.reward_scales)
         self.reward_names = list(self.spec.reward_names)
+        self._native_reward_names, self._py_rewards = [], []
         for n in self.reward_names:
-            rid = cabi.REWARD_ALIASES.get(n, n)
-            if rid not in cabi.REWARD_ID:
-                raise AttributeError(f"'{type(self).__name__}' has no native reward term '_reward_{n}'")
-        self._sum_names = list(self.spec.sum_names)
+            if cabi.REWARD_ALIASES.get(n, n) in cabi.REWARD_ID:
+                self._native_reward_names.append(n)
+            else:  # AttributeError like the reference's getattr (:834) when the task has no such method
+                self._py_rewards.append((n, getattr(self, "_reward_" + n)))
+        py_names = [n for n, _ in self._py_rewards]
+        self._sum_names = [n for n in self.spec.sum_names if n not in py_names] + py_names
         nsum = len(self._sum_names)
         self._episode_sums = torch.zeros(nsum, self.num_envs, dtype=torch.float, device=self.device)
         self.episode_sums = {name: self._episode_sums[i] for i, name in enumerate(self._sum_names)}
@@ -328,7 +337,8 @@ class LeggedRobot(BaseTask):
 
     # ------------------------------------------------------------ step ------
     def step(self, actions):
-        """Apply actions, simulate `decimation` substeps, post-physics; one launch."""
+        """Apply actions, simulate `decimation` substeps, post-physics; one launch (three
+        launches and the Python terms when the task defines Python reward terms)."""
         self._sync_stream()
         self._buf_idx ^= 1
         i = self._buf_idx
@@ -345,7 +355,14 @@ class LeggedRobot(BaseTask):
         # reference's per-reset tensors; inside a captured rollout, one per step)
         snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
         E.ep_snapshot = snap.data_ptr()
-        self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
+        if self._py_rewards:
+            self.sim.step_physics(E, self._step_mirror)
+            self.sim.post_physics_rewards(E, self._step_mirror)
+            self.reset_buf, self.time_out_buf = self._reset_bufs[i], self._timeout_bufs[i]
+            self._python_rewards()
+            self.sim.post_physics_finish(E, self._step_mirror)
+        else:
+            self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
         self._step_mirror += 1
         self.obs_buf = self._obs_bufs[i]
         self.privileged_obs_buf = self._priv_bufs[i]
@@ -355,6 +372,22 @@ class LeggedRobot(BaseTask):
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self._time_outs
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    def _python_rewards(self):
+        """compute_reward (legged_robot.py:770-787) for the Python terms: the kernel left the
+        raw sum of its own terms in rew_buf (defer_reward_total); add these terms (scale
+        already times dt), then the only_positive_rewards clip and the termination term."""
+        nat = len(self._native_reward_names) + (1 if "termination" in self.reward_scales else 0)
+        for k, (name, fn) in enumerate(self._py_rewards):
+            rew = fn() * self.reward_scales[name]
+            self.rew_buf += rew
+            self._episode_sums[nat + k] += rew
+        if self.cfg.rewards.only_positive_rewards:
+            self.rew_buf[:] = torch.clip(self.rew_buf[:], min=0.0)
+        if "termination" in self.reward_scales:
+            rew = (self.reset_buf & ~self.time_out_buf).float() * self.reward_scales["termination"]
+            self.rew_buf += rew
+            self.episode_sums["termination"] += rew
 
     def reset_idx(self, env_ids):
         """reset_idx (legged_robot.py:723-768) for any subset of envs: one masked launch

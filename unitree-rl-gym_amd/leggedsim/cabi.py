@@ -92,6 +92,7 @@ class TaskParams(C.Structure):
         ("seed", C.c_uint64),
         ("write_body_states", C.c_int32),
         ("custom_origins", C.c_int32),
+        ("defer_reward_total", C.c_int32), ("num_extra_sums", C.c_int32),
     ]
 
 

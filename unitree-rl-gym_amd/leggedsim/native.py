@@ -65,13 +65,16 @@ def load():
     lib.lgs_step_physics.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_post_physics.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_reset_idx.argtypes = [vp, C.POINTER(cabi.EnvBuffers), vp, C.c_int64]
+    lib.lgs_post_physics_rewards.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_post_physics_finish.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
                  "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
                  "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield",
-                 "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx"):
+                 "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards",
+                 "lgs_post_physics_finish"):
         getattr(lib, name).restype = C.c_int
     _LIB = lib
     return lib
@@ -87,7 +90,7 @@ EXPORTED_SYMBOLS = [
     "lgs_set_env_properties", "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
-    "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx",
+    "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
 ]
 
 
@@ -148,6 +151,14 @@ class Sim:
 
     def post_physics(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_post_physics(self.handle, C.byref(env_bufs), step_counter), "lgs_post_physics")
+
+    def post_physics_rewards(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_post_physics_rewards(self.handle, C.byref(env_bufs), step_counter),
+              "lgs_post_physics_rewards")
+
+    def post_physics_finish(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_post_physics_finish(self.handle, C.byref(env_bufs), step_counter),
+              "lgs_post_physics_finish")
 
     def reset_idx(self, env_bufs: cabi.EnvBuffers, mask_u8, step_counter: int):
         assert mask_u8.is_cuda and mask_u8.numel() == self.num_envs and mask_u8.element_size() == 1

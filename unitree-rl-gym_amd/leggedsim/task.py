@@ -83,8 +83,12 @@ def build_task_params(env) -> cabi.TaskParams:
     hip = list(env.hip_dof_indices)
     T.num_hip = len(hip)
     T.hip_dofs[: len(hip)] = hip
-    T.num_rewards = len(env.reward_names)
-    for k, n in enumerate(env.reward_names):
+    native = list(getattr(env, "_native_reward_names", env.reward_names))
+    py = [n for n, _ in getattr(env, "_py_rewards", [])]
+    T.num_rewards = len(native)
+    T.defer_reward_total = int(bool(py))
+    T.num_extra_sums = len(py)
+    for k, n in enumerate(native):
         T.reward_ids[k] = cabi.REWARD_ID[cabi.REWARD_ALIASES.get(n, n)]
         T.reward_scales[k] = float(env.reward_scales[n])
     T.has_termination_reward = int("termination" in env.reward_scales)
