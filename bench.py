@@ -94,13 +94,17 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch of the env-step kernel from the committed rocprofv3
-    PMC summary (profiles/pmc_k_step.json, written by tools/pmc_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+# the committed rocprofv3 summaries of the current build (tools/gpu_round2_profile.sh)
+PROFILE_DIR = os.path.join(ROOT, "profiles", "round2", "go2_4096")
+
+
+def load_pmc():
+    """HBM bytes per launch of the env-step kernel from the committed rocprofv3 PMC summary
+    (FETCH_SIZE / WRITE_SIZE in separate passes, each calibrated on a 1 GiB copy in the same
+    pass: tools/pmc_summary.py), or None."""
     try:
-        with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+        with open(os.path.join(PROFILE_DIR, "pmc_k_step.json")) as f:
+            return json.load(f)
     except Exception:
         return None
 
@@ -115,7 +119,7 @@ def load_sq_valu(kernel_ms):
     rocprofv3 SQ summary (profiles/sq_k_step.json, tools/sq_summary.py) over the live launch
     time.  The env step is latency-bound, so this, not GB/s, is its meaningful
     utilisation figure; reported beside the HBM roofline the contract asks for."""
-    path = os.path.join(ROOT, "profiles", "sq_k_step.json")
+    path = os.path.join(PROFILE_DIR, "sq_k_step.json")
     try:
         with open(path) as f:
             sq = json.load(f)
@@ -381,6 +385,7 @@ def main():
         return
     bytes_per_launch = GO2_BYTES_PER_ENV_STEP * N
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    pmc = load_pmc() or {}
     line = {
         "metric": "env-steps/sec + PPO-iter wall-time, Go2 4096 envs/GPU at 1/2/4/8 MI355X",
         "value": round(value, 1),
@@ -402,8 +407,10 @@ def main():
         "rollout_env_steps_per_s": round(rollout, 1),
         "env_step_kernel_ms": round(kernel_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc_traffic(),
-                     "kernel": "k_step<12,19,32> (fused Go2 control step)",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch"),
+                     "traffic_read_write": [pmc.get("read_bytes_per_launch"), pmc.get("write_bytes_per_launch")],
+                     "traffic_profile_avg_ns": pmc.get("avg_ns"),
+                     "kernel": pmc.get("kernel", "k_step (fused Go2 control step)"),
                      "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms)},
     }
     if world == 1 and not args.no_other_configs:

@@ -1,4 +1,11 @@
-"""Env-only workload for rocprofv3 passes: Go2 x 4096 fused control steps."""
+"""Env-only workload for rocprofv3 passes: Go2 x 4096 fused control steps.
+
+Also runs a calibration copy of a known byte count (CAL_BYTES read + CAL_BYTES written,
+float4 streaming, larger than the 256 MiB Infinity Cache) in the same process, so a PMC
+pass carries its own reference: tools/pmc_summary.py scales the k_step FETCH_SIZE /
+WRITE_SIZE by known / measured of that copy (MI355X_MICROARCH.md §HBM: calibrate on a
+known byte count before trusting an absolute).
+"""
 import os
 import sys
 
@@ -11,8 +18,21 @@ import isaacgym  # noqa: F401,E402
 from legged_gym.envs import task_registry  # noqa: E402
 from legged_gym.utils import get_args  # noqa: E402
 
+CAL_BYTES = 1 << 30  # 1 GiB read + 1 GiB written per calibration copy
+
+
+def calibrate(reps=3):
+    src = torch.ones(CAL_BYTES // 4, device="cuda")
+    dst = torch.empty_like(src)
+    for _ in range(reps):
+        dst.copy_(src)
+    torch.cuda.synchronize()
+    del src, dst
+    torch.cuda.empty_cache()
+
 
 def main(task="go2", n=4096, steps=100):
+    calibrate()
     args = get_args(["--task", task, "--num_envs", str(n), "--headless"])
     env, _ = task_registry.make_env(name=task, args=args)
     env.reset()

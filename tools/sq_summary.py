@@ -18,10 +18,14 @@ def load(path, kernel="k_step<"):
     if os.path.isdir(path):
         path = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)[0]
     d = collections.defaultdict(list)
+    name = None
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"]:
             d[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: statistics.mean(v) for k, v in d.items()}
+            name = r["Kernel_Name"]
+    out = {k: statistics.mean(v) for k, v in d.items()}
+    out["_name"] = name
+    return out
 
 
 def main(p1, p2, out):
@@ -30,7 +34,7 @@ def main(p1, p2, out):
     waves = c.get("SQ_WAVES", 4096.0)
     wc = c["SQ_WAVE_CYCLES"]
     res = {
-        "kernel": "k_step<12,19,32> (Go2, 4096 envs, one wave per env)",
+        "kernel": c.get("_name"),
         "waves_per_launch": waves,
         "valu_insts_per_launch": c["SQ_INSTS_VALU"],
         "lds_insts_per_launch": c["SQ_INSTS_LDS"],
