@@ -62,6 +62,8 @@
 #define LGS_MAX_CONTACT_BODIES 16
 #define LGS_MAX_OBS 128
 #define LGS_MAX_REWARDS 24
+#define LGS_MAX_SELF_PROXIES 64
+#define LGS_MAX_SELF_PAIRS 192
 
 /* ---- articulated model (host pointers; see leggedsim/model.py) ---------- */
 typedef struct lgs_model_desc {
@@ -106,6 +108,26 @@ typedef struct lgs_sim_params {
     int32_t max_rows;                /* constraint rows per env (<= compiled capacity);
                                         joint-limit rows are capped at max_rows - 3*max_contacts */
 } lgs_sim_params;
+
+/* ---- self-collision (IsaacGym create_actor collision filter, legged_robot.py:373-374:
+ *      cfg.asset.self_collisions == 0 lets the links of one actor collide; see
+ *      leggedsim/selfcollision.py).  Every collision shape group is a capsule proxy in its
+ *      body frame; the listed proxy pairs (never a body with itself or its parent) are
+ *      tested every substep: closest points of the two segments, signed distance minus both
+ *      radii and rest_offset, active below contact_offset.  A touching pair is one contact
+ *      (normal from the second body to the first, a friction pair, the env's shape friction)
+ *      in the slots after the ground contacts; up to max_self_contacts of them per substep,
+ *      first in pair order, and the ground contacts are then capped at max_contacts minus
+ *      the self contacts taken.  The contact force joins both bodies' net contact force
+ *      with opposite signs.                                                            */
+typedef struct lgs_self_collision_desc {
+    int32_t num_proxies;          /* S <= LGS_MAX_SELF_PROXIES                          */
+    const int32_t* proxy_body;    /* [S]                                                */
+    const float* capsule;         /* [S][7] segment end points p0, p1 (body frame), radius */
+    int32_t num_pairs;            /* Q <= LGS_MAX_SELF_PAIRS; 0 disables self-collision  */
+    const int32_t* pair;          /* [Q][2] proxy indices                               */
+    int32_t max_self_contacts;    /* contact slots self contacts may take per substep    */
+} lgs_self_collision_desc;
 
 /* ---- task (env) parameters: everything post_physics_step reads from cfg ---- */
 enum lgs_obs_layout {
@@ -302,6 +324,10 @@ LGS_API int lgs_reset_idx(lgs_sim* sim, const lgs_env_buffers* env, const uint8_
  * Replaces the z = 0 plane for every env; heights = NULL (or rows = 0) restores the plane. */
 LGS_API int lgs_set_heightfield(lgs_sim* sim, const int16_t* heights, int32_t rows, int32_t cols,
                                 float horizontal_scale, float vertical_scale, float border_size);
+
+/* create_actor(..., self_collisions, 0) (legged_robot.py:373-374): the self-collision
+ * proxies and pairs of every env (host descriptor, copied; NULL or num_pairs = 0: off) */
+LGS_API int lgs_set_self_collision(lgs_sim* sim, const lgs_self_collision_desc* desc);
 
 /* name/index queries */
 LGS_API int lgs_get_counts(lgs_sim* sim, int32_t* num_envs, int32_t* num_bodies, int32_t* num_dofs);

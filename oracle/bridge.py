@@ -88,10 +88,30 @@ def set_ground(lib, terrain=None, terrain_cfg=None):
                             float(terrain_cfg.border_size))
 
 
+_self = None  # the self-collision arrays the oracle points at (kept alive here)
+
+
+def set_self_collision(lib, sc=None):
+    """Give the oracle an env's self-collision proxies and pairs (None: off)."""
+    global _self
+    if sc is None or len(sc.pairs) == 0:
+        lib.orc_set_self_collision(None)
+        _self = None
+        return
+    _self = cabi.SelfCollisionHandle(sc)
+    lib.orc_set_self_collision(C.byref(_self.desc))
+
+
+def set_env(lib, env):
+    """Ground and self-collision of a live env."""
+    set_ground(lib, getattr(env, "terrain", None), env.cfg.terrain)
+    set_self_collision(lib, getattr(env, "self_collision", None))
+
+
 def step(env, snap, actions, step_counter, lib=None):
     """One fused control step of every env on the CPU oracle.  Returns new arrays."""
     lib = lib or ensure_built()
-    set_ground(lib, getattr(env, "terrain", None), env.cfg.terrain)
+    set_env(lib, env)
     b = {k: (None if v is None else np.ascontiguousarray(v).copy()) for k, v in snap.items()}
     b["actions"] = np.ascontiguousarray(actions, dtype=np.float32).copy()
     b["episode_acc"][:] = 0
@@ -104,10 +124,12 @@ def step(env, snap, actions, step_counter, lib=None):
     return b
 
 
-def step_raw(model, sim_params, task, num_envs, bufs, step_counter, lib=None, terrain=None, terrain_cfg=None):
+def step_raw(model, sim_params, task, num_envs, bufs, step_counter, lib=None, terrain=None, terrain_cfg=None,
+             self_collision=None):
     """orc_step on caller-provided host arrays (bench cpu_baseline / golden tests)."""
     lib = lib or ensure_built()
     set_ground(lib, terrain, terrain_cfg)
+    set_self_collision(lib, self_collision)
     mh = cabi.ModelHandle(model)
     E = _env_struct(bufs)
     p = lambda a: a.ctypes.data  # noqa: E731

@@ -21,7 +21,9 @@
  *       origin; composite-rigid-body mass matrix, recursive Newton-Euler bias,
  *       dense Cholesky; joint limits + point contacts vs the z=0 plane as
  *       unilateral rows solved by projected Gauss-Seidel with a circular friction
- *       cone; semi-implicit Euler.  PARITY UNPINNED vs PhysX; pinned only by
+ *       cone; capsule-proxy self-collision between links of one actor
+ *       (create_actor's self_collisions filter, legged_robot.py:373-374);
+ *       semi-implicit Euler.  PARITY UNPINNED vs PhysX; pinned only by
  *       analytic tests (free fall, resting height, momentum) and HIP==oracle.
  */
 #include <math.h>
@@ -125,6 +127,76 @@ static void matvec(const float R[9], const float v[3], float o[3]) {
     float y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
     float z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
     o[0] = x; o[1] = y; o[2] = z;
+}
+static float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+/* ---- self-collision (lgs_set_self_collision semantics, include/leggedsim.h): capsule
+ * proxies in body frames and the proxy pairs tested every substep.  Set once per process
+ * by orc_set_self_collision (test infrastructure). */
+static struct {
+    int npairs, max_self;
+    int body[LGS_MAX_SELF_PAIRS][2];
+    float cap[LGS_MAX_SELF_PAIRS][2][7];
+} g_self;
+
+void orc_set_self_collision(const lgs_self_collision_desc* d) {
+    g_self.npairs = 0;
+    g_self.max_self = 0;
+    if (!d || d->num_pairs <= 0) return;
+    int Q = d->num_pairs < LGS_MAX_SELF_PAIRS ? d->num_pairs : LGS_MAX_SELF_PAIRS;
+    for (int q = 0; q < Q; ++q)
+        for (int h = 0; h < 2; ++h) {
+            int px = d->pair[2 * q + h];
+            g_self.body[q][h] = d->proxy_body[px];
+            memcpy(g_self.cap[q][h], d->capsule + 7 * px, sizeof(float) * 7);
+        }
+    g_self.npairs = Q;
+    g_self.max_self = d->max_self_contacts;
+}
+
+/* closest points of segments p1-q1 and p2-q2 (Ericson, Real-Time Collision Detection,
+ * 5.1.9: parameters s, t of the two segments clamped to [0, 1]) */
+static void seg_closest(const float p1[3], const float q1[3], const float p2[3], const float q2[3], float c1[3],
+                        float c2[3]) {
+    float d1[3], d2[3], r[3];
+    for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+    float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    float s = 0.f, t = 0.f;
+    const float eps = 1e-12f;
+    if (a <= eps && e <= eps) {
+        /* both degenerate: the two points */
+    } else if (a <= eps) {
+        t = clampf(f / e, 0.f, 1.f);
+    } else {
+        float c = dot3(d1, r);
+        if (e <= eps) {
+            s = clampf(-c / a, 0.f, 1.f);
+        } else {
+            float b = dot3(d1, d2);
+            float den = a * e - b * b;
+            s = (den != 0.f) ? clampf((b * f - c * e) / den, 0.f, 1.f) : 0.f;
+            t = (b * s + f) / e;
+            if (t < 0.f) {
+                t = 0.f;
+                s = clampf(-c / a, 0.f, 1.f);
+            } else if (t > 1.f) {
+                t = 1.f;
+                s = clampf((b - c) / a, 0.f, 1.f);
+            }
+        }
+    }
+    for (int k = 0; k < 3; ++k) { c1[k] = p1[k] + d1[k] * s; c2[k] = p2[k] + d2[k] * t; }
+}
+
+/* friction frame of a self contact: e = x unless n is within 55 degrees of x (then y),
+ * t1 = normalise(e - (e.n) n), t2 = n x t1 */
+static void self_tangents(const float n[3], float t1[3], float t2[3]) {
+    float a[3];
+    if (fabsf(n[0]) < 0.57735f) { a[0] = 1.f - n[0] * n[0]; a[1] = 0.f - n[0] * n[1]; a[2] = 0.f - n[0] * n[2]; }
+    else { a[0] = 0.f - n[1] * n[0]; a[1] = 1.f - n[1] * n[1]; a[2] = 0.f - n[1] * n[2]; }
+    float inv = 1.f / sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    for (int k = 0; k < 3; ++k) t1[k] = a[k] * inv;
+    cross3(n, t1, t2);
 }
 static void matmul(const float A[9], const float B[9], float C[9]) {
     float T[9];
@@ -435,8 +507,9 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     static __thread float J[ROWMAX][NMAX];
     float tgt[ROWMAX], lam[ROWMAX], v[ROWMAX];
     int kind[ROWMAX]; /* 0 unilateral, 1 friction pair head, 2 friction pair tail */
-    int cb[ROWMAX / 3 + 1];
-    float mu = 0.5f * (sp->ground_friction + shape_friction);
+    int cb[ROWMAX / 3 + 1], cb2[ROWMAX / 3 + 1];
+    float cmu[ROWMAX / 3 + 1];                           /* friction coefficient per contact */
+    const float mu = 0.5f * (sp->ground_friction + shape_friction); /* ground: average with the plane */
     int nr = 0;
     const float beta = sp->baumgarte;
     const int max_rows = sp->max_rows < ROWMAX ? sp->max_rows : ROWMAX;
@@ -444,8 +517,45 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     int nc = 0;
     float cpt[ROWMAX / 3 + 1][3];
     float cfr[ROWMAX / 3 + 1][3][3]; /* contact frame: normal, tangent 1, tangent 2 */
+    /* self contacts first (pair order, at most max_self of them), so the ground leaves their
+     * slots free; they join the row list after the ground contacts */
+    int nsc = 0, sc_body[ROWMAX / 3 + 1][2];
+    float sc_pt[ROWMAX / 3 + 1][3], sc_sep[ROWMAX / 3 + 1], sc_n[ROWMAX / 3 + 1][3];
+    {
+        int maxs = g_self.max_self < sp->max_contacts ? g_self.max_self : sp->max_contacts;
+        for (int q = 0; q < g_self.npairs && nsc < maxs; ++q) {
+            float seg[2][2][3];
+            for (int h = 0; h < 2; ++h) {
+                int b = g_self.body[q][h];
+                for (int e = 0; e < 2; ++e) {
+                    matvec(K.R[b], g_self.cap[q][h] + 3 * e, seg[h][e]);
+                    for (int k = 0; k < 3; ++k) seg[h][e][k] += K.p[b][k];
+                }
+            }
+            float c1[3], c2[3];
+            seg_closest(seg[0][0], seg[0][1], seg[1][0], seg[1][1], c1, c2);
+            float dx[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
+            float dist = sqrtf(dot3(dx, dx));
+            float nrm[3] = {0.f, 0.f, 1.f};
+            if (dist > 1e-9f) {
+                float inv = 1.f / dist;
+                for (int k = 0; k < 3; ++k) nrm[k] = dx[k] * inv;
+            }
+            float ra = g_self.cap[q][0][6], rb = g_self.cap[q][1][6];
+            float sep = dist - ra - rb - sp->rest_offset;
+            if (!(sep < sp->contact_offset)) continue;
+            sc_body[nsc][0] = g_self.body[q][0];
+            sc_body[nsc][1] = g_self.body[q][1];
+            for (int k = 0; k < 3; ++k) {
+                sc_pt[nsc][k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
+                sc_n[nsc][k] = nrm[k];
+            }
+            sc_sep[nsc] = sep;
+            ++nsc;
+        }
+    }
     for (int k = 0; k < md->num_points; ++k) {
-        if (nc >= sp->max_contacts || nr + 3 > max_rows) break;
+        if (nc >= sp->max_contacts - nsc || nr + 3 > max_rows) break;
         int b = md->pt_body[k];
         float c[3];
         matvec(K.R[b], md->pt_pos + 3 * k, c);
@@ -481,6 +591,48 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         tgt[nr + 1] = tgt[nr + 2] = 0.f;
         kind[nr] = 0; kind[nr + 1] = 1; kind[nr + 2] = 2;
         cb[nc] = b;
+        cb2[nc] = -1;
+        cmu[nc] = mu;
+        memcpy(cpt[nc], pc, 12);
+        nr += 3;
+        ++nc;
+    }
+    /* the self contacts: rows J_a(pc) d - J_b(pc) d (the floating-base columns cancel) */
+    for (int i = 0; i < nsc; ++i) {
+        const int a = sc_body[i][0], b = sc_body[i][1];
+        const float* pc = sc_pt[i];
+        float dirs[3][3];
+        memcpy(dirs[0], sc_n[i], 12);
+        self_tangents(sc_n[i], dirs[1], dirs[2]);
+        memcpy(cfr[nc], dirs, 36);
+        for (int dd = 0; dd < 3; ++dd) {
+            const float* d = dirs[dd];
+            float* row = J[nr + dd];
+            memset(row, 0, sizeof(float) * n);
+            for (int l = 1; l <= md->depth[a]; ++l) {
+                int x = md->chain[a * LGS_MAX_DEPTH + l];
+                int j = md->dof[x];
+                if (j < 0) continue;
+                float rp[3] = {pc[0] - K.p[x][0], pc[1] - K.p[x][1], pc[2] - K.p[x][2]}, t[3];
+                cross3(K.aw[x], rp, t);
+                row[6 + j] = dot3(d, t);
+            }
+            for (int l = 1; l <= md->depth[b]; ++l) {
+                int x = md->chain[b * LGS_MAX_DEPTH + l];
+                int j = md->dof[x];
+                if (j < 0) continue;
+                float rp[3] = {pc[0] - K.p[x][0], pc[1] - K.p[x][1], pc[2] - K.p[x][2]}, t[3];
+                cross3(K.aw[x], rp, t);
+                row[6 + j] = row[6 + j] - dot3(d, t);
+            }
+        }
+        const float sep = sc_sep[i];
+        tgt[nr] = sep >= 0.f ? -sep * idt : fminf(-beta * sep * idt, sp->max_depenetration_velocity);
+        tgt[nr + 1] = tgt[nr + 2] = 0.f;
+        kind[nr] = 0; kind[nr + 1] = 1; kind[nr + 2] = 2;
+        cb[nc] = a;
+        cb2[nc] = b;
+        cmu[nc] = shape_friction; /* both shapes carry the env's friction: their average */
         memcpy(cpt[nc], pc, 12);
         nr += 3;
         ++nc;
@@ -530,7 +682,7 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
                 lam[r] = ln;
                 for (int s = 0; s < nr; ++s) v[s] = fmaf(A[s][r], d, v[s]); /* the kernel's fused update */
             } else if (kind[r] == 1) {
-                float lim = mu * lam[r - 1];
+                float lim = cmu[r / 3] * lam[r - 1];
                 float l1 = lam[r] - v[r] * inv[r];
                 float l2 = lam[r + 1] - v[r + 1] * inv[r + 1];
                 float nrm = sqrtf(l1 * l1 + l2 * l2);
@@ -566,6 +718,11 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         float* F = cforce + 3 * cb[c];
         for (int t = 0; t < 3; ++t) /* ln n + l1 t1 + l2 t2 */
             F[t] += (lam[r] * cfr[c][0][t] + lam[r + 1] * cfr[c][1][t] + lam[r + 2] * cfr[c][2][t]) * idt;
+        if (cb2[c] >= 0) { /* a self contact pushes its second body the other way */
+            float* G = cforce + 3 * cb2[c];
+            for (int t = 0; t < 3; ++t)
+                G[t] -= (lam[r] * cfr[c][0][t] + lam[r + 1] * cfr[c][1][t] + lam[r + 2] * cfr[c][2][t]) * idt;
+        }
     }
     (void)cpt;
     /* integrate (semi-implicit Euler) */
@@ -1066,6 +1223,7 @@ long orc_sizeof(int which) {
     case 1: return (long)sizeof(lgs_sim_params);
     case 2: return (long)sizeof(lgs_task_params);
     case 3: return (long)sizeof(lgs_env_buffers);
+    case 4: return (long)sizeof(lgs_self_collision_desc);
     default: return -1;
     }
 }

@@ -11,6 +11,7 @@ from legged_gym.envs.base.env_spec import derive_env_spec
 from legged_gym.utils import task_registry
 from leggedsim import cabi
 from leggedsim.model import MODELS_DIR, Model
+from leggedsim.selfcollision import build_self_collision
 from leggedsim.task import build_task_params
 
 MODEL_FILE = {"go2": "go2", "g1": "g1_12dof", "h1": "h1", "h1_2": "h1_2_12dof"}
@@ -30,6 +31,12 @@ def make_spec(task, cfg_edit=None):
     spec.task = build_task_params(spec)
     spec.sim_params = cabi.sim_params_from_cfg(cfg.sim, cfg.asset, max_contacts=cls.max_contacts,
                                                max_rows=cls.max_rows, ground_friction=float(cfg.terrain.static_friction))
+    # the env's self-collision proxies/pairs (LeggedRobot.create_sim); the oracle only uses them
+    # when a test hands them over (bridge.set_self_collision)
+    spec.self_collision = None
+    if int(getattr(cfg.asset, "self_collisions", 1)) == 0:
+        spec.self_collision = build_self_collision(model, np.asarray(spec.default_dof_pos).reshape(-1),
+                                                   max_self_contacts=cls.max_self_contacts)
     return spec
 
 

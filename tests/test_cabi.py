@@ -33,7 +33,8 @@ def test_library_exports_every_declared_symbol():
 
 def test_ctypes_structs_match_c_layout(oracle_lib):
     oracle_lib.orc_sizeof.restype = C.c_long
-    for i, st in enumerate((cabi.ModelDesc, cabi.SimParams, cabi.TaskParams, cabi.EnvBuffers)):
+    for i, st in enumerate((cabi.ModelDesc, cabi.SimParams, cabi.TaskParams, cabi.EnvBuffers,
+                            cabi.SelfCollisionDesc)):
         assert C.sizeof(st) == oracle_lib.orc_sizeof(i), st.__name__
 
 

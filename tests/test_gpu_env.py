@@ -126,6 +126,7 @@ def test_gymapi_style_substep_matches_oracle():
     env.sim.simulate(tau)
     torch.cuda.synchronize()
     lib = bridge.ensure_built()
+    bridge.set_env(lib, env)
     mh = cabi.ModelHandle(env.model)
     root, dofs = snap["root"].copy(), snap["dofs"].copy()
     cf, rbs = snap["cforce"].copy(), snap["rbs"].copy()

@@ -172,6 +172,7 @@ def test_post_physics_entry_matches_reference_golden(task):
     # the oracle on the same inputs: bit-exact
     lib = bridge.ensure_built()
     bridge.set_ground(lib)
+    bridge.set_self_collision(lib)
     Eh = bridge._env_struct(host)
     mh = cabi.ModelHandle(spec.model)
     p = lambda a: a.ctypes.data  # noqa: E731
@@ -219,7 +220,7 @@ def test_post_physics_on_hip_physics_state_matches_oracle_exactly(task):
 
 def bridge_post(env, snap, step):
     lib = bridge.ensure_built()
-    bridge.set_ground(lib, getattr(env, "terrain", None), env.cfg.terrain)
+    bridge.set_env(lib, env)
     b = {k: (None if v is None else np.ascontiguousarray(v).copy()) for k, v in snap.items()}
     b["episode_acc"][:] = 0
     mh = cabi.ModelHandle(env.model)

@@ -110,6 +110,10 @@ struct DevSim {
     const int16_t* hf;
     int hf_rows, hf_cols;
     float hf_inv_hs, hf_vs, hf_border;
+    // self-collision (lgs_set_self_collision): n_selfp pair records of 16 floats,
+    // [p0(3) p1(3) r body] of the first proxy then of the second; n_selfp == 0: off
+    const float4* selfp;
+    int n_selfp, max_self;
 };
 
 struct DevState {
@@ -251,6 +255,48 @@ __device__ __forceinline__ void contact_tangents(const float* n, float* t1, floa
 }
 __device__ __forceinline__ float clipf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
+// ------------------------------------------------------- self-collision --
+// Closest points c1, c2 of the segments p1q1 and p2q2 (Ericson, Real-Time Collision
+// Detection 5.1.9).  Same arithmetic as oracle/lgs_oracle.c seg_closest().
+__device__ __forceinline__ void seg_closest(const float* p1, const float* q1, const float* p2, const float* q2,
+                                            float* c1, float* c2) {
+    const float d1[3] = {q1[0] - p1[0], q1[1] - p1[1], q1[2] - p1[2]};
+    const float d2[3] = {q2[0] - p2[0], q2[1] - p2[1], q2[2] - p2[2]};
+    const float r[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    const float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    const float eps = 1e-12f;
+    float s, t;
+    if (a <= eps && e <= eps) {
+        s = 0.f; t = 0.f;
+    } else if (a <= eps) {
+        s = 0.f; t = clipf(f / e, 0.f, 1.f);
+    } else {
+        const float c = dot3(d1, r);
+        if (e <= eps) {
+            t = 0.f; s = clipf(-c / a, 0.f, 1.f);
+        } else {
+            const float b = dot3(d1, d2);
+            const float den = a * e - b * b;
+            s = den != 0.f ? clipf((b * f - c * e) / den, 0.f, 1.f) : 0.f;
+            t = (b * s + f) / e;
+            if (t < 0.f) { t = 0.f; s = clipf(-c / a, 0.f, 1.f); }
+            else if (t > 1.f) { t = 1.f; s = clipf((b - c) / a, 0.f, 1.f); }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { c1[k] = p1[k] + d1[k] * s; c2[k] = p2[k] + d2[k] * t; }
+}
+// friction frame of a self contact: t1 = normalise(e - (e.n) n) with e = x, or y when n is
+// within 55 degrees of x; t2 = n x t1
+__device__ __forceinline__ void self_tangents(const float* n, float* t1, float* t2) {
+    float a0, a1, a2;
+    if (fabsf(n[0]) < 0.57735f) { a0 = 1.f - n[0] * n[0]; a1 = 0.f - n[0] * n[1]; a2 = 0.f - n[0] * n[2]; }
+    else { a0 = 0.f - n[1] * n[0]; a1 = 1.f - n[1] * n[1]; a2 = 0.f - n[1] * n[2]; }
+    const float inv = 1.f / sqrtf(a0 * a0 + a1 * a1 + a2 * a2);
+    t1[0] = a0 * inv; t1[1] = a1 * inv; t1[2] = a2 * inv;
+    cross3(n, t1, t2);
+}
+
 // ------------------------------------------------------------ LDS layout --
 // Model topology/geometry cached in LDS at kernel start: every chain walk and
 // subtree test below is an LDS access instead of a dependent global load.
@@ -303,6 +349,9 @@ struct Smem {
     float qf[n];
     float tgt[ROWS];
     int c_body[ROWS / 3];
+    int c_body2[ROWS / 3];    // self contact: the second body (its force enters with a minus sign)
+    int sc_ab[ROWS / 3][2];   // self contacts of this substep before their slots are known
+    float sc_tmp[ROWS / 3][7];  // point(3), separation, normal(3)
     float c_pt[ROWS / 3][3];
     float c_fr[ROWS / 3][9];  // contact frame: normal, tangent 1, tangent 2
     float c_sep[ROWS / 3];
@@ -676,9 +725,63 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // Gauss-Seidel order: contacts ascending, then limits (oracle's row order).
     constexpr int CM = ROWS / 4, LM = ROWS - 3 * CM;
     const float beta = sp.beta;
-    int nc = 0;
+    int nc = 0, ncg = 0;  // contacts, of which the first ncg are ground contacts
     {
-        const int maxc = sp.max_contacts < CM ? sp.max_contacts : CM;
+        const int maxc_all = sp.max_contacts < CM ? sp.max_contacts : CM;
+        // self contacts (lane per proxy pair, first max_self in pair order) are found first,
+        // so the ground contacts can leave them their slots; they are appended below
+        int nsc = 0;
+        if (sp.n_selfp > 0) {
+            const int maxs = sp.max_self < maxc_all ? sp.max_self : maxc_all;
+            for (int base = 0; base < sp.n_selfp && nsc < maxs; base += WAVE) {
+                const int q = base + lane;
+                bool act = false;
+                float pc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 1.f}, sep = 0.f;
+                int ba = 0, bb = 0;
+                if (q < sp.n_selfp) {
+                    const float4* rec = sp.selfp + 4 * q;
+                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+                    ba = __float_as_int(r1.w);
+                    bb = __float_as_int(r3.w);
+                    float Ra[9], Rb[9];
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) { Ra[t] = s.R[ba][t]; Rb[t] = s.R[bb][t]; }
+                    const float a0[3] = {r0.x, r0.y, r0.z}, a1[3] = {r0.w, r1.x, r1.y};
+                    const float b0[3] = {r2.x, r2.y, r2.z}, b1[3] = {r2.w, r3.x, r3.y};
+                    float pa0[3], pa1[3], pb0[3], pb1[3];
+                    matvec(Ra, a0, pa0); matvec(Ra, a1, pa1); matvec(Rb, b0, pb0); matvec(Rb, b1, pb1);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        pa0[k] += s.p[ba][k]; pa1[k] += s.p[ba][k];
+                        pb0[k] += s.p[bb][k]; pb1[k] += s.p[bb][k];
+                    }
+                    float c1[3], c2[3];
+                    seg_closest(pa0, pa1, pb0, pb1, c1, c2);
+                    const float dx[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
+                    const float dist = sqrtf(dot3(dx, dx));
+                    if (dist > 1e-9f) {
+                        const float inv = 1.f / dist;
+                        nrm[0] = dx[0] * inv; nrm[1] = dx[1] * inv; nrm[2] = dx[2] * inv;
+                    }
+                    const float ra = r1.z, rb = r3.z;
+                    sep = dist - ra - rb - sp.rest_offset;
+                    act = sep < sp.contact_offset;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) pc[k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
+                }
+                const uint64_t mask = __ballot(act);
+                const int slot = nsc + __popcll(mask & ((1ull << lane) - 1ull));
+                if (act && slot < maxs) {
+                    s.sc_ab[slot][0] = ba; s.sc_ab[slot][1] = bb;
+                    float* t = s.sc_tmp[slot];
+                    t[0] = pc[0]; t[1] = pc[1]; t[2] = pc[2]; t[3] = sep;
+                    t[4] = nrm[0]; t[5] = nrm[1]; t[6] = nrm[2];
+                }
+                nsc += __popcll(mask);
+                if (nsc > maxs) nsc = maxs;
+            }
+        }
+        const int maxc = maxc_all - nsc;
         for (int base = 0; base < md.P && nc < maxc; base += WAVE) {
             const int k = base + lane;
             bool act = false;
@@ -715,6 +818,26 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             }
             nc += __popcll(mask);
             if (nc > maxc) nc = maxc;
+        }
+        ncg = nc;
+        if (nsc > 0) {
+            __syncthreads();
+            if (lane < nsc) {
+                const int slot = ncg + lane;
+                s.c_body[slot] = s.sc_ab[lane][0];
+                s.c_body2[slot] = s.sc_ab[lane][1];
+                const float* t = s.sc_tmp[lane];
+                s.c_pt[slot][0] = t[0]; s.c_pt[slot][1] = t[1]; s.c_pt[slot][2] = t[2];
+                s.c_sep[slot] = t[3];
+                const float nrm[3] = {t[4], t[5], t[6]};
+                float t1[3], t2[3];
+                self_tangents(nrm, t1, t2);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    s.c_fr[slot][k] = nrm[k]; s.c_fr[slot][3 + k] = t1[k]; s.c_fr[slot][6 + k] = t2[k];
+                }
+            }
+            nc = ncg + nsc;
         }
     }
     int nlimit;
@@ -754,8 +877,11 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         cross3(r, d, rxd);
         float* row = s.u.con.Y[lane];
         for (int i = 0; i < n; ++i) row[i] = 0.f;
-        row[0] = rxd[0]; row[1] = rxd[1]; row[2] = rxd[2];
-        row[3] = d[0]; row[4] = d[1]; row[5] = d[2];
+        const bool self = cc >= ncg;
+        if (!self) {  // ground: J(pc) d of body b; a self contact's base columns cancel to 0
+            row[0] = rxd[0]; row[1] = rxd[1]; row[2] = rxd[2];
+            row[3] = d[0]; row[4] = d[1]; row[5] = d[2];
+        }
         const int dep = mc.depth[b];
         for (int l = 1; l <= dep; ++l) {
             const int a = mc.chain[b][l];
@@ -765,6 +891,19 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             float aw[3] = {s.aw[a][0], s.aw[a][1], s.aw[a][2]};
             cross3(aw, rp, t);
             row[6 + j] = dot3(d, t);
+        }
+        if (self) {  // minus J(pc) d of the second body (shared ancestors cancel exactly)
+            const int b2 = s.c_body2[cc];
+            const int dep2 = mc.depth[b2];
+            for (int l = 1; l <= dep2; ++l) {
+                const int a = mc.chain[b2][l];
+                const int j = mc.dof[a];
+                if (j < 0) continue;
+                float rp[3] = {pc[0] - s.p[a][0], pc[1] - s.p[a][1], pc[2] - s.p[a][2]}, t[3];
+                float aw[3] = {s.aw[a][0], s.aw[a][1], s.aw[a][2]};
+                cross3(aw, rp, t);
+                row[6 + j] = row[6 + j] - dot3(d, t);
+            }
         }
         const float sep = s.c_sep[cc];
         s.tgt[lane] = dd != 0 ? 0.f : (sep >= 0.f ? -sep * idt : fminf(-beta * sep * idt, sp.max_depen));
@@ -871,7 +1010,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     float lam = 0.f;  // lane r holds lambda_r (one VGPR; read by v_readlane)
     {
-        const float mu = 0.5f * (sp.ground_friction + shape_mu);
+        const float mu = 0.5f * (sp.ground_friction + shape_mu);  // ground contacts
+        const float mus = shape_mu;  // self contacts: both shapes carry the env's friction
         float tg = used ? s.tgt[lane] : 0.f;
         // the diagonal comes from the lane's own row (above), not a 32-way select over
         // acol (32 lane masks, which spilled SGPRs into VGPR lanes)
@@ -898,7 +1038,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                     v = fmaf(acol[r], dn, v);
                     const float v1n = fmaf(rl(acol[r], r + 1), dn, v1);
                     const float v2n = fmaf(rl(acol[r], r + 2), dn, v2);
-                    const float lim = mu * ln;
+                    const float lim = (c < ncg ? mu : mus) * ln;
                     float l1 = l1o - v1n * rl(inv, r + 1);
                     float l2 = l2o - v2n * rl(inv, r + 2);
                     const float nrm = sqrtf(l1 * l1 + l2 * l2);
@@ -964,8 +1104,13 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
                 const float ln = rl(lam, 3 * c), l1 = rl(lam, 3 * c + 1), l2 = rl(lam, 3 * c + 2);
+                if (c >= ncg && s.c_body2[c] == lane) {  // self contact: the reaction on the second body
+                    const float* fr = s.c_fr[c];
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) F[t] -= (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) * idt;
+                }
                 if (s.c_body[c] == lane) {
-                    if (sp.hf) {
+                    if (sp.hf || c >= ncg) {
                         const float* fr = s.c_fr[c];  // world force = ln n + l1 t1 + l2 t2
 #pragma unroll
                         for (int t = 0; t < 3; ++t) F[t] += (ln * fr[t] + l1 * fr[3 + t] + l2 * fr[6 + t]) * idt;
@@ -1642,6 +1787,7 @@ struct lgs_sim {
     const float* torques = nullptr;
     lgs_task_params* task_dev = nullptr;
     int16_t* hf_mem = nullptr;
+    float4* self_mem = nullptr;
     int has_task = 0;
     int rows = 32;
     int chain = 0;  // dof_chain_length of the model
@@ -1787,6 +1933,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     sp.armature = p->armature; sp.clamp_qd = p->clamp_joint_velocity; sp.max_contacts = p->max_contacts;
     sp.max_rows = p->max_rows;
     sp.hf = nullptr; sp.hf_rows = sp.hf_cols = 0; sp.hf_inv_hs = sp.hf_vs = sp.hf_border = 0.f;
+    sp.selfp = nullptr; sp.n_selfp = 0; sp.max_self = 0;
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
     HIP_TRY(hipMemset(s->added_mass, 0, sizeof(float) * num_envs));
@@ -1808,6 +1955,7 @@ LGS_API int lgs_destroy_sim(lgs_sim* s) {
     (void)hipFree(s->added_mass);
     (void)hipFree(s->task_dev);
     (void)hipFree(s->hf_mem);
+    (void)hipFree(s->self_mem);
     delete s;
     return LGS_OK;
 }
@@ -1831,6 +1979,49 @@ LGS_API int lgs_set_heightfield(lgs_sim* s, const int16_t* heights, int32_t rows
     s->sp.hf_inv_hs = 1.0f / horizontal_scale;
     s->sp.hf_vs = vertical_scale;
     s->sp.hf_border = border_size;
+    return LGS_OK;
+}
+
+LGS_API int lgs_set_self_collision(lgs_sim* s, const lgs_self_collision_desc* d) {
+    if (!s) return set_err(LGS_ERR_ARG, "null sim");
+    if (d && d->num_pairs > 0) {
+        if (d->num_pairs > LGS_MAX_SELF_PAIRS || d->num_proxies <= 0 || d->num_proxies > LGS_MAX_SELF_PROXIES ||
+            !d->proxy_body || !d->capsule || !d->pair || d->max_self_contacts < 0 ||
+            d->max_self_contacts > s->sp.max_contacts)
+            return set_err(LGS_ERR_ARG, "lgs_set_self_collision: need 0 < num_pairs <= LGS_MAX_SELF_PAIRS, 0 < num_proxies <= "
+                                        "LGS_MAX_SELF_PROXIES, 0 <= max_self_contacts <= max_contacts");
+        for (int i = 0; i < d->num_proxies; ++i)
+            if (d->proxy_body[i] < 0 || d->proxy_body[i] >= s->B)
+                return set_err(LGS_ERR_ARG, "lgs_set_self_collision: proxy body out of range");
+        for (int q = 0; q < 2 * d->num_pairs; ++q)
+            if (d->pair[q] < 0 || d->pair[q] >= d->num_proxies)
+                return set_err(LGS_ERR_ARG, "lgs_set_self_collision: pair proxy index out of range");
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));  // no step may still read the previous pairs
+    (void)hipFree(s->self_mem);
+    s->self_mem = nullptr;
+    s->sp.selfp = nullptr;
+    s->sp.n_selfp = 0;
+    s->sp.max_self = 0;
+    if (!d || d->num_pairs <= 0) return LGS_OK;
+    // one 64-byte record per pair: [p0 p1 r body] of each proxy (the lane's four float4 loads)
+    const int Q = d->num_pairs;
+    float* host = (float*)malloc(sizeof(float) * 16 * Q);
+    for (int q = 0; q < Q; ++q)
+        for (int h = 0; h < 2; ++h) {
+            const int px = d->pair[2 * q + h];
+            float* o = host + 16 * q + 8 * h;
+            for (int k = 0; k < 7; ++k) o[k] = d->capsule[7 * px + k];
+            int32_t b = d->proxy_body[px];
+            memcpy(o + 7, &b, 4);
+        }
+    hipError_t e = hipMalloc(&s->self_mem, sizeof(float) * 16 * Q);
+    if (e == hipSuccess) e = hipMemcpy(s->self_mem, host, sizeof(float) * 16 * Q, hipMemcpyHostToDevice);
+    free(host);
+    if (e != hipSuccess) return set_err(LGS_ERR_HIP, std::string("lgs_set_self_collision: ") + hipGetErrorString(e));
+    s->sp.selfp = s->self_mem;
+    s->sp.n_selfp = Q;
+    s->sp.max_self = d->max_self_contacts;
     return LGS_OK;
 }
 

@@ -12,6 +12,7 @@ class HumanoidRobot(LeggedRobot):
     obs_layout = cabi.OBS_HUMANOID
     max_contacts = 12
     max_rows = 48
+    max_self_contacts = 4
 
     def _init_buffers(self):
         super()._init_buffers()

@@ -28,6 +28,7 @@ from legged_gym.envs.base.base_task import BaseTask
 from legged_gym.utils.helpers import class_to_dict
 from leggedsim import cabi, native
 from leggedsim.model import load_model
+from leggedsim.selfcollision import build_self_collision
 from leggedsim.task import build_task_params
 from legged_gym.utils.terrain import Terrain
 
@@ -40,6 +41,7 @@ class LeggedRobot(BaseTask):
     hip_dof_indices = ()
     max_contacts = 8
     max_rows = 32
+    max_self_contacts = 2  # contact slots self contacts may take per substep (cfg.asset.self_collisions == 0)
 
     def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
         self.cfg = cfg
@@ -119,6 +121,12 @@ class LeggedRobot(BaseTask):
         self.sim = native.Sim(model, sp, self.num_envs, self.sim_device_id)
         self.sim.set_env_properties(friction, added_mass)
         self.shape_friction = friction
+        # create_actor(..., self_collisions, 0) (:373-374): 0 lets the links of one robot collide
+        self.self_collision = None
+        if int(getattr(self.cfg.asset, "self_collisions", 1)) == 0:
+            self.self_collision = build_self_collision(model, np.asarray(spec.default_dof_pos).reshape(-1),
+                                                       max_self_contacts=self.max_self_contacts)
+            self.sim.set_self_collision(self.self_collision)
         if self.terrain is not None:
             self._create_heightfield()
         else:

@@ -17,6 +17,8 @@ MAX_FEET = 4
 MAX_CONTACT_BODIES = 16
 MAX_OBS = 128
 MAX_REWARDS = 24
+MAX_SELF_PROXIES = 64
+MAX_SELF_PAIRS = 192
 
 OBS_QUADRUPED = 0
 OBS_HUMANOID = 1
@@ -56,6 +58,25 @@ class SimParams(C.Structure):
         ("baumgarte", C.c_float), ("ground_friction", C.c_float), ("armature", C.c_float),
         ("clamp_joint_velocity", C.c_int32), ("max_contacts", C.c_int32), ("max_rows", C.c_int32),
     ]
+
+
+class SelfCollisionDesc(C.Structure):
+    _fields_ = [
+        ("num_proxies", C.c_int32), ("proxy_body", i32p), ("capsule", f32p),
+        ("num_pairs", C.c_int32), ("pair", i32p), ("max_self_contacts", C.c_int32),
+    ]
+
+
+class SelfCollisionHandle:
+    """Keeps the numpy arrays alive behind a SelfCollisionDesc (leggedsim.selfcollision.SelfCollision)."""
+
+    def __init__(self, sc):
+        self.body = np.ascontiguousarray(sc.proxy_body, dtype=np.int32)
+        self.caps = np.ascontiguousarray(sc.capsules, dtype=np.float32).reshape(-1)
+        self.pairs = np.ascontiguousarray(sc.pairs, dtype=np.int32).reshape(-1)
+        self.desc = SelfCollisionDesc(len(self.body), self.body.ctypes.data_as(i32p), self.caps.ctypes.data_as(f32p),
+                                      len(self.pairs) // 2, self.pairs.ctypes.data_as(i32p),
+                                      int(sc.max_self_contacts))
 
 
 class TaskParams(C.Structure):
@@ -207,4 +228,6 @@ def load_oracle():
     lib.orc_set_heightfield.restype = None
     lib.orc_terrain_sample.argtypes = [C.c_float, C.c_float, vp]
     lib.orc_terrain_sample.restype = C.c_float
+    lib.orc_set_self_collision.argtypes = [C.POINTER(SelfCollisionDesc)]
+    lib.orc_set_self_collision.restype = None
     return lib

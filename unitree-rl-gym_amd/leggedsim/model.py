@@ -51,6 +51,7 @@ class Model:
     pt_body: np.ndarray       # [P] int32
     pt_pos: np.ndarray        # [P, 3]
     pt_radius: np.ndarray     # [P]
+    pt_shape: np.ndarray = None  # [P] int32 URDF link whose collision shapes the point belongs to
 
     @property
     def num_bodies(self):
@@ -78,7 +79,10 @@ class Model:
         z = np.load(path, allow_pickle=False)
         meta = json.loads(bytes(z["meta"]).decode())
         kw = {k: z[k] for k in z.files if k != "meta"}
-        return Model(meta["name"], meta["body_names"], meta["dof_names"], **kw)
+        m = Model(meta["name"], meta["body_names"], meta["dof_names"], **kw)
+        if m.pt_shape is None:  # a model saved before shapes were recorded: one shape per body
+            m.pt_shape = m.pt_body.copy()
+        return m
 
     def reorder_points(self, first_bodies):
         """Put the contact candidates of ``first_bodies`` first (contact-slot priority
@@ -88,6 +92,7 @@ class Model:
         self.pt_body = self.pt_body[order].copy()
         self.pt_pos = self.pt_pos[order].copy()
         self.pt_radius = self.pt_radius[order].copy()
+        self.pt_shape = self.pt_shape[order].copy()
 
 
 def _shape_points(s):
@@ -137,12 +142,14 @@ def model_from_articulation(name, art: Articulation) -> Model:
     for i, b in enumerate(art.bodies):
         I = b.link.inertia
         inertia[i] = [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
-    pb, pp, pr = [], [], []
+    pb, pp, pr, ps = [], [], [], []
+    groups = {}  # (body, URDF link) -> id: the shapes a link declared, after fixed-joint collapse
     for i, b in enumerate(art.bodies):
         for s in b.link.shapes:
+            g = groups.setdefault((i, s.link), len(groups))
             pts, rads = _shape_points(s)
             for p, r in zip(pts, rads):
-                pb.append(i); pp.append(p); pr.append(r)
+                pb.append(i); pp.append(p); pr.append(r); ps.append(g)
     dof_body = np.zeros(D, dtype=np.int32)
     for i, b in enumerate(art.bodies):
         if b.dof >= 0:
@@ -163,6 +170,7 @@ def model_from_articulation(name, art: Articulation) -> Model:
         pt_body=np.array(pb, dtype=np.int32).reshape(-1),
         pt_pos=f32(np.array(pp).reshape(-1, 3)),
         pt_radius=f32(pr),
+        pt_shape=np.array(ps, dtype=np.int32).reshape(-1),
     )
 
 

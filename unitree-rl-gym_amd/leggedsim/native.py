@@ -69,12 +69,13 @@ def load():
     lib.lgs_post_physics_finish.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
+    lib.lgs_set_self_collision.argtypes = [vp, C.POINTER(cabi.SelfCollisionDesc)]
     for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
                  "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
                  "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield",
                  "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards",
-                 "lgs_post_physics_finish"):
+                 "lgs_post_physics_finish", "lgs_set_self_collision"):
         getattr(lib, name).restype = C.c_int
     _LIB = lib
     return lib
@@ -91,6 +92,7 @@ EXPORTED_SYMBOLS = [
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
+    "lgs_set_self_collision",
 ]
 
 
@@ -131,6 +133,16 @@ class Sim:
         check(self.lib, self.lib.lgs_set_heightfield(self.handle, hf.ctypes.data, hf.shape[0], hf.shape[1],
                                                      float(horizontal_scale), float(vertical_scale),
                                                      float(border_size)), "lgs_set_heightfield")
+
+    def set_self_collision(self, sc):
+        """create_actor's self-collision filter (legged_robot.py:373-374): sc is a
+        leggedsim.selfcollision.SelfCollision, or None to turn self-collision off."""
+        if sc is None or len(sc.pairs) == 0:
+            check(self.lib, self.lib.lgs_set_self_collision(self.handle, None), "lgs_set_self_collision")
+            self._sc = None
+            return
+        self._sc = cabi.SelfCollisionHandle(sc)
+        check(self.lib, self.lib.lgs_set_self_collision(self.handle, C.byref(self._sc.desc)), "lgs_set_self_collision")
 
     def bind(self, root, dofs, cforce, rbs):
         for t in (root, dofs, cforce, rbs):

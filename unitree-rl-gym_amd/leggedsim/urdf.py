@@ -57,6 +57,7 @@ class Shape:
     half_length: float = 0.0  # capsule half segment length (along shape z)
     half_extents: np.ndarray = None  # box
     points: np.ndarray = None  # (k,3) hull support points in shape frame
+    link: str = ""            # URDF link the shape was declared on (kept through fixed-joint collapse)
 
 
 @dataclass
@@ -148,12 +149,12 @@ def parse_urdf(path, mesh_points=16):
             pos = _vec(o.get("xyz") if o is not None else None)
             g = c.find("geometry")[0]
             if g.tag == "sphere":
-                link.shapes.append(Shape("sphere", rot, pos, radius=float(g.get("radius"))))
+                link.shapes.append(Shape("sphere", rot, pos, radius=float(g.get("radius")), link=link.name))
             elif g.tag == "cylinder":
                 link.shapes.append(Shape("capsule", rot, pos, radius=float(g.get("radius")),
-                                         half_length=0.5 * float(g.get("length"))))
+                                         half_length=0.5 * float(g.get("length")), link=link.name))
             elif g.tag == "box":
-                link.shapes.append(Shape("box", rot, pos, half_extents=0.5 * _vec(g.get("size"))))
+                link.shapes.append(Shape("box", rot, pos, half_extents=0.5 * _vec(g.get("size")), link=link.name))
             elif g.tag == "mesh":
                 fn = g.get("filename")
                 if fn.startswith("package://"):
@@ -163,7 +164,7 @@ def parse_urdf(path, mesh_points=16):
                     continue  # e.g. blobs listed in the reference's .MISSING_LARGE_BLOBS
                 scale = _vec(g.get("scale"), default=1.0) if g.get("scale") else np.ones(3)
                 pts = hull_support_points(read_stl(mp) * scale, mesh_points)
-                link.shapes.append(Shape("points", rot, pos, points=pts))
+                link.shapes.append(Shape("points", rot, pos, points=pts, link=link.name))
         links[link.name] = link
     joints = []
     for j in root.findall("joint"):
@@ -208,7 +209,7 @@ def _merge_into(parent: Link, child: Link, rot, pos):
     parent.mass, parent.com = m, com
     for s in child.shapes:
         parent.shapes.append(Shape(s.kind, rot @ s.rot, rot @ s.pos + pos, s.radius, s.half_length,
-                                   s.half_extents, s.points))
+                                   s.half_extents, s.points, s.link))
 
 
 @dataclass
