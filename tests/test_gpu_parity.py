@@ -347,3 +347,16 @@ def test_reset_idx_subset_matches_oracle(task):
     want = sums_before[:, mask == 1].mean(axis=1) / env.max_episode_length_s
     have = np.array([float(ep["rew_" + k]) for k in env._sum_names])
     np.testing.assert_allclose(have, want, rtol=1e-5, atol=1e-7)
+
+
+def test_two_envs_per_wave_is_bitwise_one_env_per_wave(monkeypatch):
+    """k_step carries two Go2 envs per wave (lanes 0-31 / 32-63) at even env counts; the
+    one-env-per-wave kernel (LGS_ENVS_PER_WAVE=1, read at lgs_create_sim) must give the same
+    bits for every buffer over a rollout with resets."""
+    outs = []
+    for epw in ("1", "2"):
+        monkeypatch.setenv("LGS_ENVS_PER_WAVE", epw)
+        env, g = warm("go2", 512, steps=60, seed=11)
+        outs.append(env_arrays(env))
+        env.close()
+    assert_exact(outs[1], outs[0], STATE + POST, 512, "two envs per wave vs one")

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -132,6 +133,27 @@ __device__ __forceinline__ float rl(float x, int l) {
 __device__ __forceinline__ int rli(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 // wave-uniform copy (SGPR) of a value that is identical in every lane
 __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+
+// ---- envs per wave.  EPW = 1: one env per 64-lane wave.  EPW = 2: two envs per wave in
+// lanes 0-31 and 32-63 (the Go2 variant: every per-env phase fits in 32 lanes, ROWS <= 32),
+// so half as many waves carry the same envs and the lane-per-body / per-DOF / per-row
+// phases use 2x the lanes.  hl = the lane within its env, hh = which env of the wave;
+// bc(x, r) = x of lane r of this lane's env; hballot = the ballot of this lane's env.
+template <int EPW> __device__ __forceinline__ int hl() { return EPW == 2 ? (int)(threadIdx.x & 31u) : (int)threadIdx.x; }
+template <int EPW> __device__ __forceinline__ int hh() { return EPW == 2 ? (int)(threadIdx.x >> 5) : 0; }
+// Broadcast with ds_bpermute (the LDS crossbar: one instruction, no SGPR round trip and
+// no readlane hazard wait).  The source lane must be active: every call sits outside
+// lane-divergent branches (only whole-env conditions, which keep the env's lanes together).  Two envs per wave: 0.230 -> 0.203 ms per Go2 4096-env step
+// against two v_readlane + select; one env per wave: -1 % on H1 8192 against v_readlane.
+template <int EPW> __device__ __forceinline__ float bc(float x, int r) {
+    return __int_as_float(
+        __builtin_amdgcn_ds_bpermute((int)(((EPW == 2 ? (threadIdx.x & 32u) : 0u) + (unsigned)r) << 2), __float_as_int(x)));
+}
+template <int EPW> __device__ __forceinline__ uint64_t hballot(bool p) {
+    const uint64_t m = __ballot(p);
+    if constexpr (EPW == 1) return m;
+    else return (m >> (threadIdx.x & 32u)) & 0xffffffffull;
+}
 
 __device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
     float x = a[1] * b[2] - a[2] * b[1];
@@ -314,7 +336,6 @@ struct Smem {
     static constexpr int n = 6 + D;
     static constexpr int NP = (n % 2 == 0) ? n + 1 : n;     // odd row stride: conflict-free columns
     static constexpr int AS = (ROWS % 2 == 0) ? ROWS + 1 : ROWS;
-    ModelCache<D, B> mc;
     float root[16];
     float q[D], qd[D], tau[D], act[D];
     float R[B][9], p[B][3], aw[B][3], cw[B][3];
@@ -363,10 +384,10 @@ struct Smem {
 #endif
 };
 
-template <int D, int B, int ROWS>
-__device__ __forceinline__ void load_model(Smem<D, B, ROWS>& s, const DevModel& md) {
+// the whole workgroup fills the block's (shared) model cache
+template <int D, int B>
+__device__ __forceinline__ void load_model(ModelCache<D, B>& c, const DevModel& md) {
     const int lane = threadIdx.x;
-    ModelCache<D, B>& c = s.mc;
     if (lane < B) {
         const int j = md.dof[lane];
         c.dof[lane] = j;
@@ -423,14 +444,15 @@ __host__ __device__ constexpr bool l_nz(int i, int k) {  // may L[i][k] (i > k) 
     return CH == 0 || k >= D || i >= D || i <= k + (D - 1 - k) % CH;
 }
 
-template <int D, int B, int ROWS, int CH>
-__device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& sp, float added_mass, float shape_mu) {
+template <int D, int B, int ROWS, int CH, int EPW>
+__device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const DevModel& md, const DevSim& sp,
+                        float added_mass, float shape_mu) {
     constexpr int n = 6 + D;
-    const ModelCache<D, B>& mc = s.mc;
+    Smem<D, B, ROWS>& s = sm[hh<EPW>()];
     // Opaque lane id: lane-derived addresses are recomputed each substep (a few VALU
     // ops) instead of being hoisted out of the decimation loop and held live across
     // every substep, which pushed the 4-waves/SIMD build into scratch.
-    int lane = threadIdx.x;
+    int lane = hl<EPW>();
     asm volatile("" : "+v"(lane));
     const float dt = sp.dt;
     const float idt = 1.0f / dt;  // every per-row / per-force division by dt is a multiply (as the oracle)
@@ -658,7 +680,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         // spilled to VGPR lanes
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const float d = sqrtf(fmaxf(rl(m[k], k), 1e-12f));
+        const float d = sqrtf(fmaxf(bc<EPW>(m[k], k), 1e-12f));
         const float inv = 1.0f / d;
         // Lanes above the diagonal (i < k, i < j) update their upper-triangle registers
         // too: nothing reads those (the L store, the solves and the broadcasts take the
@@ -668,7 +690,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
             if (!l_nz<D, CH>(j, k)) continue;  // L_jk == 0: no update (compile-time after unrolling)
-            const float ljk = rl(m[k], j);
+            const float ljk = bc<EPW>(m[k], j);
             m[j] = fmaf(-m[k], ljk, m[j]);  // fused, as the oracle's cholesky()
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -687,7 +709,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         int ln = lane;
         asm volatile("" : "+v"(ln));
         x = ln == i ? x * idg : x;
-        const float xi = rl(x, i);
+        const float xi = bc<EPW>(x, i);
         x = ln > i ? fmaf(-m[i], xi, x) : x;
     }
     __syncthreads();
@@ -700,7 +722,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             int ln = lane;
             asm volatile("" : "+v"(ln));
             x = ln == i ? x * idg : x;
-            const float xi = rl(x, i);
+            const float xi = bc<EPW>(x, i);
             x = ln < i ? fmaf(-lc[i], xi, x) : x;
         }
     }
@@ -733,7 +755,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
         int nsc = 0;
         if (sp.n_selfp > 0) {
             const int maxs = sp.max_self < maxc_all ? sp.max_self : maxc_all;
-            for (int base = 0; base < sp.n_selfp && nsc < maxs; base += WAVE) {
+            for (int base = 0; base < sp.n_selfp && nsc < maxs; base += WAVE / EPW) {
                 const int q = base + lane;
                 bool act = false;
                 float pc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 1.f}, sep = 0.f;
@@ -769,7 +791,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
                     for (int k = 0; k < 3; ++k) pc[k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
                 }
-                const uint64_t mask = __ballot(act);
+                const uint64_t mask = hballot<EPW>(act);
                 const int slot = nsc + __popcll(mask & ((1ull << lane) - 1ull));
                 if (act && slot < maxs) {
                     s.sc_ab[slot][0] = ba; s.sc_ab[slot][1] = bb;
@@ -782,7 +804,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             }
         }
         const int maxc = maxc_all - nsc;
-        for (int base = 0; base < md.P && nc < maxc; base += WAVE) {
+        for (int base = 0; base < md.P && nc < maxc; base += WAVE / EPW) {
             const int k = base + lane;
             bool act = false;
             float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f, nrm[3] = {0.f, 0.f, 1.f};
@@ -801,7 +823,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
                 sep = (c[2] - h) * nrm[2] - rad - sp.rest_offset;
                 act = sep < sp.contact_offset;
             }
-            const uint64_t mask = __ballot(act);
+            const uint64_t mask = hballot<EPW>(act);
             const int slot = nc + __popcll(mask & ((1ull << lane) - 1ull));
             if (act && slot < maxc) {
                 s.c_body[slot] = b;
@@ -851,7 +873,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             else if (qn > hi) { hi_act = true; gap = hi - qj; }
         }
         const bool act = lo_act || hi_act;
-        const uint64_t mask = __ballot(act);
+        const uint64_t mask = hballot<EPW>(act);
         const int slot = __popcll(mask & ((1ull << lane) - 1ull));
         int max_limit = sp.max_rows - 3 * sp.max_contacts;
         if (max_limit > LM) max_limit = LM;
@@ -954,9 +976,36 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     // ---- 11. projected Gauss-Seidel.  Lane s holds column s of A (registers) and
     // v_s; per-row lambda are wave-uniform (SGPRs).  One contact = normal row,
     // then its friction pair against the post-normal velocities.
-    const int li = lane & 31, lk = lane >> 5;
+    static_assert(EPW == 1 || ROWS <= 32, "two envs per wave need one A tile per env");
+    const int li = threadIdx.x & 31, lk = threadIdx.x >> 5;  // the tiles take the whole wave
     float acol[ROWS];
-    if constexpr (ROWS <= 32) {
+    if constexpr (ROWS <= 32 && EPW == 2) {
+        // one tile per env, both fed by all 64 lanes; lane l of env h owns column l&31 of
+        // that env's A: for env 0 its own accumulators hold rows (t&3)+8(t>>2) and lane
+        // l+32's rows +4; for env 1 the other way round.  Each lane sends the other half the
+        // accumulator it needs (one shuffle per element, as for one env).
+        floatx16 acc0, acc1;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) { acc0[t] = 0.f; acc1[t] = 0.f; }
+#pragma unroll
+        for (int st = 0; st < (n + 1) / 2; ++st) {
+            const int kk = 2 * st + lk;
+            const float a0 = (li < ROWS && kk < n) ? sm[0].u.con.Y[li][kk] : 0.f;
+            const float a1 = (li < ROWS && kk < n) ? sm[1].u.con.Y[li][kk] : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, a1, acc1, 0, 0, 0);
+        }
+        const bool up = threadIdx.x >= 32;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int r0 = (t & 3) + 8 * (t >> 2);
+            const float own = up ? acc1[t] : acc0[t];
+            const float other = __shfl_xor(up ? acc0[t] : acc1[t], 32);
+            if (r0 < ROWS) acol[r0] = up ? other : own;
+            if (r0 + 4 < ROWS) acol[r0 + 4] = up ? own : other;
+        }
+        STAMP(11);
+    } else if constexpr (ROWS <= 32) {
         // one tile; lane l < 32 owns column l: rows (t&3)+8(t>>2) from its own
         // accumulators, rows +4 from lane l+32's.
         floatx16 acc;
@@ -1031,16 +1080,16 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             for (int c = 0; c < CM; ++c) {
                 if (c < nc) {
                     const int r = 3 * c;
-                    const float lno = rl(lam, r), l1o = rl(lam, r + 1), l2o = rl(lam, r + 2);
-                    const float vn = rl(v, r), v1 = rl(v, r + 1), v2 = rl(v, r + 2);
-                    const float ln = fmaxf(0.f, lno + (rl(tg, r) - vn) * rl(inv, r));
+                    const float lno = bc<EPW>(lam, r), l1o = bc<EPW>(lam, r + 1), l2o = bc<EPW>(lam, r + 2);
+                    const float vn = bc<EPW>(v, r), v1 = bc<EPW>(v, r + 1), v2 = bc<EPW>(v, r + 2);
+                    const float ln = fmaxf(0.f, lno + (bc<EPW>(tg, r) - vn) * bc<EPW>(inv, r));
                     const float dn = ln - lno;
                     v = fmaf(acol[r], dn, v);
-                    const float v1n = fmaf(rl(acol[r], r + 1), dn, v1);
-                    const float v2n = fmaf(rl(acol[r], r + 2), dn, v2);
+                    const float v1n = fmaf(bc<EPW>(acol[r], r + 1), dn, v1);
+                    const float v2n = fmaf(bc<EPW>(acol[r], r + 2), dn, v2);
                     const float lim = (c < ncg ? mu : mus) * ln;
-                    float l1 = l1o - v1n * rl(inv, r + 1);
-                    float l2 = l2o - v2n * rl(inv, r + 2);
+                    float l1 = l1o - v1n * bc<EPW>(inv, r + 1);
+                    float l2 = l2o - v2n * bc<EPW>(inv, r + 2);
                     const float nrm = sqrtf(l1 * l1 + l2 * l2);
                     if (nrm > lim) {
                         const float sc = nrm > 0.f ? lim / nrm : 0.f;
@@ -1055,8 +1104,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             for (int l = 0; l < LM; ++l) {
                 if (l < nlimit) {
                     const int r = 3 * CM + l;
-                    const float lo = rl(lam, r);
-                    const float ln = fmaxf(0.f, lo + (rl(tg, r) - rl(v, r)) * rl(inv, r));
+                    const float lo = bc<EPW>(lam, r);
+                    const float ln = fmaxf(0.f, lo + (bc<EPW>(tg, r) - bc<EPW>(v, r)) * bc<EPW>(inv, r));
                     v = fmaf(acol[r], ln - lo, v);
                     lam = lid == r ? ln : lam;
                 }
@@ -1065,19 +1114,25 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     STAMP(12);
     // ---- 12. z = Y^T lambda ; dq = L^-T z (register columns) ; qd' = qf + dq
+    // (the broadcasts stay outside the lane < n test: ds_bpermute reads nothing from a lane
+    // that is switched off)
     float z = 0.f;
-    if (lane < n) {
 #pragma unroll
-        for (int c = 0; c < CM; ++c)
-            if (c < nc) {
-                z = fmaf(s.u.con.Y[3 * c][lane], rl(lam, 3 * c), z);
-                z = fmaf(s.u.con.Y[3 * c + 1][lane], rl(lam, 3 * c + 1), z);
-                z = fmaf(s.u.con.Y[3 * c + 2][lane], rl(lam, 3 * c + 2), z);
+    for (int c = 0; c < CM; ++c)
+        if (c < nc) {
+            const float l0 = bc<EPW>(lam, 3 * c), l1 = bc<EPW>(lam, 3 * c + 1), l2 = bc<EPW>(lam, 3 * c + 2);
+            if (lane < n) {
+                z = fmaf(s.u.con.Y[3 * c][lane], l0, z);
+                z = fmaf(s.u.con.Y[3 * c + 1][lane], l1, z);
+                z = fmaf(s.u.con.Y[3 * c + 2][lane], l2, z);
             }
+        }
 #pragma unroll
-        for (int l = 0; l < LM; ++l)
-            if (l < nlimit) z = fmaf(s.u.con.Y[3 * CM + l][lane], rl(lam, 3 * CM + l), z);
-    }
+    for (int l = 0; l < LM; ++l)
+        if (l < nlimit) {
+            const float ll = bc<EPW>(lam, 3 * CM + l);
+            if (lane < n) z = fmaf(s.u.con.Y[3 * CM + l][lane], ll, z);
+        }
     {
         float lc[n];
 #pragma unroll
@@ -1087,7 +1142,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
             int ln = lane;
             asm volatile("" : "+v"(ln));
             z = ln == i ? z * idg : z;
-            const float zi = rl(z, i);
+            const float zi = bc<EPW>(z, i);
             z = ln < i ? fmaf(-lc[i], zi, z) : z;
         }
     }
@@ -1103,7 +1158,7 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
-                const float ln = rl(lam, 3 * c), l1 = rl(lam, 3 * c + 1), l2 = rl(lam, 3 * c + 2);
+                const float ln = bc<EPW>(lam, 3 * c), l1 = bc<EPW>(lam, 3 * c + 1), l2 = bc<EPW>(lam, 3 * c + 2);
                 if (c >= ncg && s.c_body2[c] == lane) {  // self contact: the reaction on the second body
                     const float* fr = s.c_fr[c];
 #pragma unroll
@@ -1123,8 +1178,8 @@ __device__ void substep(Smem<D, B, ROWS>& s, const DevModel& md, const DevSim& s
     }
     STAMP(13);
     // ---- 13. integrate
-    const float qw0 = rl(qn, n - 1), qw1 = rl(qn, n - 2), qw2 = rl(qn, n - 3);
-    const float qv0 = rl(qn, n - 4), qv1 = rl(qn, n - 5), qv2 = rl(qn, n - 6);
+    const float qw0 = bc<EPW>(qn, n - 1), qw1 = bc<EPW>(qn, n - 2), qw2 = bc<EPW>(qn, n - 3);
+    const float qv0 = bc<EPW>(qn, n - 4), qv1 = bc<EPW>(qn, n - 5), qv2 = bc<EPW>(qn, n - 6);
     __syncthreads();
     if (lane < D) {
         const int j = D - 1 - lane;
@@ -1167,10 +1222,9 @@ __device__ __forceinline__ int xcd_env(int b, int nwg) {
 }
 
 // rigid body states [B][13] of the block's env into global memory
-template <int D, int B, int ROWS>
-__device__ void body_states(Smem<D, B, ROWS>& s, float* rbs_out) {
-    const ModelCache<D, B>& mc = s.mc;
-    const int lane = threadIdx.x;
+template <int D, int B, int ROWS, int EPW>
+__device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, float* rbs_out) {
+    const int lane = hl<EPW>();
     if (lane < B) {
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
         quat_to_mat(s.root + 3, R);
@@ -1221,48 +1275,50 @@ __device__ void body_states(Smem<D, B, ROWS>& s, float* rbs_out) {
     }
 }
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int EPW>
 __device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
-    const int lane = threadIdx.x;
+    const int lane = hl<EPW>();
     if (lane < 13) s.root[lane] = st.root[13 * e + lane];
     if (lane < 2 * D) {
         const float v = st.dofs[(size_t)2 * D * e + lane];
         if (lane & 1) s.qd[lane >> 1] = v; else s.q[lane >> 1] = v;
     }
 }
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int EPW>
 __device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
-    int lane = threadIdx.x;
+    int lane = hl<EPW>();
     asm volatile("" : "+v"(lane));  // recompute the lane indices here (no value kept live from load_state)
     if (lane < 13) st.root[13 * e + lane] = s.root[lane];
     if (lane < 2 * D) st.dofs[(size_t)2 * D * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
-    for (int i = lane; i < 3 * B; i += WAVE) st.cforce[(size_t)3 * B * e + i] = (&s.cf[0][0])[i];
+    for (int i = lane; i < 3 * B; i += WAVE / EPW) st.cforce[(size_t)3 * B * e + i] = (&s.cf[0][0])[i];
 }
 
 // ---------------------------------------------------------- kernels --------
 template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
+    __shared__ ModelCache<D, B> mc;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
-    load_model(s, md);
-    load_state(s, st, e);
+    load_model(mc, md);
+    load_state<D, B, ROWS, 1>(s, st, e);
     if (threadIdx.x < D) s.tau[threadIdx.x] = st.torques_in[(size_t)D * e + threadIdx.x];
     __syncthreads();
-    substep<D, B, ROWS, CH>(s, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
-    store_state(s, st, e);
-    if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
+    substep<D, B, ROWS, CH, 1>(&s, mc, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
+    store_state<D, B, ROWS, 1>(s, st, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
 }
 
 template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
+    __shared__ ModelCache<D, B> mc;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
-    load_model(s, md);
-    load_state(s, st, e);
+    load_model(mc, md);
+    load_state<D, B, ROWS, 1>(s, st, e);
     __syncthreads();
-    body_states(s, st.rbs + (size_t)13 * B * e);
+    body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
 }
 
 struct DevEnv {
@@ -1429,10 +1485,10 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
     return r;
 }
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int EPW>
 __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                                     const float* rbs, int N, int e, uint32_t step) {
-    const int lane = threadIdx.x;
+    const int lane = hl<EPW>();
     if (lane == 0) {
         float* root = s.root;
         float* cmd = E.commands + 4 * e;
@@ -1541,17 +1597,17 @@ enum { RESET_STEP = 0, RESET_ALL = 1, RESET_IDS = 2 };
 // the rest from the state the first part left in the env buffers (lgs_post_physics_finish)
 enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
 
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, int EPW>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                              const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL) {
-    const int lane = threadIdx.x;
+    const int lane = hl<EPW>();
     const int A = T.num_actions;
     const uint64_t seed = T.seed;
     const bool force_reset = reset_mode != RESET_STEP;
     if (force_reset) {
         if (lane == 0) s.flags[0] = 1;
     } else if (part != PART_FINISH) {
-        post_physics_scalar(s, T, E, rbs, N, e, step);
+        post_physics_scalar<D, B, ROWS, EPW>(s, T, E, rbs, N, e, step);
         if (part == PART_REWARDS) return;
     } else if (lane == 0) {  // the first part's results: reset decision, base-frame state, commands
         s.flags[0] = E.reset[e];
@@ -1640,13 +1696,13 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     __syncthreads();
     const int O = T.num_obs, P = T.num_privileged_obs;
     const int off = (T.obs_layout == LGS_OBS_HUMANOID) ? 3 : 0;
-    for (int i = lane; i < O; i += WAVE) {
+    for (int i = lane; i < O; i += WAVE / EPW) {
         float x = s.u.post.obs_tmp[off + i];
         if (T.add_noise) x += (2.f * philox_uniform(seed, e, step, LGS_STREAM_NOISE, i) - 1.f) * T.noise_vec[i];
         E.obs[(size_t)O * e + i] = clipf(x, -T.clip_observations, T.clip_observations);
     }
     if (P > 0 && E.priv_obs && T.obs_layout == LGS_OBS_HUMANOID)
-        for (int i = lane; i < P; i += WAVE)
+        for (int i = lane; i < P; i += WAVE / EPW)
             E.priv_obs[(size_t)P * e + i] = clipf(s.u.post.obs_tmp[i], -T.clip_observations, T.clip_observations);
     // bookkeeping (:707-709)
     if (lane < A) E.last_actions[A * e + lane] = act[lane];
@@ -1660,17 +1716,21 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
 // bit for bit: the post half reads back exactly what the physics half stored.
 enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MODE_POST_FINISH = 4 };
 
-template <int D, int B, int ROWS, int CH>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32 ? LGS_WAVES_PER_EU : 2))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
+// EPW envs per workgroup (one wave): env EPW * xcd_env(block) + hh; with EPW = 2 the grid
+// has N / 2 workgroups (N even) and every wave carries two envs.
+template <int D, int B, int ROWS, int CH, int EPW>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(EPW == 2 ? 2 : (ROWS <= 32 ? LGS_WAVES_PER_EU : 2)))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step, int mode) {
-    __shared__ Smem<D, B, ROWS> s;
-    const int e = xcd_env(blockIdx.x, gridDim.x);
-    if (e >= N) return;
+    __shared__ Smem<D, B, ROWS> sm[EPW];
+    __shared__ ModelCache<D, B> mc;
+    const int e = EPW * xcd_env(blockIdx.x, gridDim.x) + hh<EPW>();
+    if (EPW * xcd_env(blockIdx.x, gridDim.x) >= N) return;  // (EPW = 2: N is even, both envs exist)
+    Smem<D, B, ROWS>& s = sm[hh<EPW>()];
     if (E.step_counter) step = (uint32_t)*E.step_counter;
     const lgs_task_params& T = *Tp;
-    const int lane = threadIdx.x;
-    load_model(s, md);
-    load_state(s, st, e);
+    const int lane = hl<EPW>();
+    load_model(mc, md);
+    load_state<D, B, ROWS, EPW>(s, st, e);
     const int A = T.num_actions;
     float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * B * e : nullptr;
     STAMP_INIT();
@@ -1697,24 +1757,24 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(ROWS <= 32
                 s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
             }
             __syncthreads();
-            substep<D, B, ROWS, CH>(s, md, sp, am, mu);
+            substep<D, B, ROWS, CH, EPW>(sm, mc, md, sp, am, mu);
         }
         STAMP(0);
         if (lane < D) E.torques[D * e + lane] = s.tau[lane];
-        if (rbs) body_states(s, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
+        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
     } else {  // the physics half's outputs, as it stored them
         if (lane < A) s.act[lane] = E.actions[A * e + lane];
         if (lane < D) s.tau[lane] = E.torques[D * e + lane];
-        for (int i = lane; i < 3 * B; i += WAVE) (&s.cf[0][0])[i] = st.cforce[(size_t)3 * B * e + i];
+        for (int i = lane; i < 3 * B; i += WAVE / EPW) (&s.cf[0][0])[i] = st.cforce[(size_t)3 * B * e + i];
     }
     __syncthreads();
     STAMP(15);
     if (mode != MODE_PHYSICS)
-        post_physics(s, T, E, rbs, N, e, step, RESET_STEP,
-                     mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL));
+        post_physics<D, B, ROWS, EPW>(s, T, E, rbs, N, e, step, RESET_STEP,
+                                      mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL));
     __syncthreads();
     STAMP(16);
-    store_state(s, st, e);
+    store_state<D, B, ROWS, EPW>(s, st, e);
     STAMP(17);
     STAMP_FLUSH(e);
 }
@@ -1724,18 +1784,19 @@ template <int D, int B, int ROWS, int CH>
 __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
                                                     lgs_env_buffers E, int N, uint32_t step, const uint8_t* mask) {
     __shared__ Smem<D, B, ROWS> s;
+    __shared__ ModelCache<D, B> mc;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     if (mask && !mask[e]) return;
     if (E.step_counter) step = (uint32_t)*E.step_counter;
-    load_model(s, md);
-    load_state(s, st, e);
+    load_model(mc, md);
+    load_state<D, B, ROWS, 1>(s, st, e);
     if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
     __syncthreads();
-    post_physics(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
+    post_physics<D, B, ROWS, 1>(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
     __syncthreads();
-    store_state(s, st, e);
-    if (st.rbs) body_states(s, st.rbs + (size_t)13 * B * e);
+    store_state<D, B, ROWS, 1>(s, st, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
 }
 
 // After k_step (one block): the extras of reset_idx (legged_robot.py:742-768) —
@@ -1791,6 +1852,7 @@ struct lgs_sim {
     int has_task = 0;
     int rows = 32;
     int chain = 0;  // dof_chain_length of the model
+    int epw = 1;    // envs per wave of k_step (2 for the 32-row variant at even N)
 };
 
 // Compiled (dofs, max bodies, constraint-row capacity, chain length) variants.  The
@@ -1818,6 +1880,27 @@ static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 
             hipLaunchKernelGGL((KERNEL<D_, B_, R_, 0>), dim3((sim)->N), dim3(WAVE), 0, (sim)->stream,    \
                                __VA_ARGS__);                                                             \
     } while (0)
+// k_step with EPW envs per wave (grid N / EPW)
+#define LGS_LAUNCH_EPW(sim, KERNEL, D_, B_, R_, EPW_, ...)                                                 \
+    do {                                                                                                  \
+        if ((sim)->chain == variant_chain(pick(sim)))                                                     \
+            hipLaunchKernelGGL((KERNEL<D_, B_, R_, (D_ == 10 ? 5 : (B_ == 13 ? 6 : 3)), EPW_>),            \
+                               dim3((sim)->N / EPW_), dim3(WAVE), 0, (sim)->stream, __VA_ARGS__);         \
+        else                                                                                              \
+            hipLaunchKernelGGL((KERNEL<D_, B_, R_, 0, EPW_>), dim3((sim)->N / EPW_), dim3(WAVE), 0,        \
+                               (sim)->stream, __VA_ARGS__);                                               \
+    } while (0)
+#define LGS_DISPATCH_STEP(sim, KERNEL, ...)                                                               \
+    switch (pick(sim)) {                                                                                  \
+    case V_12_19:                                                                                         \
+        if ((sim)->epw == 2) LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 2, __VA_ARGS__);                     \
+        else LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 1, __VA_ARGS__);                                     \
+        break;                                                                                            \
+    case V_12_13: LGS_LAUNCH_EPW(sim, KERNEL, 12, 13, 48, 1, __VA_ARGS__); break;                         \
+    case V_10_11: LGS_LAUNCH_EPW(sim, KERNEL, 10, 11, 48, 1, __VA_ARGS__); break;                         \
+    case V_12_19_48: LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 48, 1, __VA_ARGS__); break;                      \
+    default: return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");                                 \
+    }
 #define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
     switch (pick(sim)) {                                                                                  \
     case V_12_19: LGS_LAUNCH(sim, KERNEL, 12, 19, 32, __VA_ARGS__); break;                                \
@@ -1878,6 +1961,12 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     s->N = num_envs; s->B = m->num_bodies; s->D = m->num_dofs; s->P = m->num_points; s->device = device_id;
     s->rows = p->max_rows;
     s->chain = dof_chain_length(m);
+    // two envs per wave for the 32-row variant at an even env count (LGS_ENVS_PER_WAVE=1: one)
+    {
+        const char* ev = getenv("LGS_ENVS_PER_WAVE");
+        const bool one = ev && atoi(ev) == 1;
+        s->epw = (!one && num_envs % 2 == 0 && s->D == 12 && s->B <= 19 && s->rows <= 32) ? 2 : 1;
+    }
     if (pick(s) == V_NONE) {
         delete s;
         return set_err(LGS_ERR_ARG, "lgs_create_sim: no kernel instantiation for this (dofs, bodies)");
@@ -2118,7 +2207,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     if (!s || !env) return set_err(LGS_ERR_ARG, std::string(what) + ": null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, std::string(what) + ": state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
+    LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     HIP_TRY(hipGetLastError());
     if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1);
