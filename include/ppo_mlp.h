@@ -81,6 +81,18 @@ typedef struct {
     pmlp_bf16* ct;
     int32_t lda, ldb, ldyp, ldcf, ldcb, ldct;
     int32_t M, N, K;
+    /* Optional operand forms (NULL / 0: the defaults above; every job of a call alike):
+     *  af (FWD_HIDDEN, FWD_OUT): A is fp32 af[rows[m]][k] (ld ldaf, a multiple of 4; rows
+     *      NULL = row m; columns >= kaf read as 0) converted to bf16 on load -- the mini-batch
+     *      gather and conversion of the observations inside the first layer's GEMM; A is
+     *      unused.  xa (optional): the converted bf16 rows are also stored to xa[M, ldxa]
+     *      (the weight gradient's operand).
+     *  b_kn (BWD_DX): B is given as [K,N] (ldb >= N, n contiguous): the layer's weight
+     *      W[out,in] itself, read through transposed LDS reads (no W^T copy).          */
+    const float* af;
+    const int64_t* rows;
+    pmlp_bf16* xa;
+    int32_t ldaf, kaf, ldxa, b_kn;
 } pmlp_gemm_job;
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
 
@@ -145,6 +157,19 @@ PMLP_API int pmlp_opt_prepare(const float* grad, int64_t n, float grad_scale, fl
 PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float grad_scale, const float* partial, const float* step, const float* lr, float max_norm,
                        float beta1, float beta2, float eps, void* stream);
+/* pmlp_adam that also refreshes bf16 copies of the updated weights (the GEMM operands):
+ * param[offset + r*cols + c] -> dst[r*ld + c] for every mirror job, so no conversion launch
+ * precedes the next forward.  At most PMLP_MAX_MIRROR jobs, disjoint parameter ranges.   */
+#define PMLP_MAX_MIRROR 8
+typedef struct {
+    int64_t offset;
+    int32_t rows, cols, ld;
+    pmlp_bf16* dst;
+} pmlp_mirror_job;
+PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                              float grad_scale, const float* partial, const float* step, const float* lr,
+                              float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
+                              const pmlp_mirror_job* mirror, void* stream);
 
 /* RolloutStorage.compute_returns (rsl_rl v1.0.2): GAE(gamma, lam) over [T,N]
  * rewards/dones(bool bytes)/values with last_values[N], writing returns and

@@ -61,6 +61,12 @@ struct GemmArgs {
     bf16* ct;
     int lda, ldb, ldyp, ldcf, ldcb, ldct;
     int M, N, K, ksplit;
+    // MODE & 1: A = fp32 af[rows[m]][k] (k < kaf, else 0) converted on load; the blocks of
+    // the first column tile also store the bf16 rows to xa (ld ldxa)
+    const float* af;
+    const int64_t* rows;
+    bf16* xa;
+    int ldaf, kaf, ldxa;
 };
 
 #ifdef PMLP_EXACT_ELU
@@ -82,7 +88,11 @@ __device__ __forceinline__ shortx4 lds_read_tr(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)p);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4>
+// MODE bit 0: A is fp32 rows gathered and converted on load (the first forward GEMM reads
+// the observations itself: no conversion launch); bit 1: B is given [K][N] (n contiguous)
+// and staged k-major like PARTIAL_TN's operands (the input gradient reads W[out][in]
+// itself: no transposed weight copy).
+template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0>
 __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     const int job = blockIdx.z / gb.slabs, slice = blockIdx.z % gb.slabs;
     const GemmArgs& g = gb.j[job];
@@ -91,13 +101,15 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     // gradients), staged k-major in LDS and fed to the MFMAs by transposed reads
     constexpr bool TNL = EPI == PMLP_EPI_PARTIAL_TN;
     constexpr bool PART = EPI == PMLP_EPI_PARTIAL || TNL;
-    static_assert(!TNL || PMLP_NBUF == 1, "PARTIAL_TN stages one k-tile");
+    constexpr bool AF32 = (MODE & 1) != 0;
+    constexpr bool BKN = TNL || (MODE & 2) != 0;  // B staged from [K][N]
+    static_assert(!BKN || PMLP_NBUF == 1, "k-major B stages one k-tile");
     constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
     constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
     // TN images [BK][BM + 32]: a row stride of 16 (mod 64) dwords puts the four rows of
     // one transposed read on disjoint banks (conflict-free for BM, BN multiples of 64)
-    constexpr int SA = TNL ? BM + 32 : LS, SB = TNL ? BN + 32 : LS;
-    constexpr int ATILE = TNL ? BK * SA : BM * LS, BTILE = TNL ? BK * SB : BN * LS;
+    constexpr int SA = TNL ? BM + 32 : LS, SB = BKN ? BN + 32 : LS;
+    constexpr int ATILE = TNL ? BK * SA : BM * LS, BTILE = BKN ? BK * SB : BN * LS;
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 32, FN = TN / 32;
@@ -141,6 +153,41 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 if (c < ACH && gk < ke && gm < g.M) v = *(const uint4*)(g.A + (size_t)gk * g.lda + gm);
                 ra[i] = v;
             }
+        } else if constexpr (AF32) {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int c = tid + i * NT;
+                const int r = c / CPR, kc = (c % CPR) * 8;
+                const int gr = m0 + r, gk = k0 + kc;
+                bf16x8 t;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] = (bf16)0.f;
+                if (c < ACH && gr < g.M && gk < ke) {
+                    const float* src = g.af + (size_t)(g.rows ? g.rows[gr] : (int64_t)gr) * g.ldaf + gk;
+                    if (gk + 8 <= g.kaf) {
+                        const float4 x0 = *(const float4*)src, x1 = *(const float4*)(src + 4);
+                        t[0] = (bf16)x0.x; t[1] = (bf16)x0.y; t[2] = (bf16)x0.z; t[3] = (bf16)x0.w;
+                        t[4] = (bf16)x1.x; t[5] = (bf16)x1.y; t[6] = (bf16)x1.z; t[7] = (bf16)x1.w;
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) t[u] = gk + u < g.kaf ? (bf16)src[u] : (bf16)0.f;
+                    }
+                    if (g.xa && blockIdx.y == 0) *(bf16x8*)(g.xa + (size_t)gr * g.ldxa + gk) = t;
+                }
+                ra[i] = *(const uint4*)&t;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int c = tid + i * NT;
+                const int r = c / CPR, kc = (c % CPR) * 8;
+                const int gr = m0 + r, gk = k0 + kc;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (c < ACH && gr < g.M && gk < ke) v = *(const uint4*)(g.A + (size_t)gr * g.lda + gk);
+                ra[i] = v;
+            }
+        }
+        if constexpr (BKN) {
 #pragma unroll
             for (int i = 0; i < BL; ++i) {
                 const int c = tid + i * NT;
@@ -150,25 +197,16 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 if (c < BCH && gk < ke && gn < g.N) v = *(const uint4*)(g.B + (size_t)gk * g.ldb + gn);
                 rb[i] = v;
             }
-            return;
-        }
+        } else {
 #pragma unroll
-        for (int i = 0; i < AL; ++i) {
-            const int c = tid + i * NT;
-            const int r = c / CPR, kc = (c % CPR) * 8;
-            const int gr = m0 + r, gk = k0 + kc;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (c < ACH && gr < g.M && gk < ke) v = *(const uint4*)(g.A + (size_t)gr * g.lda + gk);
-            ra[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < BL; ++i) {
-            const int c = tid + i * NT;
-            const int r = c / CPR, kc = (c % CPR) * 8;
-            const int gr = n0 + r, gk = k0 + kc;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (c < BCH && gr < g.N && gk < ke) v = *(const uint4*)(g.B + (size_t)gr * g.ldb + gk);
-            rb[i] = v;
+            for (int i = 0; i < BL; ++i) {
+                const int c = tid + i * NT;
+                const int r = c / CPR, kc = (c % CPR) * 8;
+                const int gr = n0 + r, gk = k0 + kc;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (c < BCH && gr < g.N && gk < ke) v = *(const uint4*)(g.B + (size_t)gr * g.ldb + gk);
+                rb[i] = v;
+            }
         }
     };
     auto lstore = [&]() {
@@ -178,22 +216,25 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const int c = tid + i * NT;
                 if (c < ACH) *(uint4*)(As + (c / (BM / 8)) * SA + (c % (BM / 8)) * 8) = ra[i];
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int c = tid + i * NT;
+                if (c < ACH) *(uint4*)(As + (c / CPR) * LS + (c % CPR) * 8) = ra[i];
+            }
+        }
+        if constexpr (BKN) {
 #pragma unroll
             for (int i = 0; i < BL; ++i) {
                 const int c = tid + i * NT;
                 if (c < BCH) *(uint4*)(Bs + (c / (BN / 8)) * SB + (c % (BN / 8)) * 8) = rb[i];
             }
-            return;
-        }
+        } else {
 #pragma unroll
-        for (int i = 0; i < AL; ++i) {
-            const int c = tid + i * NT;
-            if (c < ACH) *(uint4*)(As + (c / CPR) * LS + (c % CPR) * 8) = ra[i];
-        }
-#pragma unroll
-        for (int i = 0; i < BL; ++i) {
-            const int c = tid + i * NT;
-            if (c < BCH) *(uint4*)(Bs + (c / CPR) * LS + (c % CPR) * 8) = rb[i];
+            for (int i = 0; i < BL; ++i) {
+                const int c = tid + i * NT;
+                if (c < BCH) *(uint4*)(Bs + (c / CPR) * LS + (c % CPR) * 8) = rb[i];
+            }
         }
     };
 
@@ -203,6 +244,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
     auto kstep = [&](int s) {
         bf16x8 af[FM], bfr[FN];
+        const int ko = s * 16 + (lane >> 5) * 8;
         if constexpr (TNL) {
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
@@ -210,6 +252,11 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const shortx4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * SA);
                 af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(As + (wm * TM + i * 32 + (lane & 31)) * LS + ko);
+        }
+        if constexpr (BKN) {
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 const bf16* p = Bs + (s * 16 + tr_off) * SB + wn * TN + j * 32 + tr_col;
@@ -217,9 +264,6 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
         } else {
-            const int ko = s * 16 + (lane >> 5) * 8;
-#pragma unroll
-            for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(As + (wm * TM + i * 32 + (lane & 31)) * LS + ko);
 #pragma unroll
             for (int j = 0; j < FN; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn * TN + j * 32 + (lane & 31)) * LS + ko);
         }
@@ -948,11 +992,17 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_opt_prepare(const float* _
     }
 }
 
+struct MirrorJobs {
+    int64_t off[PMLP_MAX_MIRROR];
+    int rows[PMLP_MAX_MIRROR], cols[PMLP_MAX_MIRROR], ld[PMLP_MAX_MIRROR];
+    bf16* dst[PMLP_MAX_MIRROR];
+    int n;
+};
 __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p, const float* __restrict__ g,
                                                            float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                            float scale, const float* __restrict__ partial, int nparts,
                                                            const float* step, const float* lr, float max_norm,
-                                                           float b1, float b2, float eps) {
+                                                           float b1, float b2, float eps, MirrorJobs mj) {
     __shared__ float sh[4];
     float s = 0.f;
     for (int i = threadIdx.x; i < nparts; i += PMLP_OPT_THREADS) s += partial[i];
@@ -969,7 +1019,15 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
         const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
         m[i] = mi;
         v[i] = vi;
-        p[i] -= step_size * (mi / (sqrtf(vi) / bc2s + eps));
+        const float pi = p[i] - step_size * (mi / (sqrtf(vi) / bc2s + eps));
+        p[i] = pi;
+        for (int j = 0; j < mj.n; ++j) {  // the bf16 GEMM operand copy of a weight
+            const int64_t o = i - mj.off[j];
+            if (o >= 0 && o < (int64_t)mj.rows[j] * mj.cols[j]) {
+                const int r = (int)(o / mj.cols[j]), c = (int)(o % mj.cols[j]);
+                mj.dst[j][(size_t)r * mj.ld[j] + c] = (bf16)pi;
+            }
+        }
     }
 }
 
@@ -1358,21 +1416,33 @@ __global__ __launch_bounds__(64 * MLP4_WAVES) void k_mlp4_fwd(Mlp4Jobs jobs, int
 }
 
 template <int BM, int BN, int WM, int WN>
-static void launch(int epi, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk, hipStream_t st) {
+static void launch(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
+    const bool af = (mode & 1) != 0, bkn = (mode & 2) != 0;
     // one short k-tile: only the k-steps that carry data (K = 48 forward, K = 16 input gradient)
     if (epi == PMLP_EPI_FWD_HIDDEN && maxk <= 48 && maxk > 32) {
-        hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 3>), grid, block, 0, st, gb);
+        if (af) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 3, 1>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 3>), grid, block, 0, st, gb);
         return;
     }
     if (epi == PMLP_EPI_BWD_DX && maxk <= 16) {
-        hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1>), grid, block, 0, st, gb);
+        if (bkn) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1, 2>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1>), grid, block, 0, st, gb);
         return;
     }
     switch (epi) {
-    case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, gb); break;
-    case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, gb); break;
-    case PMLP_EPI_BWD_DX: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, gb); break;
+    case PMLP_EPI_FWD_HIDDEN:
+        if (af) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 1>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0>), grid, block, 0, st, gb);
+        break;
+    case PMLP_EPI_FWD_OUT:
+        if (af) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1, 4, 1>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1>), grid, block, 0, st, gb);
+        break;
+    case PMLP_EPI_BWD_DX:
+        if (bkn) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2>), grid, block, 0, st, gb);
+        break;
     case PMLP_EPI_PARTIAL: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 3>), grid, block, 0, st, gb); break;
     default: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4>), grid, block, 0, st, gb); break;
     }
@@ -1414,11 +1484,25 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
     GemmBatch gb{};
     gb.slabs = 1;
     int maxm = 0, maxn = 0, maxk = 0;
+    const int mode = (jobs[0].af ? 1 : 0) | (jobs[0].b_kn ? 2 : 0);
     for (int i = 0; i < njobs; ++i) {
         const pmlp_gemm_job& J = jobs[i];
         const std::string w = "pmlp_gemm job " + std::to_string(i) + ": ";
-        if (!J.A || !J.B || J.M <= 0 || J.N <= 0 || J.K <= 0) return fail(-1, w + "null operand or empty shape");
-        if (epi == PMLP_EPI_PARTIAL_TN) {
+        if (((J.af ? 1 : 0) | (J.b_kn ? 2 : 0)) != mode) return fail(-1, w + "every job must use the same operand forms");
+        if ((!J.A && !J.af) || !J.B || J.M <= 0 || J.N <= 0 || J.K <= 0) return fail(-1, w + "null operand or empty shape");
+        if (J.af) {
+            if ((epi != PMLP_EPI_FWD_HIDDEN && epi != PMLP_EPI_FWD_OUT) || J.kaf <= 0 || J.kaf > J.K ||
+                J.ldaf < J.kaf || J.ldaf % 4 || ((uintptr_t)J.af & 15) ||
+                (J.xa && (J.ldxa < J.K || J.ldxa % 8 || !al16(J.xa))))
+                return fail(-1, w + "fp32 A: forward epilogues, 0 < kaf <= K, ldaf >= kaf a multiple of 4, "
+                                    "16-byte aligned; xa: ldxa >= K, a multiple of 8");
+        }
+        if (J.b_kn && (epi != PMLP_EPI_BWD_DX || J.ldb < J.N || J.ldb % 8 || !al16(J.B) || J.K % 8 || J.lda % 8 ||
+                       J.lda < J.K || !al16(J.A)))
+            return fail(-1, w + "B given [K,N]: BWD_DX only, ldb >= N, K/lda/ldb multiples of 8, 16-byte aligned");
+        if (J.af || J.b_kn) {
+            // checked above
+        } else if (epi == PMLP_EPI_PARTIAL_TN) {
             // A[K,M], B[K,N]: whole 16-byte chunks along m and n are read
             if (J.lda % 8 || J.ldb % 8 || J.lda < (J.M + 7) / 8 * 8 || J.ldb < (J.N + 7) / 8 * 8 || !al16(J.A) ||
                 !al16(J.B))
@@ -1437,6 +1521,7 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         g.cf = J.cf; g.cb = (bf16*)J.cb; g.ct = (bf16*)J.ct;
         g.lda = J.lda; g.ldb = J.ldb; g.ldyp = J.ldyp; g.ldcf = J.ldcf; g.ldcb = J.ldcb; g.ldct = J.ldct;
         g.M = J.M; g.N = J.N; g.K = J.K; g.ksplit = ksplit;
+        g.af = J.af; g.rows = J.rows; g.xa = (bf16*)J.xa; g.ldaf = J.ldaf; g.kaf = J.kaf; g.ldxa = J.ldxa;
         maxm = std::max(maxm, J.M); maxn = std::max(maxn, J.N); maxk = std::max(maxk, J.K);
     }
     if (part) {
@@ -1447,11 +1532,11 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         gb.slabs = (maxk + ksplit - 1) / ksplit;
     }
     hipStream_t st = (hipStream_t)stream;
-    if (maxm <= 32) launch<32, 128, 1, 4>(epi, gb, njobs, maxm, maxn, maxk, st);
-    else if (maxn <= 32) launch<128, 32, 4, 1>(epi, gb, njobs, maxm, maxn, maxk, st);
-    else if (maxn <= 64) launch<128, 64, 4, 1>(epi, gb, njobs, maxm, maxn, maxk, st);
+    if (maxm <= 32) launch<32, 128, 1, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+    else if (maxn <= 32) launch<128, 32, 4, 1>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+    else if (maxn <= 64) launch<128, 64, 4, 1>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
     else if (!part && (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512)
-        launch<64, 64, 2, 2>(epi, gb, njobs, maxm, maxn, maxk, st);  // small grids: 4x the blocks hide the k-loop latency
+        launch<64, 64, 2, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);  // small grids: 4x the blocks hide the k-loop latency
     else {
         // 128x128 output tiles: 8 waves of 64x32 (accumulators in 32 VGPRs, no AGPRs:
         // 4 waves/SIMD resident instead of 3) for the epilogue-heavy short-K GEMMs; 4 waves
@@ -1462,10 +1547,23 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
             const char* v = getenv("PMLP_BIG_TILE");
             return v ? atoi(v) : -1;
         }();
+        // 128 x 256 tiles (8 waves of 64x64) for the widest GEMMs (PMLP_WIDE_TILE=1): the A
+        // operand is re-read by half as many column tiles -- measured SLOWER (forward N = 256
+        // 30 -> 39 us, input gradient N = 512 39 -> 47 us: the re-reads hit L2, and 67 KB of
+        // LDS per block halves the resident blocks), so off by default
+        static const int wide_env = [] {
+            const char* v = getenv("PMLP_WIDE_TILE");
+            return v ? atoi(v) : 0;
+        }();
+        const bool wide = wide_env > 0 && big < 0 &&
+                          ((epi == PMLP_EPI_FWD_HIDDEN && maxn >= 256 && maxk >= 256) ||
+                           (epi == PMLP_EPI_BWD_DX && maxn >= 512) ||
+                           (epi == PMLP_EPI_PARTIAL_TN && maxn >= 256 && maxm >= 128));
         const int pick = big >= 0 ? big : ((epi == PMLP_EPI_FWD_HIDDEN && maxk >= 256) ? 0 : 1);
-        if (pick == 1) launch<128, 128, 2, 4>(epi, gb, njobs, maxm, maxn, maxk, st);
-        else if (pick == 2) launch<128, 128, 4, 2>(epi, gb, njobs, maxm, maxn, maxk, st);
-        else launch<128, 128, 2, 2>(epi, gb, njobs, maxm, maxn, maxk, st);
+        if (wide) launch<128, 256, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+        else if (pick == 1) launch<128, 128, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+        else if (pick == 2) launch<128, 128, 4, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+        else launch<128, 128, 2, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
     }
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
@@ -1578,9 +1676,34 @@ PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* e
     if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !partial || !step || !lr)
         return fail(-1, "pmlp_adam: null buffer or empty parameter set");
     const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    MirrorJobs mj{};
     hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
-                       exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps);
+                       exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps, mj);
     PMLP_CHECK_LAUNCH("pmlp_adam");
+    return 0;
+}
+
+PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                              float grad_scale, const float* partial, const float* step, const float* lr,
+                              float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
+                              const pmlp_mirror_job* mirror, void* stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !partial || !step || !lr)
+        return fail(-1, "pmlp_adam_mirror: null buffer or empty parameter set");
+    if (nmirror < 0 || nmirror > PMLP_MAX_MIRROR || (nmirror && !mirror))
+        return fail(-1, "pmlp_adam_mirror: 0..PMLP_MAX_MIRROR mirror jobs");
+    MirrorJobs mj{};
+    mj.n = nmirror;
+    for (int j = 0; j < nmirror; ++j) {
+        const pmlp_mirror_job& J = mirror[j];
+        if (!J.dst || J.offset < 0 || J.rows <= 0 || J.cols <= 0 || J.ld < J.cols ||
+            J.offset + (int64_t)J.rows * J.cols > n)
+            return fail(-1, "pmlp_adam_mirror: bad mirror job " + std::to_string(j));
+        mj.off[j] = J.offset; mj.rows[j] = J.rows; mj.cols[j] = J.cols; mj.ld[j] = J.ld; mj.dst[j] = (bf16*)J.dst;
+    }
+    const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
+                       exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps, mj);
+    PMLP_CHECK_LAUNCH("pmlp_adam_mirror");
     return 0;
 }
 

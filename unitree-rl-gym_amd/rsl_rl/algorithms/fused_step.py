@@ -76,11 +76,19 @@ class FusedPPOStep:
                 self._vview[id(p)] = self.exp_avg_sq[off:off + k].view_as(p)
                 off += k
         self.stats = self.grad[n:n + 4]
+        self._offset = {}  # flat offset of every parameter
+        off = 0
+        for p in params:
+            self._offset[id(p)] = off
+            off += p.numel()
         self._side = None  # side stream of the weight-gradient GEMMs (run())
         # dW_l beside dX_l on a second stream: measured SLOWER (one update 6.44 -> 6.77 ms,
         # tools/probes/update_env_ab.py), the two latency-bound GEMMs contend; off by default
         self.dw_side_stream = os.environ.get("PMLP_DW_SIDE_STREAM", "0") == "1"
-        # the bf16 weight copies (wb) lag the fp32 weights after an optimizer step
+        # the bf16 weight copies (wb) are the GEMM operands of the rollout and the update;
+        # every fused Adam step rewrites them (pmlp_adam_mirror).  weights_changed: they lag
+        # the fp32 weights (construction, a checkpoint load, any update outside this path)
+        # and are reconverted before their next use (ensure_weights)
         self.weights_changed = True
         # weight gradients read the row-major activations through LDS-transposed MFMA
         # operands (PARTIAL_TN), so no transposed copy is ever written; PMLP_TN=0 keeps
@@ -103,10 +111,16 @@ class FusedPPOStep:
                    torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
         self.xt = [None if tn else self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k)
                    for k in self.k0p]
-        self.wb = [[torch.empty(lin.out_features, self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
+        # W[out, in] in bf16: the forward's B[N, K] and, unchanged, the input gradient's B[K, N]
+        # (b_kn); the last layer's rows are padded to a multiple of 8 with zero rows (the input
+        # gradient's K) -- no transposed copy
+        self.wb = [[torch.zeros(_ceil8(lin.out_features) if l == len(ls) - 1 else lin.out_features,
+                                self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
                     for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
-        self.wt = [[torch.empty(lin.in_features, _ceil8(lin.out_features), dtype=bf, device=dev) if l > 0 else None
-                    for l, lin in enumerate(ls)] for ls in self.lins]
+        self.mirror = (mm.MirrorJob * (2 * len(self.lins[0])))(*[
+            mm.MirrorJob(self._offset[id(lin.weight)], lin.out_features, lin.in_features, self.wb[n][l].shape[1],
+                         self.wb[n][l].data_ptr())
+            for n, ls in enumerate(self.lins) for l, lin in enumerate(ls)])
         self.y = [[self._ones_col(torch.empty(M, lin.out_features + 8, dtype=bf, device=dev), lin.out_features) if tn
                    else torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
         self.yt = [[None if tn else
@@ -171,6 +185,18 @@ class FusedPPOStep:
                 if p.grad is None or p.grad.data_ptr() != self._gview[id(p)].data_ptr():
                     p.grad = self._gview[id(p)]
 
+    def ensure_weights(self):
+        """Refresh the bf16 weight copies when they lag the fp32 weights (outside any
+        captured graph: the captured steps keep them current through the Adam mirror)."""
+        if not self.weights_changed:
+            return
+        jobs = []
+        for n in range(2):
+            for l, lin in enumerate(self.lins[n]):
+                jobs.append((lin.weight.detach(), self.wb[n][l].shape[1], self.wb[n][l][:lin.out_features], None))
+        mm._convert(jobs)
+        self.weights_changed = False
+
     # -------------------------------------------------------------- step ----
     def run(self, rows, src, acc):
         """One optimizer step on mini-batch rows `rows` (int64 [M]) of the flat rollout
@@ -180,39 +206,37 @@ class FusedPPOStep:
         obs, cobs, actions, values, adv, ret, logp, mu_old, sigma_old = src
         shared = cobs is obs and self.k0p[0] == self.k0p[1]
         lib = mm.load()
-        # 1. gathered observations + weights -> bf16
+        self.ensure_weights()  # (a no-op once the Adam mirror keeps them current)
+        # 1. no conversion launch: the first forward GEMM gathers the mini-batch's fp32
+        #    observations through `rows` and converts them on load, storing the bf16 rows
+        #    (the first weight gradient's operand) on the way; the bf16 weights are current
+        #    (the previous Adam step wrote them)
         tn = self.tn
-        if tn:  # row-major [M, k0p + 8] with the ones column at k0p
-            jobs = [(obs, self.k0p[0] + 8, self.xb[0], None, rows, self.k0p[0])]
+        if not tn:
+            jobs = [(obs, self.k0p[0], None, self.xt[0], rows)]
             if not shared:
-                jobs.append((cobs, self.k0p[1] + 8, self.xb[1], None, rows, self.k0p[1]))
-        else:
-            jobs = [(obs, self.k0p[0], self.xb[0], self.xt[0], rows)]
-            if not shared:
-                jobs.append((cobs, self.k0p[1], self.xb[1], self.xt[1], rows))
-        for n in range(2):
-            for l, lin in enumerate(self.lins[n]):
-                W = lin.weight.detach()
-                jobs.append((W, self.wb[n][l].shape[1], self.wb[n][l], None))
-                if l > 0:
-                    jobs.append((W, W.shape[1], None, self.wt[n][l]))
-        mm._convert(jobs)
+                jobs.append((cobs, self.k0p[1], None, self.xt[1], rows))
+            mm._convert(jobs)
         xb = [self.xb[0], self.xb[0] if shared else self.xb[1]]
         xt = [self.xt[0], self.xt[0] if shared else self.xt[1]]
+        fobs = [obs, cobs]
         # 2. forward
         for l in range(L):
             last = l == L - 1
             gj = []
             for n in range(2):
                 lin = self.lins[n][l]
-                a_in = xb[n] if l == 0 else self.y[n][l - 1]
                 K = self.k0p[n] if l == 0 else lin.in_features
-                if last:
-                    gj.append(dict(A=a_in, B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
-                                   cf=self.out[n]))
+                if l == 0:
+                    a = dict(af=fobs[n], rows=rows, xa=self.xb[n] if (n == 0 or not shared) else None)
                 else:
-                    gj.append(dict(A=a_in, B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
-                                   cb=self.y[n][l], ct=self.yt[n][l]))
+                    a = dict(A=self.y[n][l - 1])
+                if last:
+                    gj.append(dict(B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cf=self.out[n], **a))
+                else:
+                    gj.append(dict(B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cb=self.y[n][l], ct=self.yt[n][l], **a))
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
         # 3. loss forward + backward in one pass (rollout inputs read through `rows`); the
         #    output gradients land directly in the backward's bf16 operands
@@ -262,7 +286,7 @@ class FusedPPOStep:
                 for n in range(2):
                     lin = self.lins[n][l]
                     # the input layer's gradient is only consumed transposed (its weight gradient)
-                    gj.append(dict(A=dz[n], B=self.wt[n][l], M=M, N=lin.in_features, K=dz[n].shape[1],
+                    gj.append(dict(A=dz[n], B=self.wb[n][l], b_kn=1, M=M, N=lin.in_features, K=dz[n].shape[1],
                                    yprev=self.y[n][l - 1], cb=self.dz[n][l], ct=self.dzt[n][l]))
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
@@ -286,10 +310,11 @@ class FusedPPOStep:
                                     float(alg.desired_kl if alg.desired_kl is not None else 0.0), adaptive, st),
                "pmlp_opt_prepare")
         max_norm = float(alg.max_grad_norm) if alg.max_grad_norm is not None else 0.0
-        mm._ok(lib.pmlp_adam(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg), mm._p(self.exp_avg_sq), self.n,
-                             scale, mm._p(self.opt_partial), mm._p(self.step_t), mm._p(alg._lr), max_norm, float(b1),
-                             float(b2), float(eps), st), "pmlp_adam")
-        self.weights_changed = True
+        # Adam, and the bf16 weight copies of the next forward written on the way
+        mm._ok(lib.pmlp_adam_mirror(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg), mm._p(self.exp_avg_sq),
+                                    self.n, scale, mm._p(self.opt_partial), mm._p(self.step_t), mm._p(alg._lr),
+                                    max_norm, float(b1), float(b2), float(eps), len(self.mirror), self.mirror, st),
+               "pmlp_adam_mirror")
 
 
 class FusedRollout:
@@ -305,7 +330,6 @@ class FusedRollout:
         N, dev, bf = int(num_envs), step.dev, torch.bfloat16
         self.N = N
         lins = step.lins
-        self.x = [torch.empty(N, k, dtype=bf, device=dev) for k in step.k0p]
         self.y = [[torch.empty(N, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in lins]
         self.out = [torch.empty(N, ls[-1].out_features, device=dev) for ls in lins]
         self.actions = torch.empty(N, lins[0][-1].out_features, device=dev)
@@ -327,36 +351,27 @@ class FusedRollout:
         return storage.num_envs == self.N
 
     def forward(self, obs, cobs, t=None):
-        """(mu, value) of the actor and critic on N rows into static buffers.  The bf16
-        weight copies are refreshed at the first step of a rollout (t == 0; the update
-        changes the weights only between rollouts) or on any call outside one."""
+        """(mu, value) of the actor and critic on N rows into static buffers: L GEMM launches,
+        the first reading the fp32 observations itself.  The bf16 weight copies are current
+        (the fused Adam step writes them); they are reconverted only when they lag."""
         f, N = self.f, self.N
         if self.regs:  # one launch, activations in registers
             return mm.mlp4_forward([self.f.ac.actor, self.f.ac.critic], [obs, cobs], self.out)
-        shared = cobs is obs and f.k0p[0] == f.k0p[1]
-        jobs = [(obs, f.k0p[0], self.x[0], None)]
-        if not shared:
-            jobs.append((cobs, f.k0p[1], self.x[1], None))
-        if t is None or t == 0 or f.weights_changed:
-            for n in range(2):
-                for l, lin in enumerate(f.lins[n]):
-                    jobs.append((lin.weight.detach(), f.wb[n][l].shape[1], f.wb[n][l], None))
-            f.weights_changed = False
-        mm._convert(jobs)
-        xs = [self.x[0], self.x[0] if shared else self.x[1]]
+        f.ensure_weights()
+        xs = [obs, cobs]
         for l in range(f.L):
             last = l == f.L - 1
             gj = []
             for n in range(2):
                 lin = f.lins[n][l]
-                a_in = xs[n] if l == 0 else self.y[n][l - 1]
+                a = dict(af=xs[n]) if l == 0 else dict(A=self.y[n][l - 1])
                 K = f.k0p[n] if l == 0 else lin.in_features
                 if last:
-                    gj.append(dict(A=a_in, B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
-                                   cf=self.out[n]))
+                    gj.append(dict(B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cf=self.out[n], **a))
                 else:
-                    gj.append(dict(A=a_in, B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
-                                   cb=self.y[n][l]))
+                    gj.append(dict(B=f.wb[n][l], M=N, N=lin.out_features, K=K, bias=lin.bias.detach(),
+                                   cb=self.y[n][l], **a))
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
         return self.out
 

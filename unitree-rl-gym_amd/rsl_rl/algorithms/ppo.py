@@ -335,6 +335,7 @@ class PPO:
         RolloutStorage.mini_batch_generator: one randperm per update, reused every epoch."""
         f, st = self._fused, self.storage
         f.sync_optimizer_state(self.optimizer)
+        f.ensure_weights()  # the captured steps read the bf16 weight copies from the first one
         mb = f.M
         if self._fgraph is None and not hasattr(self, "_fperm"):
             self._fperm = torch.empty(self.num_mini_batches * mb, dtype=torch.int64, device=self.device)

@@ -39,7 +39,14 @@ class GemmJob(C.Structure):
     _fields_ = [("A", C.c_void_p), ("B", C.c_void_p), ("bias", C.c_void_p), ("yprev", C.c_void_p),
                 ("cf", C.c_void_p), ("cb", C.c_void_p), ("ct", C.c_void_p), ("lda", C.c_int32), ("ldb", C.c_int32),
                 ("ldyp", C.c_int32), ("ldcf", C.c_int32), ("ldcb", C.c_int32), ("ldct", C.c_int32),
-                ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32)]
+                ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32),
+                ("af", C.c_void_p), ("rows", C.c_void_p), ("xa", C.c_void_p), ("ldaf", C.c_int32),
+                ("kaf", C.c_int32), ("ldxa", C.c_int32), ("b_kn", C.c_int32)]
+
+
+class MirrorJob(C.Structure):
+    _fields_ = [("offset", C.c_int64), ("rows", C.c_int32), ("cols", C.c_int32), ("ld", C.c_int32),
+                ("dst", C.c_void_p)]
 
 
 class ReduceJob(C.Structure):
@@ -83,6 +90,8 @@ def load():
         L.pmlp_opt_parts.restype = i32
         L.pmlp_opt_prepare.argtypes = [vp, i64, f32, vp, vp, vp, vp, vp, f32, i32, vp]
         L.pmlp_adam.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, vp]
+        L.pmlp_adam_mirror.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, i32,
+                                       C.POINTER(MirrorJob), vp]
         L.pmlp_gae_parts.argtypes = [i32]
         L.pmlp_gae_parts.restype = i32
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
@@ -149,13 +158,18 @@ def _convert(jobs):
 
 
 def _gemm(epi, jobs, ksplit=0):
-    """jobs: dicts with A, B, M, N, K and optional bias, yprev, cf, cb, ct (tensors)."""
+    """jobs: dicts with A, B, M, N, K and optional bias, yprev, cf, cb, ct (tensors); the
+    first forward may give af (fp32 rows, A unused) with rows (int64 gather) and xa (bf16
+    copy of the converted rows); the input gradient may give b_kn=1 (B = W[out, in])."""
     def mk(j):
         g = lambda k: j.get(k)  # noqa: E731
         ld = lambda t: 0 if t is None else t.stride(0)  # noqa: E731
-        return GemmJob(_p(j["A"]), _p(j["B"]), _p(g("bias")), _p(g("yprev")), _p(g("cf")), _p(g("cb")), _p(g("ct")),
-                       j["A"].stride(0), j["B"].stride(0), ld(g("yprev")),
-                       0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"])
+        af = g("af")
+        return GemmJob(_p(g("A")), _p(j["B"]), _p(g("bias")), _p(g("yprev")), _p(g("cf")), _p(g("cb")), _p(g("ct")),
+                       ld(g("A")), j["B"].stride(0), ld(g("yprev")),
+                       0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"],
+                       _p(af), _p(g("rows")), _p(g("xa")), ld(af), 0 if af is None else af.shape[1], ld(g("xa")),
+                       int(bool(g("b_kn"))))
     arr = (GemmJob * len(jobs))(*[mk(j) for j in jobs])
     _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
 
@@ -188,16 +202,26 @@ def _tiles(M, N):
         bm, bn = 128, 32
     elif N <= 64:
         bm, bn = 128, 64
+    elif N >= 256 and os.environ.get("PMLP_WIDE_TILE", "0") == "1":  # (the weight gradient's wide tiles)
+        bm, bn = 128, 256
     else:
         bm, bn = 128, 128
     return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
 
 
-def _ksplit(batch, tiles, slab_bytes=0, target_blocks=256, min_rows=256, budget=12 << 20):
+# ~128 workgroups per weight-gradient job: fewer slabs than 256 cut the slab combine
+# 16.8 -> 11.6 us per optimizer step at equal GEMM time (tools/gpu_update_ab.sh)
+_KS_TARGET = int(os.environ.get("PMLP_KSPLIT_TARGET", "128"))  # (A/B knobs of the split-K heuristic)
+_KS_BUDGET = int(os.environ.get("PMLP_KSPLIT_BUDGET_MB", "12")) << 20
+
+
+def _ksplit(batch, tiles, slab_bytes=0, target_blocks=None, min_rows=256, budget=None):
     """Rows per slab of a split-K weight gradient: ~target_blocks workgroups per job (the
     short-K GEMM is latency-bound, so more slabs = more blocks in flight), >= min_rows rows
     per slab, and at most `budget` bytes of fp32 slabs per job (written once by the GEMM,
     read once by the slab combine)."""
+    target_blocks = _KS_TARGET if target_blocks is None else target_blocks
+    budget = _KS_BUDGET if budget is None else budget
     slabs = max(1, min(batch // min_rows, round(target_blocks / tiles)))
     if slab_bytes:
         slabs = max(1, min(slabs, budget // slab_bytes))
