@@ -1057,7 +1057,12 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acol[r] = (lane < ROWS) ? s.u.con.A[r][lane < ROWS ? lane : 0] : 0.f;
     }
-    float lam = 0.f;  // lane r holds lambda_r (one VGPR; read by v_readlane)
+    float lam = 0.f;  // one env per wave: lane r holds lambda_r (one VGPR; broadcast when read)
+    // two envs per wave: every lane holds every lambda of its env (the values are uniform
+    // over the env's lanes), so the sweep reads them from registers instead of broadcasts
+    float lamv[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) lamv[r] = 0.f;
     {
         const float mu = 0.5f * (sp.ground_friction + shape_mu);  // ground contacts
         const float mus = shape_mu;  // self contacts: both shapes carry the env's friction
@@ -1065,6 +1070,67 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         // the diagonal comes from the lane's own row (above), not a 32-way select over
         // acol (32 lane masks, which spilled SGPRs into VGPR lanes)
         float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
+        if constexpr (EPW == 2) {
+            // the sweep-invariant per-row constants broadcast once (256 VGPRs at 2 waves/SIMD
+            // hold them): targets, 1/A_rr, a contact's normal-friction couplings.  The
+            // dependency chain of a contact update then carries 3 broadcasts (v) instead of 12.
+            float ptg[ROWS], pinv[ROWS], pa1[CM], pa2[CM];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) { ptg[r] = 0.f; pinv[r] = 0.f; }
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                pa1[c] = 0.f; pa2[c] = 0.f;
+                if (c < nc) {
+                    const int r = 3 * c;
+                    ptg[r] = bc<EPW>(tg, r);
+                    pinv[r] = bc<EPW>(inv, r); pinv[r + 1] = bc<EPW>(inv, r + 1); pinv[r + 2] = bc<EPW>(inv, r + 2);
+                    pa1[c] = bc<EPW>(acol[r], r + 1); pa2[c] = bc<EPW>(acol[r], r + 2);
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < LM; ++l)
+                if (l < nlimit) {
+                    const int r = 3 * CM + l;
+                    ptg[r] = bc<EPW>(tg, r);
+                    pinv[r] = bc<EPW>(inv, r);
+                }
+            for (int it = 0; it < sp.iters; ++it) {
+#pragma unroll
+                for (int c = 0; c < CM; ++c) {
+                    if (c < nc) {
+                        const int r = 3 * c;
+                        const float lno = lamv[r], l1o = lamv[r + 1], l2o = lamv[r + 2];
+                        const float vn = bc<EPW>(v, r), v1 = bc<EPW>(v, r + 1), v2 = bc<EPW>(v, r + 2);
+                        const float ln = fmaxf(0.f, lno + (ptg[r] - vn) * pinv[r]);
+                        const float dn = ln - lno;
+                        v = fmaf(acol[r], dn, v);
+                        const float v1n = fmaf(pa1[c], dn, v1);
+                        const float v2n = fmaf(pa2[c], dn, v2);
+                        const float lim = (c < ncg ? mu : mus) * ln;
+                        float l1 = l1o - v1n * pinv[r + 1];
+                        float l2 = l2o - v2n * pinv[r + 2];
+                        const float nrm = sqrtf(l1 * l1 + l2 * l2);
+                        if (nrm > lim) {
+                            const float sc = nrm > 0.f ? lim / nrm : 0.f;
+                            l1 *= sc; l2 *= sc;
+                        }
+                        const float d1 = l1 - l1o, d2 = l2 - l2o;
+                        v = fmaf(acol[r + 2], d2, fmaf(acol[r + 1], d1, v));
+                        lamv[r] = ln; lamv[r + 1] = l1; lamv[r + 2] = l2;
+                    }
+                }
+#pragma unroll
+                for (int l = 0; l < LM; ++l) {
+                    if (l < nlimit) {
+                        const int r = 3 * CM + l;
+                        const float lo = lamv[r];
+                        const float ln = fmaxf(0.f, lo + (ptg[r] - bc<EPW>(v, r)) * pinv[r]);
+                        v = fmaf(acol[r], ln - lo, v);
+                        lamv[r] = ln;
+                    }
+                }
+            }
+        } else
         for (int it = 0; it < sp.iters; ++it) {
             // Opaque per sweep: otherwise LICM hoists ~64 loop-invariant readlanes
             // (targets, 1/A_rr, normal-friction couplings) out of the sweep loop; with
@@ -1120,7 +1186,9 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
     for (int c = 0; c < CM; ++c)
         if (c < nc) {
-            const float l0 = bc<EPW>(lam, 3 * c), l1 = bc<EPW>(lam, 3 * c + 1), l2 = bc<EPW>(lam, 3 * c + 2);
+            const float l0 = EPW == 2 ? lamv[3 * c] : bc<EPW>(lam, 3 * c);
+            const float l1 = EPW == 2 ? lamv[3 * c + 1] : bc<EPW>(lam, 3 * c + 1);
+            const float l2 = EPW == 2 ? lamv[3 * c + 2] : bc<EPW>(lam, 3 * c + 2);
             if (lane < n) {
                 z = fmaf(s.u.con.Y[3 * c][lane], l0, z);
                 z = fmaf(s.u.con.Y[3 * c + 1][lane], l1, z);
@@ -1130,7 +1198,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
     for (int l = 0; l < LM; ++l)
         if (l < nlimit) {
-            const float ll = bc<EPW>(lam, 3 * CM + l);
+            const float ll = EPW == 2 ? lamv[3 * CM + l] : bc<EPW>(lam, 3 * CM + l);
             if (lane < n) z = fmaf(s.u.con.Y[3 * CM + l][lane], ll, z);
         }
     {
@@ -1158,7 +1226,9 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
         for (int c = 0; c < CM; ++c)
             if (c < nc) {
-                const float ln = bc<EPW>(lam, 3 * c), l1 = bc<EPW>(lam, 3 * c + 1), l2 = bc<EPW>(lam, 3 * c + 2);
+                const float ln = EPW == 2 ? lamv[3 * c] : bc<EPW>(lam, 3 * c);
+                const float l1 = EPW == 2 ? lamv[3 * c + 1] : bc<EPW>(lam, 3 * c + 1);
+                const float l2 = EPW == 2 ? lamv[3 * c + 2] : bc<EPW>(lam, 3 * c + 2);
                 if (c >= ncg && s.c_body2[c] == lane) {  // self contact: the reaction on the second body
                     const float* fr = s.c_fr[c];
 #pragma unroll
