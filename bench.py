@@ -211,8 +211,20 @@ def cpu_baseline(env, seconds):
     the policy and the PPO update on CPU torch: Go2 4096 and 4 envs,
     all host threads of this job and 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import subprocess
     import bridge
-    lib = bridge.ensure_built()
+    from leggedsim import cabi
+    # the oracle compiled for this host's CPU (-march=native); the portable x86-64-v3 build
+    # that travels with the tree if the host compiler is unavailable
+    build = "gcc -O3 -march=native -ffp-contract=off -fopenmp, built on this host (oracle/Makefile native)"
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True, timeout=180,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        lib = cabi.load_oracle(os.path.join(ROOT, "oracle", "_build", "liblgs_oracle_native.so"))
+    except Exception:
+        lib = bridge.ensure_built()
+        build = ("gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (oracle/Makefile; built in the container, "
+                 "the native build failed on this host)")
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     n = env.num_envs
     half = max(2.0, seconds / 4)
@@ -236,9 +248,7 @@ def cpu_baseline(env, seconds):
             "go2_4_envs": {"env_only_env_steps_per_s": round(rate4_all, 1),
                            "env_only_env_steps_per_s_1_thread": round(rate4_one, 1),
                            "ppo_iter_ms": round(it4 * 1e3, 2)},
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count(),
-            "build": "gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (oracle/Makefile; the .so is built "
-                     "in the container and travels to the GPU box)"}
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "build": build}
 
 
 def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
@@ -423,6 +433,8 @@ def main():
             "h1_2_8192": env_kernel_rate("h1_2", 8192, dev, 50, get_args, task_registry),
         }
         line["other_configs_ppo_iter"] = {
+            # configs[0]: the reference's CPU-runnable case (Go2, 4 envs) on this GPU
+            "go2_4": ppo_iter_rate("go2", 4, dev, 5, 2, get_args, task_registry),
             "g1_rough_heightfield_4096": ppo_iter_rate("g1_rough", 4096, dev, 3, 2, get_args, task_registry),
             "h1_8192": ppo_iter_rate("h1", 8192, dev, 3, 2, get_args, task_registry),
             "h1_2_8192": ppo_iter_rate("h1_2", 8192, dev, 3, 2, get_args, task_registry),

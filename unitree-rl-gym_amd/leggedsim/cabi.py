@@ -204,9 +204,9 @@ def oracle_path():
     return os.path.join(root, "oracle", "_build", "liblgs_oracle.so")
 
 
-def load_oracle():
-    """The CPU oracle (test infrastructure only)."""
-    p = oracle_path()
+def load_oracle(path=None):
+    """The CPU oracle (test infrastructure only); path: another build of it (e.g. -march=native)."""
+    p = path or oracle_path()
     if not os.path.exists(p):
         raise FileNotFoundError(f"oracle not built: {p} (run `make -C oracle`)")
     lib = C.CDLL(p)
