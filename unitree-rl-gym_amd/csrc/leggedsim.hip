@@ -444,6 +444,44 @@ __host__ __device__ constexpr bool l_nz(int i, int k) {  // may L[i][k] (i > k) 
     return CH == 0 || k >= D || i >= D || i <= k + (D - 1 - k) % CH;
 }
 
+// L L^T x = b for an env-uniform b (LDS), every lane computing the whole x from env-uniform
+// LDS reads of L (leaves-first, structural zeros skipped: l_nz).  Forward then backward; per
+// element the operations and their order of the lane-distributed solves in substep().
+template <int D, int CH, int n, int LP>
+__device__ __forceinline__ void uniform_back(const float* b, const float (*L)[LP], const float* Linv, float* xv) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) xv[i] = b[i];
+#pragma unroll
+    for (int i = n - 1; i >= 0; --i) {
+        float t = xv[i];
+#pragma unroll
+        for (int k = n - 1; k > i; --k)
+            if (l_nz<D, CH>(k, i)) t = fmaf(-L[k][i], xv[k], t);
+        xv[i] = t * Linv[i];
+    }
+}
+template <int D, int CH, int n, int LP>
+__device__ __forceinline__ void uniform_solve(const float* b, const float (*L)[LP], const float* Linv, float* xv) {
+    float yv[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        float t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k)
+            if (l_nz<D, CH>(i, k)) t = fmaf(-L[i][k], yv[k], t);
+        yv[i] = t * Linv[i];
+    }
+    // backward from the register vector (the same arithmetic as uniform_back)
+#pragma unroll
+    for (int i = n - 1; i >= 0; --i) {
+        float t = yv[i];
+#pragma unroll
+        for (int k = n - 1; k > i; --k)
+            if (l_nz<D, CH>(k, i)) t = fmaf(-L[k][i], xv[k], t);
+        xv[i] = t * Linv[i];
+    }
+}
+
 template <int D, int B, int ROWS, int CH, int EPW>
 __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const DevModel& md, const DevSim& sp,
                         float added_mass, float shape_mu) {
@@ -704,6 +742,20 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
     }
     STAMP(6);
     // ---- 7. qdd = M^-1 rhs: forward on rows (registers), backward on columns
+    if constexpr (EPW == 2) {
+        // every lane solves the whole system from env-uniform LDS reads of L (no broadcast
+        // chain: the L loads are independent of x and issue ahead; structural zeros
+        // skipped), then keeps its own entry.  Per element the same operations in the same
+        // order as the lane-distributed form below.
+        if (lane < n) s.qf[lane] = x;  // (s.qf is scratch until the free velocity below)
+        __syncthreads();
+        float xv[n];
+        uniform_solve<D, CH, n, Smem<D, B, ROWS>::LP>(s.qf, s.L, s.Linv, xv);
+        x = 0.f;
+#pragma unroll
+        for (int i = 0; i < n; ++i) x = lane == i ? xv[i] : x;
+        __syncthreads();
+    } else {
 #pragma unroll
     for (int i = 0; i < n; ++i) {
         int ln = lane;
@@ -725,6 +777,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
             const float xi = bc<EPW>(x, i);
             x = ln < i ? fmaf(-lc[i], xi, x) : x;
         }
+    }
     }
     // free velocity (classical velocity of the root origin after dt); lane i holds
     // qdd of natural index r = n-1-i, s.qf is in the natural order
@@ -1201,7 +1254,16 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
             const float ll = EPW == 2 ? lamv[3 * CM + l] : bc<EPW>(lam, 3 * CM + l);
             if (lane < n) z = fmaf(s.u.con.Y[3 * CM + l][lane], ll, z);
         }
-    {
+    if constexpr (EPW == 2) {  // the uniform backward solve of step 7
+        __syncthreads();  // (every read of s.tgt / the limit rows is done: reuse s.tgt as scratch)
+        if (lane < n) s.tgt[lane] = z;
+        __syncthreads();
+        float zv[n];
+        uniform_back<D, CH, n, Smem<D, B, ROWS>::LP>(s.tgt, s.L, s.Linv, zv);
+        z = 0.f;
+#pragma unroll
+        for (int i = 0; i < n; ++i) z = lane == i ? zv[i] : z;
+    } else {
         float lc[n];
 #pragma unroll
         for (int k = 0; k < n; ++k) lc[k] = (lane < n && k >= lane) ? s.L[k][lane] : 0.f;
