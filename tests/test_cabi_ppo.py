@@ -1,0 +1,87 @@
+"""libppomlp.so (include/ppo_mlp.h) on the CPU: the library loads and exports every
+function the header declares, the ctypes job structs have the C layout (checked against a
+helper compiled from the header with gcc), and malformed jobs come back as a status with a
+message -- the argument checks run before any HIP call, so no GPU is needed."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ppo_mlp.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"PMLP_API\s+[\w\s\*]+?\b(pmlp_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import torch  # noqa: F401  (the HIP runtime first)
+    from rsl_rl.modules import mfma_mlp
+    return mfma_mlp.load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    for must in ("pmlp_gemm", "pmlp_adam", "pmlp_adam_mirror", "pmlp_ppo_loss_step", "pmlp_gae", "pmlp_lstm_fwd"):
+        assert must in names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_ctypes_job_structs_match_c_layout(tmp_path):
+    from rsl_rl.modules import mfma_mlp as mm
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "ppo_mlp.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
+                   ' sizeof(pmlp_gemm_job), sizeof(pmlp_mirror_job), sizeof(pmlp_convert_job),'
+                   ' sizeof(pmlp_reduce_job)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob)]
+
+
+def _job(**kw):
+    from rsl_rl.modules import mfma_mlp as mm
+    j = mm.GemmJob()
+    j.A, j.B = 16, 16  # non-null, 16-byte aligned (never dereferenced: the checks fail first)
+    j.lda = j.ldb = 64
+    j.M, j.N, j.K = 128, 64, 64
+    j.cb, j.ldcb, j.yprev, j.ldyp = 16, 64, 16, 64
+    for k, v in kw.items():
+        setattr(j, k, v)
+    return j
+
+
+@pytest.mark.parametrize("epi,kw,msg", [
+    (0, dict(b_kn=1), b"B given [K,N]"),          # W[out,in] operand only for the input gradient
+    (2, dict(af=16, kaf=64, ldaf=64), b"fp32 A"),  # fp32-gathered A only for the forward
+    (0, dict(af=16, kaf=96, ldaf=96), b"fp32 A"),  # kaf > K
+    (0, dict(af=16, kaf=64, ldaf=66), b"fp32 A"),  # ldaf not a multiple of 4
+])
+def test_malformed_gemm_jobs_are_refused(lib, epi, kw, msg):
+    from rsl_rl.modules import mfma_mlp as mm
+    arr = (mm.GemmJob * 1)(_job(**kw))
+    assert lib.pmlp_gemm(epi, 1, arr, 0, None) != 0
+    assert msg in lib.pmlp_last_error()
+
+
+def test_mixed_operand_forms_in_one_call_are_refused(lib):
+    from rsl_rl.modules import mfma_mlp as mm
+    arr = (mm.GemmJob * 2)(_job(), _job(b_kn=1))
+    assert lib.pmlp_gemm(2, 2, arr, 0, None) != 0
+    assert b"same operand forms" in lib.pmlp_last_error()
+
+
+def test_adam_mirror_checks_its_jobs(lib):
+    from rsl_rl.modules import mfma_mlp as mm
+    ok = mm.MirrorJob(0, 4, 4, 4, 16)
+    over = mm.MirrorJob(8, 4, 4, 4, 16)  # runs past n = 16
+    for jobs, n_jobs in (((mm.MirrorJob * 1)(over), 1), ((mm.MirrorJob * 9)(*([ok] * 9)), 9)):
+        rc = lib.pmlp_adam_mirror(16, 16, 16, 16, 16, 1.0, 16, 16, 16, 1.0, 0.9, 0.999, 1e-8, n_jobs, jobs, None)
+        assert rc != 0 and b"pmlp_adam_mirror" in lib.pmlp_last_error()
