@@ -88,11 +88,14 @@ typedef struct {
      *      unused.  xa (optional): the converted bf16 rows are also stored to xa[M, ldxa]
      *      (the weight gradient's operand).
      *  b_kn (BWD_DX): B is given as [K,N] (ldb >= N, n contiguous): the layer's weight
-     *      W[out,in] itself, read through transposed LDS reads (no W^T copy).          */
+     *      W[out,in] itself, read through transposed LDS reads (no W^T copy).
+     *  sum_col (PARTIAL_TN, > 0): slab column sum_col (N <= sum_col < ldcf) also receives
+     *      sum_k A[k,m], the product with a column of ones: the bias gradient, without
+     *      the extra (mostly empty) column tile a ones column in B would cost.          */
     const float* af;
     const int64_t* rows;
     pmlp_bf16* xa;
-    int32_t ldaf, kaf, ldxa, b_kn;
+    int32_t ldaf, kaf, ldxa, b_kn, sum_col;
 } pmlp_gemm_job;
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
 

@@ -63,6 +63,8 @@ def _job(**kw):
     (2, dict(af=16, kaf=64, ldaf=64), b"fp32 A"),  # fp32-gathered A only for the forward
     (0, dict(af=16, kaf=96, ldaf=96), b"fp32 A"),  # kaf > K
     (0, dict(af=16, kaf=64, ldaf=66), b"fp32 A"),  # ldaf not a multiple of 4
+    (0, dict(sum_col=64), b"sum_col"),             # the ones product only for PARTIAL_TN
+    (4, dict(sum_col=32, cf=16, ldcf=72, M=64), b"sum_col"),  # sum_col inside the N columns
 ])
 def test_malformed_gemm_jobs_are_refused(lib, epi, kw, msg):
     from rsl_rl.modules import mfma_mlp as mm

@@ -276,6 +276,31 @@ def test_partial_tn_gemm_matches_transposed_partial_and_fp32(K, ks):
         assert err < 1e-5, (M, N, err)
 
 
+@pytest.mark.parametrize("K,ks", [(24576, 1536), (1000, 320)])
+def test_partial_tn_sum_col_is_the_ones_column_product(K, ks):
+    """sum_col (the bias gradient from the A fragments times a ones operand) == the
+    product with a column of ones appended to B, bitwise, and the weight columns are
+    unchanged; column tiles no longer include the ones column."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for M, n in ((512, 48), (256, 512), (128, 256), (12, 128), (1, 128), (64, 56)):
+        mp = (M + 7) // 8 * 8
+        a = torch.randn(K, mp, device="cuda", generator=g).to(torch.bfloat16)
+        b = torch.zeros(K, n + 8, device="cuda", dtype=torch.bfloat16)
+        b[:, :n] = torch.randn(K, n, device="cuda", generator=g).to(torch.bfloat16)
+        b[:, n] = 1.0
+        nsl = (K + ks - 1) // ks
+        s_col = torch.full((nsl, M, n + 8), float("nan"), device="cuda")
+        s_sum = torch.full((nsl, M, n + 8), float("nan"), device="cuda")
+        mfma_mlp._gemm(mfma_mlp.EPI_PARTIAL_TN, [dict(A=a, B=b, M=M, N=n + 8, K=K, cf=s_col)], ksplit=ks)
+        mfma_mlp._gemm(mfma_mlp.EPI_PARTIAL_TN, [dict(A=a, B=b, M=M, N=n, K=K, cf=s_sum, sum_col=n)], ksplit=ks)
+        torch.cuda.synchronize()
+        assert torch.equal(s_sum[..., :n + 1], s_col[..., :n + 1]), (M, n)
+        assert torch.isnan(s_sum[..., n + 1:]).all()  # nothing past the bias column written
+        ref = a[:, :M].float().sum(0)
+        err = float((s_sum[..., n].sum(0) - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, (M, n, err)
+
+
 def test_fused_update_tn_is_bitwise_transposed_copies(monkeypatch):
     """The whole fused update with row-major-only activations (PMLP_TN=1, the default)
     equals the transposed-copy dataflow (PMLP_TN=0) bitwise: losses and parameters."""

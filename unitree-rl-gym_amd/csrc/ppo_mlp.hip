@@ -67,6 +67,7 @@ struct GemmArgs {
     const int64_t* rows;
     bf16* xa;
     int ldaf, kaf, ldxa;
+    int sumc;  // PARTIAL_TN: slab column of sum_k A (the bias gradient), 0 = none
 };
 
 #ifdef PMLP_EXACT_ELU
@@ -92,11 +93,33 @@ __device__ __forceinline__ shortx4 lds_read_tr(const bf16* p) {
 // the observations itself: no conversion launch); bit 1: B is given [K][N] (n contiguous)
 // and staged k-major like PARTIAL_TN's operands (the input gradient reads W[out][in]
 // itself: no transposed weight copy).
-template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0>
+//
+// PF > 1: the k-loop keeps PF k-tiles of global loads in flight (a ring of register
+// stages): a grid of about one block per CU (the split-K weight gradients) is otherwise
+// bound by one load round trip per k-tile.
+template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0, int PF = 1>
 __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
-    const int job = blockIdx.z / gb.slabs, slice = blockIdx.z % gb.slabs;
+    // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (b % 8), each
+    // with its own L2; give every XCD a contiguous range of logical tiles, ordered so that
+    // the tiles sharing an operand panel are neighbours -- the n-tiles of one row block
+    // (forward / input gradient: they share the A rows), the tiles of one split-K slab
+    // (weight gradient: they share its rows of both operands) -- and read it from one L2.
+    int bx, by, bz;
+    {
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), nwg = gx * gy * gridDim.z;
+        const int xcd = b % 8, q = nwg / 8, r = nwg % 8;
+        const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+        if (EPI == PMLP_EPI_PARTIAL || EPI == PMLP_EPI_PARTIAL_TN) {
+            bx = L % gx; by = (L / gx) % gy;
+        } else {
+            by = L % gy; bx = (L / gy) % gx;
+        }
+        bz = L / (gx * gy);
+    }
+    const int job = bz / gb.slabs, slice = bz % gb.slabs;
     const GemmArgs& g = gb.j[job];
-    if ((int)blockIdx.x * BM >= g.M || (int)blockIdx.y * BN >= g.N) return;  // grid covers the largest job
+    if (bx * BM >= g.M || by * BN >= g.N) return;  // grid covers the largest job
     // PARTIAL_TN: A[K,M] and B[K,N] (m / n contiguous: the row-major activations and
     // gradients), staged k-major in LDS and fed to the MFMAs by transposed reads
     constexpr bool TNL = EPI == PMLP_EPI_PARTIAL_TN;
@@ -104,6 +127,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     constexpr bool AF32 = (MODE & 1) != 0;
     constexpr bool BKN = TNL || (MODE & 2) != 0;  // B staged from [K][N]
     static_assert(!BKN || PMLP_NBUF == 1, "k-major B stages one k-tile");
+    static_assert(PF == 1 || PMLP_NBUF == 1, "the load ring feeds one LDS stage");
     constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
     constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
     // TN images [BK][BM + 32]: a row stride of 16 (mod 64) dwords puts the four rows of
@@ -127,7 +151,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int m0 = bx * BM, n0 = by * BN;
     int kb = 0, ke = g.K;
     if (PART) {
         kb = slice * g.ksplit;
@@ -140,9 +164,17 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         for (int j = 0; j < FN; ++j)
 #pragma unroll
             for (int t = 0; t < 16; ++t) acc[i][j][t] = 0.f;
+    // PARTIAL_TN bias gradient: the first column tile's wn == 0 waves also multiply their A
+    // fragments by a column of ones (every output column = sum_k A[k][m])
+    const bool dosum = TNL && g.sumc > 0 && by == 0 && wn == 0;  // wave-uniform
+    floatx16 accs[TNL ? FM : 1];
+#pragma unroll
+    for (int i = 0; i < (TNL ? FM : 1); ++i)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) accs[i][t] = 0.f;
 
-    uint4 ra[AL], rb[BL];
-    auto gload = [&](int k0) {
+    uint4 ra[PF][AL], rb[PF][BL];
+    auto gload = [&](int p, int k0) {
         if constexpr (TNL) {
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
@@ -151,7 +183,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const int gk = k0 + r, gm = m0 + mc;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (c < ACH && gk < ke && gm < g.M) v = *(const uint4*)(g.A + (size_t)gk * g.lda + gm);
-                ra[i] = v;
+                ra[p][i] = v;
             }
         } else if constexpr (AF32) {
 #pragma unroll
@@ -172,9 +204,9 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 #pragma unroll
                         for (int u = 0; u < 8; ++u) t[u] = gk + u < g.kaf ? (bf16)src[u] : (bf16)0.f;
                     }
-                    if (g.xa && blockIdx.y == 0) *(bf16x8*)(g.xa + (size_t)gr * g.ldxa + gk) = t;
+                    if (g.xa && by == 0) *(bf16x8*)(g.xa + (size_t)gr * g.ldxa + gk) = t;
                 }
-                ra[i] = *(const uint4*)&t;
+                ra[p][i] = *(const uint4*)&t;
             }
         } else {
 #pragma unroll
@@ -184,7 +216,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const int gr = m0 + r, gk = k0 + kc;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (c < ACH && gr < g.M && gk < ke) v = *(const uint4*)(g.A + (size_t)gr * g.lda + gk);
-                ra[i] = v;
+                ra[p][i] = v;
             }
         }
         if constexpr (BKN) {
@@ -195,7 +227,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const int gk = k0 + r, gn = n0 + nc;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (c < BCH && gk < ke && gn < g.N) v = *(const uint4*)(g.B + (size_t)gk * g.ldb + gn);
-                rb[i] = v;
+                rb[p][i] = v;
             }
         } else {
 #pragma unroll
@@ -205,35 +237,35 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                 const int gr = n0 + r, gk = k0 + kc;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (c < BCH && gr < g.N && gk < ke) v = *(const uint4*)(g.B + (size_t)gr * g.ldb + gk);
-                rb[i] = v;
+                rb[p][i] = v;
             }
         }
     };
-    auto lstore = [&]() {
+    auto lstore = [&](int p) {
         if constexpr (TNL) {
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
                 const int c = tid + i * NT;
-                if (c < ACH) *(uint4*)(As + (c / (BM / 8)) * SA + (c % (BM / 8)) * 8) = ra[i];
+                if (c < ACH) *(uint4*)(As + (c / (BM / 8)) * SA + (c % (BM / 8)) * 8) = ra[p][i];
             }
         } else {
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
                 const int c = tid + i * NT;
-                if (c < ACH) *(uint4*)(As + (c / CPR) * LS + (c % CPR) * 8) = ra[i];
+                if (c < ACH) *(uint4*)(As + (c / CPR) * LS + (c % CPR) * 8) = ra[p][i];
             }
         }
         if constexpr (BKN) {
 #pragma unroll
             for (int i = 0; i < BL; ++i) {
                 const int c = tid + i * NT;
-                if (c < BCH) *(uint4*)(Bs + (c / (BN / 8)) * SB + (c % (BN / 8)) * 8) = rb[i];
+                if (c < BCH) *(uint4*)(Bs + (c / (BN / 8)) * SB + (c % (BN / 8)) * 8) = rb[p][i];
             }
         } else {
 #pragma unroll
             for (int i = 0; i < BL; ++i) {
                 const int c = tid + i * NT;
-                if (c < BCH) *(uint4*)(Bs + (c / CPR) * LS + (c % CPR) * 8) = rb[i];
+                if (c < BCH) *(uint4*)(Bs + (c / CPR) * LS + (c % CPR) * 8) = rb[p][i];
             }
         }
     };
@@ -272,6 +304,15 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 #pragma unroll
             for (int j = 0; j < FN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (TNL) {
+            if (dosum) {
+                bf16x8 ones;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ones[u] = (bf16)1.f;
+#pragma unroll
+                for (int i = 0; i < FM; ++i) accs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accs[i], 0, 0, 0);
+            }
+        }
     };
     // NKS < 4: a single short k-tile (K <= 16 NKS: 48 for the first layer's forward, 16
     // for the last layer's input gradient), so the k-steps of zero operands are not issued
@@ -280,34 +321,68 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         for (int s = 0; s < NKS; ++s) kstep(s);
     };
 
-    gload(kb);
 #if PMLP_NBUF == 2
     // two LDS stages: the next k-tile is stored into the other stage while this one
     // is consumed -> one barrier per k-tile
-    lstore();
+    gload(0, kb);
+    lstore(0);
     __syncthreads();
     for (int k0 = kb; k0 < ke; k0 += BK) {
         const bool more = k0 + BK < ke;
-        if (more) gload(k0 + BK);
+        if (more) gload(0, k0 + BK);
         compute(k0);
         if (more) {
             As = (As == smem) ? smem + (BM + BN) * LS : smem;
             Bs = As + BM * LS;
-            lstore();
+            lstore(0);
         }
         __syncthreads();
     }
 #else
-    for (int k0 = kb; k0 < ke; k0 += BK) {
-        __syncthreads();
-        lstore();
-        __syncthreads();
-        if (k0 + BK < ke) gload(k0 + BK);
-        compute(k0);
+    if constexpr (PF == 1) {
+        gload(0, kb);
+        for (int k0 = kb; k0 < ke; k0 += BK) {
+            __syncthreads();
+            lstore(0);
+            __syncthreads();
+            if (k0 + BK < ke) gload(0, k0 + BK);
+            compute(k0);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (kb + p * BK < ke) gload(p, kb + p * BK);
+        for (int k0 = kb; k0 < ke; k0 += PF * BK) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) {
+                const int kt = k0 + p * BK;  // block-uniform
+                if (kt < ke) {
+                    __syncthreads();
+                    lstore(p);
+                    __syncthreads();
+                    if (kt + PF * BK < ke) gload(p, kt + PF * BK);
+                    compute(kt);
+                }
+            }
+        }
     }
 #endif
 
     // ---- epilogue: lane owns column (lane&31), rows (t&3)+8(t>>2)+4(lane>>5)
+    if constexpr (TNL) {
+        if (dosum && (lane & 31) == 0) {
+            float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int row = rbase + (t & 3) + 8 * (t >> 2);
+                    if (row < g.M) slab[(size_t)row * g.ldcf + g.sumc] = accs[i][t];
+                }
+            }
+        }
+    }
     constexpr int RCH = BM * BN / 8;  // 16-byte chunks of a bf16 output tile
     if (EPI == PMLP_EPI_BWD_DX) {
         // ELU' operand: the y tile [BM][BN] read coalesced (16-byte chunks along n),
@@ -1415,6 +1490,20 @@ __global__ __launch_bounds__(64 * MLP4_WAVES) void k_mlp4_fwd(Mlp4Jobs jobs, int
     mlp4_layer<H2 / 16, 1, false, true>(x3, dummy, J.W[3], J.b[3], H2, J.NO, lds, J.out, J.ldo, grow, M);
 }
 
+#ifndef PMLP_PF_TN_DEFAULT
+#define PMLP_PF_TN_DEFAULT 1
+#endif
+#ifndef PMLP_PF_DX_DEFAULT
+#define PMLP_PF_DX_DEFAULT 1
+#endif
+#ifndef PMLP_PF_FWD_DEFAULT
+#define PMLP_PF_FWD_DEFAULT 1
+#endif
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
@@ -1428,6 +1517,25 @@ static void launch(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, 
     if (epi == PMLP_EPI_BWD_DX && maxk <= 16) {
         if (bkn) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1, 2>), grid, block, 0, st, gb);
         else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1>), grid, block, 0, st, gb);
+        return;
+    }
+    // load-ring depth per epilogue (PMLP_PF_TN / PMLP_PF_DX / PMLP_PF_FWD, 1..3)
+    static const int pf_tn = env_int("PMLP_PF_TN", PMLP_PF_TN_DEFAULT);
+    static const int pf_dx = env_int("PMLP_PF_DX", PMLP_PF_DX_DEFAULT);
+    static const int pf_fw = env_int("PMLP_PF_FWD", PMLP_PF_FWD_DEFAULT);
+    if (PMLP_NBUF == 1 && epi == PMLP_EPI_PARTIAL_TN && pf_tn > 1) {
+        if (pf_tn == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 2>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 3>), grid, block, 0, st, gb);
+        return;
+    }
+    if (PMLP_NBUF == 1 && epi == PMLP_EPI_BWD_DX && bkn && pf_dx > 1) {
+        if (pf_dx == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2, 2>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2, 3>), grid, block, 0, st, gb);
+        return;
+    }
+    if (PMLP_NBUF == 1 && epi == PMLP_EPI_FWD_HIDDEN && !af && pf_fw > 1) {
+        if (pf_fw == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 0, 2>), grid, block, 0, st, gb);
+        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 0, 3>), grid, block, 0, st, gb);
         return;
     }
     switch (epi) {
@@ -1510,6 +1618,8 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         } else if (J.K % 8 || J.lda % 8 || J.ldb % 8 || J.lda < J.K || J.ldb < J.K || !al16(J.A) || !al16(J.B)) {
             return fail(-1, w + "K, lda, ldb must be multiples of 8 with 16-byte aligned operands");
         }
+        if (J.sum_col && (epi != PMLP_EPI_PARTIAL_TN || J.sum_col < J.N || J.sum_col >= J.ldcf))
+            return fail(-1, w + "sum_col: PARTIAL_TN only, N <= sum_col < ldcf");
         if ((epi == PMLP_EPI_FWD_OUT || part) && (!J.cf || J.ldcf < J.N))
             return fail(-1, w + "fp32 output missing or ldcf < N");
         if ((epi == PMLP_EPI_FWD_HIDDEN || epi == PMLP_EPI_BWD_DX) &&
@@ -1522,6 +1632,7 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         g.lda = J.lda; g.ldb = J.ldb; g.ldyp = J.ldyp; g.ldcf = J.ldcf; g.ldcb = J.ldcb; g.ldct = J.ldct;
         g.M = J.M; g.N = J.N; g.K = J.K; g.ksplit = ksplit;
         g.af = J.af; g.rows = J.rows; g.xa = (bf16*)J.xa; g.ldaf = J.ldaf; g.kaf = J.kaf; g.ldxa = J.ldxa;
+        g.sumc = J.sum_col;
         maxm = std::max(maxm, J.M); maxn = std::max(maxn, J.N); maxk = std::max(maxk, J.K);
     }
     if (part) {

@@ -104,11 +104,12 @@ class FusedPPOStep:
         self.L = L
         self.k0p = [_ceil8(ls[0].in_features) for ls in self.lins]
         tn = self.tn
-        # Activations carry 8 extra columns (tn: row-major) or rows (transposed copies): a
-        # column of ones (then zeros) makes the weight-gradient GEMM's extra output column
-        # the bias gradient (no separate row sums).  The forward reads only the first K.
-        self.xb = [self._ones_col(torch.empty(M, k + 8, dtype=bf, device=dev), k) if tn else
-                   torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
+        # tn: row-major activations of exactly the layer's width (rows of 512 / 256 / 128
+        # features start on 128-byte lines); the weight-gradient GEMM forms the bias
+        # gradient as its A operand times ones (sum_col).  The transposed copies carry 8
+        # extra rows instead: a row of ones (then zeros) makes the GEMM's extra output
+        # column the bias gradient.
+        self.xb = [torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
         self.xt = [None if tn else self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k)
                    for k in self.k0p]
         # W[out, in] in bf16: the forward's B[N, K] and, unchanged, the input gradient's B[K, N]
@@ -121,8 +122,7 @@ class FusedPPOStep:
             mm.MirrorJob(self._offset[id(lin.weight)], lin.out_features, lin.in_features, self.wb[n][l].shape[1],
                          self.wb[n][l].data_ptr())
             for n, ls in enumerate(self.lins) for l, lin in enumerate(ls)])
-        self.y = [[self._ones_col(torch.empty(M, lin.out_features + 8, dtype=bf, device=dev), lin.out_features) if tn
-                   else torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
+        self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
         self.yt = [[None if tn else
                     self._ones_row(torch.empty(lin.out_features + 8, M, dtype=bf, device=dev), lin.out_features)
                     for lin in ls[:-1]] for ls in self.lins]
@@ -144,7 +144,9 @@ class FusedPPOStep:
         self.ks, self.slab, self.dw_stage = [], [], []
         for l in range(L):
             kps = [self.k0p[n] if l == 0 else self.lins[n][l].in_features for n in range(2)]
-            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n] + 8) for n in range(2)),
+            # (the bias column is the TN kernel's ones product, not an extra column tile;
+            # the transposed-copy path takes the same slabs, so the two agree bitwise)
+            ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n]) for n in range(2)),
                             slab_bytes=max(4 * self.lins[n][l].out_features * (kps[n] + 8) for n in range(2)))
             nsl = (M + ks - 1) // ks
             self.ks.append(ks)
@@ -153,12 +155,6 @@ class FusedPPOStep:
             self.dw_stage.append([None if kps[n] == self.lins[n][l].in_features else
                                   torch.empty(self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
         self.opt_partial = torch.empty(mm.load().pmlp_opt_parts(), device=dev)
-
-    @staticmethod
-    def _ones_col(t, k):
-        t[:, k:].zero_()
-        t[:, k].fill_(1.0)
-        return t
 
     @staticmethod
     def _ones_row(t, k):
@@ -269,7 +265,7 @@ class FusedPPOStep:
                 slab = self.slab[l][n]
                 if tn:  # A = dz [M, out], B = activations [M, kp + 8] (row-major)
                     B = xb[n] if l == 0 else self.y[n][l - 1]
-                    gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
+                    gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab, sum_col=kp))
                 else:
                     B = xt[n] if l == 0 else self.yt[n][l - 1]
                     gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))

@@ -41,7 +41,8 @@ class GemmJob(C.Structure):
                 ("ldyp", C.c_int32), ("ldcf", C.c_int32), ("ldcb", C.c_int32), ("ldct", C.c_int32),
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32),
                 ("af", C.c_void_p), ("rows", C.c_void_p), ("xa", C.c_void_p), ("ldaf", C.c_int32),
-                ("kaf", C.c_int32), ("ldxa", C.c_int32), ("b_kn", C.c_int32)]
+                ("kaf", C.c_int32), ("ldxa", C.c_int32), ("b_kn", C.c_int32),
+                ("sum_col", C.c_int32)]
 
 
 class MirrorJob(C.Structure):
@@ -160,7 +161,9 @@ def _convert(jobs):
 def _gemm(epi, jobs, ksplit=0):
     """jobs: dicts with A, B, M, N, K and optional bias, yprev, cf, cb, ct (tensors); the
     first forward may give af (fp32 rows, A unused) with rows (int64 gather) and xa (bf16
-    copy of the converted rows); the input gradient may give b_kn=1 (B = W[out, in])."""
+    copy of the converted rows); the input gradient may give b_kn=1 (B = W[out, in]); a
+    PARTIAL_TN weight gradient may give sum_col (slab column receiving sum_k A = the bias
+    gradient)."""
     def mk(j):
         g = lambda k: j.get(k)  # noqa: E731
         ld = lambda t: 0 if t is None else t.stride(0)  # noqa: E731
@@ -169,7 +172,7 @@ def _gemm(epi, jobs, ksplit=0):
                        ld(g("A")), j["B"].stride(0), ld(g("yprev")),
                        0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"],
                        _p(af), _p(g("rows")), _p(g("xa")), ld(af), 0 if af is None else af.shape[1], ld(g("xa")),
-                       int(bool(g("b_kn"))))
+                       int(bool(g("b_kn"))), int(g("sum_col") or 0))
     arr = (GemmJob * len(jobs))(*[mk(j) for j in jobs])
     _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
 
@@ -222,7 +225,9 @@ def _ksplit(batch, tiles, slab_bytes=0, target_blocks=None, min_rows=256, budget
     read once by the slab combine)."""
     target_blocks = _KS_TARGET if target_blocks is None else target_blocks
     budget = _KS_BUDGET if budget is None else budget
-    slabs = max(1, min(batch // min_rows, round(target_blocks / tiles)))
+    # (floor: a job count of blocks just above a multiple of the 256 CUs leaves a
+    # second round of blocks on a few CUs)
+    slabs = max(1, min(batch // min_rows, target_blocks // tiles))
     if slab_bytes:
         slabs = max(1, min(slabs, budget // slab_bytes))
     ks = (batch + slabs - 1) // slabs
