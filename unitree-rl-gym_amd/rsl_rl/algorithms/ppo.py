@@ -271,9 +271,19 @@ class PPO:
                         returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
                         masks_batch, acc):
         """One PPO optimizer step on one mini-batch (rsl_rl v1.0.2 PPO.update body)."""
-        if self._fused_loss and not self.actor_critic.is_recurrent:
+        recurrent = self.actor_critic.is_recurrent
+        if self._fused_loss and (not recurrent or self._dense_recurrent):
             # same loss, two fused kernels forward + two backward (modules/mfma_mlp.ppo_loss)
-            mu_batch, value_batch = self.actor_critic.mean_and_value(obs_batch, critic_obs_batch)
+            if recurrent:  # dense form: every [T, envs, .] tensor flattened to T*envs rows
+                mu_batch, value_batch = self.actor_critic.mean_and_value_dense(obs_batch, critic_obs_batch,
+                                                                               hid_states_batch, masks_batch)
+                flat = lambda t: t.reshape(-1, t.shape[-1])  # noqa: E731
+                (actions_batch, target_values_batch, advantages_batch, returns_batch, old_actions_log_prob_batch,
+                 old_mu_batch, old_sigma_batch) = map(flat, (actions_batch, target_values_batch, advantages_batch,
+                                                             returns_batch, old_actions_log_prob_batch,
+                                                             old_mu_batch, old_sigma_batch))
+            else:
+                mu_batch, value_batch = self.actor_critic.mean_and_value(obs_batch, critic_obs_batch)
             loss, stats = mfma_mlp.ppo_loss(mu_batch, self.actor_critic.std, value_batch, actions_batch,
                                             old_actions_log_prob_batch, old_mu_batch, old_sigma_batch,
                                             advantages_batch, returns_batch, target_values_batch, self.clip_param,

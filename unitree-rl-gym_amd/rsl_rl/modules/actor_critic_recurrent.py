@@ -59,6 +59,14 @@ class ActorCriticRecurrent(ActorCritic):
         input_a = self.memory_a.dense(observations, hidden_states, reset)
         self.update_distribution(input_a.reshape(-1, input_a.shape[-1]))
 
+    def mean_and_value_dense(self, observations, critic_observations, hidden_states, reset):
+        """(action mean, value) over the T*B rows of a [T,B,.] sequence pair (the fused-loss
+        update: the distribution object is never built)."""
+        input_a = self.memory_a.dense(observations, hidden_states[0], reset)
+        input_c = self.memory_c.dense(critic_observations, hidden_states[1], reset)
+        return (self.actor(input_a.reshape(-1, input_a.shape[-1])),
+                self.critic(input_c.reshape(-1, input_c.shape[-1])))
+
     def evaluate_dense(self, critic_observations, hidden_states, reset):
         input_c = self.memory_c.dense(critic_observations, hidden_states, reset)
         return super().evaluate(input_c.reshape(-1, input_c.shape[-1]))

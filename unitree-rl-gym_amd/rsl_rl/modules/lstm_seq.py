@@ -51,6 +51,19 @@ def _gx(x, w_ih, b_ih, b_hh):
     return torch.addmm(b_ih + b_hh, x.reshape(T * B, I), w_ih.t()).view(T, B, w_ih.shape[0])
 
 
+def _rows_tn(g, x, chunk=2048):
+    """g^T x for tall g [m, p], x [m, q]: a batched product over row chunks, then the sum
+    over chunks (fp32 throughout)."""
+    m = g.shape[0]
+    c = m // chunk
+    if c < 2:
+        return g.t().mm(x)
+    main = torch.bmm(g[:c * chunk].view(c, chunk, -1).transpose(1, 2), x[:c * chunk].view(c, chunk, -1)).sum(0)
+    if c * chunk < m:
+        main += g[c * chunk:].t().mm(x[c * chunk:])
+    return main
+
+
 class _LSTMDense(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, h0, c0, reset, w_ih, w_hh, b_ih, b_hh):
@@ -76,18 +89,21 @@ class _LSTMDense(torch.autograd.Function):
         p = mm._p
         _ok(_lib().pmlp_lstm_bwd(T, B, H, p(whh), p(c0), p(reset), p(c_out), p(gact), p(dh_out.contiguous()), p(dgx),
                                  mm._stream()), "pmlp_lstm_bwd")
-        g = dgx.view(T * B, 4 * H)
-        dw_ih = g.t().mm(x.reshape(T * B, I))
-        hprev = torch.empty(T, B, H, device=x.device)
+        # all three weight gradients from ONE product dgx^T [x | h_prev | 1] over the T*B
+        # rows, split over the rows (a library GEMM puts a 49k-long reduction on a few
+        # output tiles: 170 us per call at H1 scale)
+        xh = torch.empty(T, B, I + H + 1, device=x.device)
+        xh[..., :I].copy_(x)
         if h0 is None:
-            hprev[0].zero_()
+            xh[0, :, I:I + H].zero_()
         else:
-            hprev[0].copy_(h0)
-        hprev[1:].copy_(h_out[:-1])
+            xh[0, :, I:I + H].copy_(h0)
+        xh[1:, :, I:I + H].copy_(h_out[:-1])
         if reset is not None:
-            hprev.masked_fill_(reset.bool().unsqueeze(-1), 0.0)
-        dw_hh = g.t().mm(hprev.view(T * B, H))
-        db = g.sum(0)
+            xh[..., I:I + H].masked_fill_(reset.bool().unsqueeze(-1), 0.0)
+        xh[..., I + H].fill_(1.0)
+        dw = _rows_tn(dgx.view(T * B, 4 * H), xh.view(T * B, I + H + 1))
+        dw_ih, dw_hh, db = dw[:, :I].contiguous(), dw[:, I:I + H].contiguous(), dw[:, I + H].contiguous()
         return None, None, None, None, dw_ih, dw_hh, db, db
 
 
