@@ -22,19 +22,27 @@
 
 namespace {
 
-constexpr int EB = 8;  // envs per workgroup
+// envs per workgroup: 8, or 4 when that leaves fewer than two workgroups per CU (the
+// update's 2048-env mini-batches: a step is latency-bound, so more resident workgroups)
+constexpr int EB_MAX = 8;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Per step every thread issues the NEXT step's global inputs (gx, reset flags; in the
+// backward dh_out, c, c_prev, gates) before this step's work, so one load round trip is
+// in flight behind each step instead of exposed in it; the EB envs' dot products run
+// interleaved (EB independent FMA chains).
+
 // forward over T steps: gact [T,B,4H] (activated gates), c_out [T,B,H], h_out [T,B,H];
 // each of gact / c_out / h_out / h_last / c_last may be null
-template <int H>
+template <int H, int EB>
 __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* __restrict__ gx,
                                                     const float* __restrict__ whh, const float* __restrict__ h0,
                                                     const float* __restrict__ c0, const uint8_t* __restrict__ reset,
                                                     float* __restrict__ h_out, float* __restrict__ c_out,
                                                     float* __restrict__ gact, float* h_last, float* c_last) {
     constexpr int G = 4 * H;
+    constexpr int PE = EB / 4;  // (env, unit) elements per thread in the elementwise phases (EB*H / 4H)
     __shared__ __attribute__((aligned(16))) float hs[EB][H];
     __shared__ float cs[EB][H];
     __shared__ float ga[EB][G];
@@ -46,43 +54,81 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
         const float4 v = *reinterpret_cast<const float4*>(whh + (size_t)j * H + k);
         w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
     }
-    for (int i = j; i < EB * H; i += G) {
-        const int e = i / H, k = i % H, ge = e0 + e;
+#pragma unroll
+    for (int p = 0; p < PE; ++p) {
+        const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
         hs[e][k] = (ge < B && h0) ? h0[(size_t)ge * H + k] : 0.f;
         cs[e][k] = (ge < B && c0) ? c0[(size_t)ge * H + k] : 0.f;
     }
-    __syncthreads();
     const int kind = j / H;  // 0 i, 1 f, 2 g (tanh), 3 o
+    float gxn[EB];
+    bool rsn[PE];
+    auto fetch = [&](int t) {
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+            const int ge = e0 + e;
+            gxn[e] = ge < B ? gx[((size_t)t * B + ge) * G + j] : 0.f;
+        }
+#pragma unroll
+        for (int p = 0; p < PE; ++p) {
+            const int ge = e0 + (j + p * G) / H;
+            rsn[p] = reset && ge < B && reset[(size_t)t * B + ge];
+        }
+    };
+    fetch(0);
+    __syncthreads();
     for (int t = 0; t < T; ++t) {
+        float acc[EB];
+        bool rs[PE];
+#pragma unroll
+        for (int e = 0; e < EB; ++e) acc[e] = gxn[e];
+#pragma unroll
+        for (int p = 0; p < PE; ++p) rs[p] = rsn[p];
+        if (t + 1 < T) fetch(t + 1);
         if (reset) {
-            for (int i = j; i < EB * H; i += G) {
-                const int e = i / H, k = i % H, ge = e0 + e;
-                if (ge < B && reset[(size_t)t * B + ge]) { hs[e][k] = 0.f; cs[e][k] = 0.f; }
+#pragma unroll
+            for (int p = 0; p < PE; ++p) {
+                const int i = j + p * G, e = i / H, k = i % H;
+                if (rs[p]) { hs[e][k] = 0.f; cs[e][k] = 0.f; }
             }
             __syncthreads();
         }
-#pragma unroll 2
+        // env pairs: two interleaved FMA chains (the compiler barrier keeps one pair's LDS
+        // reads in flight at a time instead of hoisting all EB*H/4 of them)
+#pragma unroll
+        for (int e = 0; e < EB; e += 2) {
+#pragma unroll
+            for (int k4 = 0; k4 < H / 4; ++k4) {
+                const float4 ha = reinterpret_cast<const float4*>(hs[e])[k4];
+                const float4 hb = reinterpret_cast<const float4*>(hs[e + 1])[k4];
+                acc[e] = fmaf(ha.x, w[4 * k4], acc[e]);
+                acc[e + 1] = fmaf(hb.x, w[4 * k4], acc[e + 1]);
+                acc[e] = fmaf(ha.y, w[4 * k4 + 1], acc[e]);
+                acc[e + 1] = fmaf(hb.y, w[4 * k4 + 1], acc[e + 1]);
+                acc[e] = fmaf(ha.z, w[4 * k4 + 2], acc[e]);
+                acc[e + 1] = fmaf(hb.z, w[4 * k4 + 2], acc[e + 1]);
+                acc[e] = fmaf(ha.w, w[4 * k4 + 3], acc[e]);
+                acc[e + 1] = fmaf(hb.w, w[4 * k4 + 3], acc[e + 1]);
+            }
+            asm volatile("" ::: "memory");
+        }
+        if (kind == 2) {  // (wave-uniform for H >= 64; a branch, not both functions per env)
+#pragma unroll
+            for (int e = 0; e < EB; ++e) acc[e] = tanhf(acc[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < EB; ++e) acc[e] = sigm(acc[e]);
+        }
+#pragma unroll
         for (int e = 0; e < EB; ++e) {
             const int ge = e0 + e;
-            if (ge >= B) break;
-            const size_t row = (size_t)t * B + ge;
-            float acc = gx[row * G + j];
-            const float4* h4 = reinterpret_cast<const float4*>(hs[e]);
-#pragma unroll
-            for (int k = 0; k < H / 4; ++k) {
-                const float4 hv = h4[k];
-                acc = fmaf(hv.x, w[4 * k], acc);
-                acc = fmaf(hv.y, w[4 * k + 1], acc);
-                acc = fmaf(hv.z, w[4 * k + 2], acc);
-                acc = fmaf(hv.w, w[4 * k + 3], acc);
-            }
-            const float a = kind == 2 ? tanhf(acc) : sigm(acc);
-            ga[e][j] = a;
-            if (gact) gact[row * G + j] = a;
+            ga[e][j] = acc[e];
+            if (gact && ge < B) gact[((size_t)t * B + ge) * G + j] = acc[e];
         }
         __syncthreads();
-        for (int i = j; i < EB * H; i += G) {
-            const int e = i / H, k = i % H, ge = e0 + e;
+#pragma unroll
+        for (int p = 0; p < PE; ++p) {
+            const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
             if (ge >= B) continue;
             const float ig = ga[e][k], fg = ga[e][H + k], gg = ga[e][2 * H + k], og = ga[e][3 * H + k];
             const float c = fg * cs[e][k] + ig * gg;
@@ -95,8 +141,9 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
         }
         __syncthreads();
     }
-    for (int i = j; i < EB * H; i += G) {
-        const int e = i / H, k = i % H, ge = e0 + e;
+#pragma unroll
+    for (int p = 0; p < PE; ++p) {
+        const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
         if (ge >= B) continue;
         if (h_last) h_last[(size_t)ge * H + k] = hs[e][k];
         if (c_last) c_last[(size_t)ge * H + k] = cs[e][k];
@@ -106,12 +153,13 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
 // backward through time: dh_out [T,B,H] -> dgx [T,B,4H] (gradient of the gate
 // pre-activations, i.e. of gx and of the biases).  No gradient flows into h0/c0 or
 // across a reset (the state was replaced by zeros there).
-template <int H>
+template <int H, int EB>
 __global__ __launch_bounds__(4 * H) void k_lstm_bwd(int T, int B, const float* __restrict__ whh,
                                                     const float* __restrict__ c0, const uint8_t* __restrict__ reset,
                                                     const float* __restrict__ c_out, const float* __restrict__ gact,
                                                     const float* __restrict__ dh_out, float* __restrict__ dgx) {
     constexpr int G = 4 * H;
+    constexpr int PE = EB / 4;
     __shared__ float dhn[EB][H], dcn[EB][H];
     __shared__ __attribute__((aligned(16))) float dgs[EB][G];
     __shared__ float red[4][EB][H];
@@ -122,61 +170,97 @@ __global__ __launch_bounds__(4 * H) void k_lstm_bwd(int T, int B, const float* _
     float w[H];
 #pragma unroll
     for (int jj = 0; jj < H; ++jj) w[jj] = whh[(size_t)(q * H + jj) * H + k_own];
-    for (int i = tid; i < EB * H; i += G) {
-        const int e = i / H, k = i % H;
+#pragma unroll
+    for (int p = 0; p < PE; ++p) {
+        const int i = tid + p * G, e = i / H, k = i % H;
         dhn[e][k] = 0.f;
         dcn[e][k] = 0.f;
     }
+    // step inputs of the thread's (env, unit) elements
+    struct In {
+        float dh, c, cp, ig, fg, gg, og;
+        bool rs;
+    };
+    In nx[PE];
+    auto fetch = [&](int t) {
+#pragma unroll
+        for (int p = 0; p < PE; ++p) {
+            const int i = tid + p * G, e = i / H, k = i % H, ge = e0 + e;
+            In& v = nx[p];
+            if (ge >= B) {
+                v = In{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, false};
+                continue;
+            }
+            const size_t row = (size_t)t * B + ge;
+            v.rs = reset && reset[row];
+            v.dh = dh_out[row * H + k];
+            v.c = c_out[row * H + k];
+            v.cp = t > 0 ? c_out[(row - B) * H + k] : (c0 ? c0[(size_t)ge * H + k] : 0.f);
+            const float* a = gact + row * G;
+            v.ig = a[k]; v.fg = a[H + k]; v.gg = a[2 * H + k]; v.og = a[3 * H + k];
+        }
+    };
+    fetch(T - 1);
     __syncthreads();
     for (int t = T - 1; t >= 0; --t) {
+        In cur[PE];
+#pragma unroll
+        for (int p = 0; p < PE; ++p) cur[p] = nx[p];
+        if (t > 0) fetch(t - 1);
         // gate gradients of step t, (env, unit) pairs
-        for (int i = tid; i < EB * H; i += G) {
-            const int e = i / H, k = i % H, ge = e0 + e;
+#pragma unroll
+        for (int p = 0; p < PE; ++p) {
+            const int i = tid + p * G, e = i / H, k = i % H, ge = e0 + e;
             if (ge >= B) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) dgs[e][g * H + k] = 0.f;
                 continue;
             }
+            const In& v = cur[p];
             const size_t row = (size_t)t * B + ge;
-            const bool rs = reset && reset[row];
-            const float dh = dh_out[row * H + k] + dhn[e][k];
-            const float c = c_out[row * H + k];
-            const float cp = rs ? 0.f : (t > 0 ? c_out[(row - B) * H + k] : (c0 ? c0[(size_t)ge * H + k] : 0.f));
-            const float* a = gact + row * G;
-            const float ig = a[k], fg = a[H + k], gg = a[2 * H + k], og = a[3 * H + k];
-            const float tc = tanhf(c);
-            const float dc = dcn[e][k] + dh * og * (1.f - tc * tc);
-            const float d_i = dc * gg * ig * (1.f - ig);
-            const float d_f = dc * cp * fg * (1.f - fg);
-            const float d_g = dc * ig * (1.f - gg * gg);
-            const float d_o = dh * tc * og * (1.f - og);
+            const float dh = v.dh + dhn[e][k];
+            const float cp = v.rs ? 0.f : v.cp;
+            const float tc = tanhf(v.c);
+            const float dc = dcn[e][k] + dh * v.og * (1.f - tc * tc);
+            const float d_i = dc * v.gg * v.ig * (1.f - v.ig);
+            const float d_f = dc * cp * v.fg * (1.f - v.fg);
+            const float d_g = dc * v.ig * (1.f - v.gg * v.gg);
+            const float d_o = dh * tc * v.og * (1.f - v.og);
             dgs[e][k] = d_i; dgs[e][H + k] = d_f; dgs[e][2 * H + k] = d_g; dgs[e][3 * H + k] = d_o;
             float* o = dgx + row * G;
             o[k] = d_i; o[H + k] = d_f; o[2 * H + k] = d_g; o[3 * H + k] = d_o;
-            dcn[e][k] = rs ? 0.f : dc * fg;  // into c_{t-1} (none across a reset)
+            dcn[e][k] = v.rs ? 0.f : dc * v.fg;  // into c_{t-1} (none across a reset)
         }
         __syncthreads();
         // dh_{t-1} = dG W_hh: four partial sums over gate-row quarters, then a fixed-order add
-#pragma unroll 2
-        for (int e = 0; e < EB; ++e) {
-            float acc = 0.f;
-            const float4* d4 = reinterpret_cast<const float4*>(&dgs[e][q * H]);
+        float acc[EB];
 #pragma unroll
-            for (int jj = 0; jj < H / 4; ++jj) {
-                const float4 dv = d4[jj];
-                acc = fmaf(dv.x, w[4 * jj], acc);
-                acc = fmaf(dv.y, w[4 * jj + 1], acc);
-                acc = fmaf(dv.z, w[4 * jj + 2], acc);
-                acc = fmaf(dv.w, w[4 * jj + 3], acc);
+        for (int e = 0; e < EB; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int e = 0; e < EB; e += 2) {
+#pragma unroll
+            for (int j4 = 0; j4 < H / 4; ++j4) {
+                const float4 da = reinterpret_cast<const float4*>(&dgs[e][q * H])[j4];
+                const float4 db = reinterpret_cast<const float4*>(&dgs[e + 1][q * H])[j4];
+                acc[e] = fmaf(da.x, w[4 * j4], acc[e]);
+                acc[e + 1] = fmaf(db.x, w[4 * j4], acc[e + 1]);
+                acc[e] = fmaf(da.y, w[4 * j4 + 1], acc[e]);
+                acc[e + 1] = fmaf(db.y, w[4 * j4 + 1], acc[e + 1]);
+                acc[e] = fmaf(da.z, w[4 * j4 + 2], acc[e]);
+                acc[e + 1] = fmaf(db.z, w[4 * j4 + 2], acc[e + 1]);
+                acc[e] = fmaf(da.w, w[4 * j4 + 3], acc[e]);
+                acc[e + 1] = fmaf(db.w, w[4 * j4 + 3], acc[e + 1]);
             }
-            red[q][e][k_own] = acc;
+            asm volatile("" ::: "memory");
         }
+#pragma unroll
+        for (int e = 0; e < EB; ++e) red[q][e][k_own] = acc[e];
         __syncthreads();
-        for (int i = tid; i < EB * H; i += G) {
-            const int e = i / H, k = i % H, ge = e0 + e;
-            const bool rs = ge < B && reset && reset[(size_t)t * B + ge];
+#pragma unroll
+        for (int p = 0; p < PE; ++p) {
+            const int i = tid + p * G, e = i / H, k = i % H;
             const float s = (red[0][e][k] + red[1][e][k]) + (red[2][e][k] + red[3][e][k]);
-            dhn[e][k] = rs ? 0.f : s;
+            dhn[e][k] = cur[p].rs ? 0.f : s;
         }
         __syncthreads();
     }
@@ -192,8 +276,12 @@ int fail(const std::string& m) {
 template <int H>
 int fwd_h(int T, int B, const float* gx, const float* whh, const float* h0, const float* c0, const uint8_t* reset,
           float* h_out, float* c_out, float* gact, float* h_last, float* c_last, hipStream_t s) {
-    hipLaunchKernelGGL(k_lstm_fwd<H>, dim3((B + EB - 1) / EB), dim3(4 * H), 0, s, T, B, gx, whh, h0, c0, reset, h_out,
-                       c_out, gact, h_last, c_last);
+    if ((B + EB_MAX - 1) / EB_MAX >= 512)
+        hipLaunchKernelGGL((k_lstm_fwd<H, EB_MAX>), dim3((B + EB_MAX - 1) / EB_MAX), dim3(4 * H), 0, s, T, B, gx, whh,
+                           h0, c0, reset, h_out, c_out, gact, h_last, c_last);
+    else
+        hipLaunchKernelGGL((k_lstm_fwd<H, 4>), dim3((B + 3) / 4), dim3(4 * H), 0, s, T, B, gx, whh, h0, c0, reset,
+                           h_out, c_out, gact, h_last, c_last);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd: ") + hipGetErrorString(e));
 }
@@ -201,8 +289,12 @@ int fwd_h(int T, int B, const float* gx, const float* whh, const float* h0, cons
 template <int H>
 int bwd_h(int T, int B, const float* whh, const float* c0, const uint8_t* reset, const float* c_out,
           const float* gact, const float* dh_out, float* dgx, hipStream_t s) {
-    hipLaunchKernelGGL(k_lstm_bwd<H>, dim3((B + EB - 1) / EB), dim3(4 * H), 0, s, T, B, whh, c0, reset, c_out, gact,
-                       dh_out, dgx);
+    if ((B + EB_MAX - 1) / EB_MAX >= 512)
+        hipLaunchKernelGGL((k_lstm_bwd<H, EB_MAX>), dim3((B + EB_MAX - 1) / EB_MAX), dim3(4 * H), 0, s, T, B, whh, c0,
+                           reset, c_out, gact, dh_out, dgx);
+    else
+        hipLaunchKernelGGL((k_lstm_bwd<H, 4>), dim3((B + 3) / 4), dim3(4 * H), 0, s, T, B, whh, c0, reset, c_out, gact,
+                           dh_out, dgx);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd: ") + hipGetErrorString(e));
 }

@@ -181,11 +181,23 @@ class RolloutStorage:
         reset = self._dense_reset
         reset[1:].copy_(self.dones[:-1, :, 0])  # in place: a captured update reads this buffer
         cobs = self.privileged_observations if self.privileged_observations is not None else self.observations
+        # Once per update, every [T, N, .] tensor is regrouped into contiguous per-mini-batch
+        # blocks [num_mini_batches, T, mb, .] (persistent buffers, written in place: a captured
+        # update reads them), so the epochs' steps read contiguous slices and nothing is
+        # copied per optimizer step.
+        srcs = (self.observations, cobs, self.actions, self.values, self.advantages, self.returns,
+                self.actions_log_prob, self.mu, self.sigma, reset)
+        blocks = getattr(self, "_dense_blocks", None)
+        if blocks is None or len(blocks) != len(srcs) or blocks[0].shape[:3] != (num_mini_batches, self.dones.shape[0],
+                                                                               mb):
+            blocks = [torch.empty((num_mini_batches, t.shape[0], mb) + tuple(t.shape[2:]), dtype=t.dtype,
+                                  device=t.device) for t in srcs]
+            self._dense_blocks = blocks
+        for b, t in zip(blocks, srcs):
+            b.copy_(t[:, :num_mini_batches * mb].unflatten(1, (num_mini_batches, mb)).transpose(0, 1))
         for _ in range(num_epochs):
             for i in range(num_mini_batches):
                 sl = slice(i * mb, (i + 1) * mb)
                 hid_a = tuple(h[0][:, sl] for h in self.saved_hidden_states_a)
                 hid_c = tuple(h[0][:, sl] for h in self.saved_hidden_states_c)
-                yield (self.observations[:, sl], cobs[:, sl], self.actions[:, sl], self.values[:, sl],
-                       self.advantages[:, sl], self.returns[:, sl], self.actions_log_prob[:, sl], self.mu[:, sl],
-                       self.sigma[:, sl], (hid_a, hid_c), reset[:, sl])
+                yield tuple(b[i] for b in blocks[:9]) + ((hid_a, hid_c), blocks[9][i])
