@@ -398,6 +398,51 @@ class FusedRollout:
                                                                          ok(time_outs, torch.bool))
 
 
+class RecurrentRollout:
+    """PPO.act + RolloutStorage.add_transitions and PPO.process_env_step for
+    ActorCriticRecurrent on the GPU: the state before the step is saved, both memories
+    step in place on the LSTM kernel, the fp32 MLP heads run as torch ops, and pmlp_act /
+    pmlp_store_step sample the actions, compute the log-probability and write the storage
+    rows and the bootstrapped reward in one launch each (the distribution object and the
+    per-field copies of the generic path are never built).  Capturable: the noise is
+    Philox keyed on a device draw counter, as in FusedRollout."""
+
+    def __init__(self, alg, num_envs):
+        self.alg = alg
+        self.N = int(num_envs)
+        ac = alg.actor_critic
+        self.actions = torch.empty(self.N, ac.std.shape[0], device=ac.std.device)
+        self.draw = torch.zeros((), dtype=torch.int64, device=ac.std.device)
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+
+    def usable(self, obs, cobs, storage):
+        ok = lambda t: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
+                        t.shape[0] == self.N and t.is_contiguous())
+        if not ok(obs) or not ok(cobs) or storage.num_envs != self.N:
+            return False
+        if storage.privileged_observations is None and cobs is not obs:
+            return False
+        return self.alg.actor_critic.rollout_capturable()
+
+    def act(self, obs, cobs, storage, t):
+        ac = self.alg.actor_critic
+        storage._save_hidden_states(ac.get_hidden_states())  # the state BEFORE this step
+        mu = ac.actor(ac.memory_a(obs).squeeze(0)).contiguous()
+        value = ac.critic(ac.memory_c(cobs).squeeze(0)).contiguous()
+        A = self.actions.shape[1]
+        priv = storage.privileged_observations
+        P = mm._p
+        mm._ok(mm.load().pmlp_act(P(mu), P(ac.std.detach()), P(value), P(obs), P(cobs) if priv is not None else None,
+                                  self.N, A, obs.shape[1], cobs.shape[1] if priv is not None else 0, P(self.draw),
+                                  self.seed, P(self.actions), P(storage.actions[t]), P(storage.actions_log_prob[t]),
+                                  P(storage.mu[t]), P(storage.sigma[t]), P(storage.values[t]),
+                                  P(storage.observations[t]), P(priv[t]) if priv is not None else None,
+                                  mm._stream()), "pmlp_act")
+        return self.actions
+
+    store = FusedRollout.store
+
+
 def gae(storage, last_values, gamma, lam, world_size=1):
     """RolloutStorage.compute_returns on the GPU in two launches (pmlp_gae): GAE
     backwards over T per env, then advantage normalisation.  world_size > 1: the

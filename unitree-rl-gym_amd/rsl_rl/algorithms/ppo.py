@@ -114,6 +114,9 @@ class PPO:
                 self._rollout = fused_step.FusedRollout(self._fused, num_envs) if num_envs % 8 == 0 else None
             except ValueError:
                 self._fused = self._rollout = None
+        if self.actor_critic.is_recurrent and self._rollout is None and str(self.device).startswith("cuda") and \
+                hasattr(self.actor_critic, "rollout_capturable"):
+            self._rollout = fused_step.RecurrentRollout(self, num_envs)
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -133,6 +136,7 @@ class PPO:
             tr.actions, tr.values, tr.actions_log_prob = st.actions[t], st.values[t], st.actions_log_prob[t]
             tr.action_mean, tr.action_sigma = st.mu[t], st.sigma[t]
             tr.observations, tr.critic_observations = obs, critic_obs
+            tr.hidden_states = None
             self._stored_t = t
             return actions
         if self.actor_critic.is_recurrent:
