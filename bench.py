@@ -274,7 +274,7 @@ def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
     out = {"num_envs": n, "policy": runner.cfg["policy_class_name"], "decimation": env_cfg.control.decimation,
            "ppo_iter_ms": round(el / iters * 1e3, 3), "env_steps_per_s": round(n * T * iters / el, 1),
            "rollout_graph": runner._rollout_graph is not None,
-           "update_graph": getattr(runner.alg, "_graph", None) is not None,
+           "update_graph": (getattr(runner.alg, "_graph", None) or getattr(runner.alg, "_fgraph", None)) is not None,
            "domain_rand": bool(env_cfg.domain_rand.randomize_friction or env_cfg.domain_rand.randomize_base_mass),
            "terrain": env_cfg.terrain.mesh_type, "iters_timed": iters}
     env.close()
