@@ -160,6 +160,11 @@ PMLP_API int pmlp_opt_prepare(const float* grad, int64_t n, float grad_scale, fl
 PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float grad_scale, const float* partial, const float* step, const float* lr, float max_norm,
                        float beta1, float beta2, float eps, void* stream);
+/* For a torch-optimizer step on the fused loss (the recurrent policy): from stats = [surrogate,
+ * value, kl, entropy], acc[0] += value loss, acc[1] += surrogate loss (acc may be NULL) and, when
+ * adaptive != 0, the KL rule of rsl_rl's adaptive schedule updates lr[0]; one launch.          */
+PMLP_API int pmlp_loss_bookkeeping(const float* stats, float* lr, float* acc, float desired_kl, int32_t adaptive,
+                                   void* stream);
 /* pmlp_adam that also refreshes bf16 copies of the updated weights (the GEMM operands):
  * param[offset + r*cols + c] -> dst[r*ld + c] for every mirror job, so no conversion launch
  * precedes the next forward.  At most PMLP_MAX_MIRROR jobs, disjoint parameter ranges.   */
@@ -258,6 +263,14 @@ PMLP_API int pmlp_lstm_supported(int32_t hidden);
 PMLP_API int pmlp_lstm_fwd(int32_t T, int32_t B, int32_t H, const float* gx, const float* whh, const float* h0,
                            const float* c0, const uint8_t* reset, float* h_out, float* c_out, float* gact,
                            float* h_last, float* c_last, void* stream);
+/* pmlp_lstm_fwd with the input projection fused in: x [T,B,I] (I <= 64), wih [4H,I], bih / bhh [4H]
+ * (either may be NULL) instead of gx; xh (optional) [T,B,I+H+1] receives [x | h_prev | 1] per row
+ * (h_prev = the state the step starts from, after a reset): the operand of the weight gradients
+ * dW_ih, dW_hh and the bias (dgx^T xh). */
+PMLP_API int pmlp_lstm_fwd_x(int32_t T, int32_t B, int32_t H, int32_t I, const float* x, const float* wih,
+                             const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
+                             const uint8_t* reset, float* h_out, float* c_out, float* gact, float* h_last,
+                             float* c_last, float* xh, void* stream);
 PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0, const uint8_t* reset,
                            const float* c_out, const float* gact, const float* dh_out, float* dgx, void* stream);
 

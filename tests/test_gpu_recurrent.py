@@ -15,12 +15,14 @@ from rsl_rl.modules import ActorCriticRecurrent  # noqa: E402
 from rsl_rl.modules import lstm_seq  # noqa: E402
 
 
-@pytest.mark.parametrize("H", [32, 64, 128])
-def test_lstm_kernels_match_torch(H):
+@pytest.mark.parametrize("H,I", [(32, 47), (64, 47), (128, 47), (64, 17), (64, 64), (64, 80)])
+def test_lstm_kernels_match_torch(H, I):
     """Forward outputs and the four parameter gradients of the dense LSTM (resets inside
-    the sequence, a carried initial state) vs the same recurrence in torch fp32 ops."""
-    torch.manual_seed(H)
-    T, B, I = 24, 1000, 47
+    the sequence, a carried initial state) vs the same recurrence in torch fp32 ops.  I <= 64:
+    the input projection inside the sequence kernel (pmlp_lstm_fwd_x); I = 80: a GEMM
+    beforehand (pmlp_lstm_fwd)."""
+    torch.manual_seed(H + I)
+    T, B = 24, 1000
     rnn = torch.nn.LSTM(I, H).cuda()
     x = torch.randn(T, B, I, device="cuda")
     h0 = 0.5 * torch.randn(1, B, H, device="cuda")
@@ -40,6 +42,30 @@ def test_lstm_kernels_match_torch(H):
     # without resets and from zeros, the reference statement is nn.LSTM itself
     y0 = lstm_seq.lstm_dense(rnn, x, None, None, None)
     torch.testing.assert_close(y0, rnn(x)[0], rtol=1e-5, atol=2e-6)
+
+
+def test_lstm_fused_input_writes_the_weight_gradient_operand():
+    """pmlp_lstm_fwd_x's xh = [x | h_prev | 1]: h_prev is the state each step starts from
+    (h0 at t = 0, zero after a reset, else the previous output)."""
+    torch.manual_seed(1)
+    T, B, I, H = 6, 37, 41, 64
+    rnn = torch.nn.LSTM(I, H).cuda()
+    x = torch.randn(T, B, I, device="cuda")
+    h0 = torch.randn(B, H, device="cuda")
+    c0 = torch.randn(B, H, device="cuda")
+    reset = (torch.rand(T, B, device="cuda") < 0.3).to(torch.uint8)
+    h_out = torch.empty(T, B, H, device="cuda")
+    xh = torch.full((T, B, I + H + 1), float("nan"), device="cuda")
+    p = lstm_seq.mm._p
+    lib = lstm_seq._lib()
+    w = [t.detach().contiguous() for t in (rnn.weight_ih_l0, rnn.bias_ih_l0, rnn.bias_hh_l0, rnn.weight_hh_l0)]
+    assert lib.pmlp_lstm_fwd_x(T, B, H, I, p(x), p(w[0]), p(w[1]), p(w[2]), p(w[3]), p(h0), p(c0), p(reset),
+                               p(h_out), None, None, None, None, p(xh), lstm_seq.mm._stream()) == 0
+    torch.cuda.synchronize()
+    hp = torch.cat([h0.unsqueeze(0), h_out[:-1]]) * (reset == 0).float().unsqueeze(-1)
+    assert torch.equal(xh[..., :I], x)
+    assert torch.equal(xh[..., I:I + H], hp)
+    assert bool((xh[..., I + H] == 1).all())
 
 
 def test_lstm_rollout_step_in_place_matches_nn_lstm():

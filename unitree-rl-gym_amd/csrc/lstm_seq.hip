@@ -34,64 +34,143 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 // interleaved (EB independent FMA chains).
 
 // forward over T steps: gact [T,B,4H] (activated gates), c_out [T,B,H], h_out [T,B,H];
-// each of gact / c_out / h_out / h_last / c_last may be null
-template <int H, int EB>
-__global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* __restrict__ gx,
-                                                    const float* __restrict__ whh, const float* __restrict__ h0,
-                                                    const float* __restrict__ c0, const uint8_t* __restrict__ reset,
-                                                    float* __restrict__ h_out, float* __restrict__ c_out,
-                                                    float* __restrict__ gact, float* h_last, float* c_last) {
+// each of gact / c_out / h_out / h_last / c_last may be null.
+// IP == 0: the gate pre-activations come as gx [T,B,4H] (x W_ih^T + b, a GEMM beforehand).
+// IP > 0: the input projection is fused in: x [T,B,I] (I <= IP) is staged through LDS per
+// step and thread j adds b_ih[j] + b_hh[j] + x . W_ih[j] (its W_ih row in registers) --
+// no [T,B,4H] gx round trip through HBM; xh (optional) receives [x | h_prev | 1] per row,
+// the operand of the weight gradients (h_prev: the state the step starts from, after a
+// reset).
+struct FwdArgs {
+    int T, B, I;
+    const float* gx;
+    const float* x;
+    const float* wih;
+    const float* bih;
+    const float* bhh;
+    const float* whh;
+    const float* h0;
+    const float* c0;
+    const uint8_t* reset;
+    float* h_out;
+    float* c_out;
+    float* gact;
+    float* h_last;
+    float* c_last;
+    float* xh;
+};
+
+template <int H, int EB, int IP>
+__global__ __launch_bounds__(4 * H) void k_lstm_fwd(FwdArgs a) {
     constexpr int G = 4 * H;
     constexpr int PE = EB / 4;  // (env, unit) elements per thread in the elementwise phases (EB*H / 4H)
+    constexpr int XS = IP > 0 ? IP : 4;
+    constexpr int XPT = IP > 0 ? (EB * IP + G - 1) / G : 1;  // staged x elements per thread
     __shared__ __attribute__((aligned(16))) float hs[EB][H];
     __shared__ float cs[EB][H];
     __shared__ float ga[EB][G];
+    __shared__ __attribute__((aligned(16))) float xs[EB][XS];
+    const int T = a.T, B = a.B, I = a.I;
     const int j = threadIdx.x;
     const int e0 = blockIdx.x * EB;
     float w[H];
 #pragma unroll
     for (int k = 0; k < H; k += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(whh + (size_t)j * H + k);
+        const float4 v = *reinterpret_cast<const float4*>(a.whh + (size_t)j * H + k);
         w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+    }
+    float wi[IP > 0 ? IP : 1];
+    float bj = 0.f;
+    if constexpr (IP > 0) {
+#pragma unroll
+        for (int i = 0; i < IP; ++i) wi[i] = i < I ? a.wih[(size_t)j * I + i] : 0.f;
+        bj = (a.bih ? a.bih[j] : 0.f) + (a.bhh ? a.bhh[j] : 0.f);
     }
 #pragma unroll
     for (int p = 0; p < PE; ++p) {
         const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
-        hs[e][k] = (ge < B && h0) ? h0[(size_t)ge * H + k] : 0.f;
-        cs[e][k] = (ge < B && c0) ? c0[(size_t)ge * H + k] : 0.f;
+        hs[e][k] = (ge < B && a.h0) ? a.h0[(size_t)ge * H + k] : 0.f;
+        cs[e][k] = (ge < B && a.c0) ? a.c0[(size_t)ge * H + k] : 0.f;
     }
     const int kind = j / H;  // 0 i, 1 f, 2 g (tanh), 3 o
-    float gxn[EB];
+    float gxn[IP > 0 ? 1 : EB];
+    float xn[XPT];
     bool rsn[PE];
     auto fetch = [&](int t) {
+        if constexpr (IP == 0) {
 #pragma unroll
-        for (int e = 0; e < EB; ++e) {
-            const int ge = e0 + e;
-            gxn[e] = ge < B ? gx[((size_t)t * B + ge) * G + j] : 0.f;
+            for (int e = 0; e < EB; ++e) {
+                const int ge = e0 + e;
+                gxn[e] = ge < B ? a.gx[((size_t)t * B + ge) * G + j] : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < XPT; ++p) {
+                const int q = j + p * G, e = q / IP, i = q % IP, ge = e0 + e;
+                xn[p] = (q < EB * IP && ge < B && i < I) ? a.x[((size_t)t * B + ge) * I + i] : 0.f;
+            }
         }
 #pragma unroll
         for (int p = 0; p < PE; ++p) {
             const int ge = e0 + (j + p * G) / H;
-            rsn[p] = reset && ge < B && reset[(size_t)t * B + ge];
+            rsn[p] = a.reset && ge < B && a.reset[(size_t)t * B + ge];
         }
     };
     fetch(0);
     __syncthreads();
+    const int RL = I + H + 1;  // xh row
     for (int t = 0; t < T; ++t) {
         float acc[EB];
         bool rs[PE];
+        if constexpr (IP == 0) {
 #pragma unroll
-        for (int e = 0; e < EB; ++e) acc[e] = gxn[e];
+            for (int e = 0; e < EB; ++e) acc[e] = gxn[e];
+        } else {
+#pragma unroll
+            for (int p = 0; p < XPT; ++p) {
+                const int q = j + p * G;
+                if (q < EB * IP) xs[q / IP][q % IP] = xn[p];
+            }
+#pragma unroll
+            for (int e = 0; e < EB; ++e) acc[e] = bj;
+        }
 #pragma unroll
         for (int p = 0; p < PE; ++p) rs[p] = rsn[p];
         if (t + 1 < T) fetch(t + 1);
-        if (reset) {
+        if (a.reset) {
 #pragma unroll
             for (int p = 0; p < PE; ++p) {
                 const int i = j + p * G, e = i / H, k = i % H;
                 if (rs[p]) { hs[e][k] = 0.f; cs[e][k] = 0.f; }
             }
-            __syncthreads();
+        }
+        if (IP > 0 || a.reset) __syncthreads();
+        if constexpr (IP > 0) {
+            if (a.xh) {
+                for (int q = j; q < EB * RL; q += G) {
+                    const int e = q / RL, c = q % RL, ge = e0 + e;
+                    if (ge < B)
+                        a.xh[((size_t)t * B + ge) * RL + c] = c < I ? xs[e][c] : (c < I + H ? hs[e][c - I] : 1.f);
+                }
+            }
+            // input projection: env pairs, two interleaved FMA chains from the bias
+#pragma unroll
+            for (int e = 0; e < EB; e += 2) {
+#pragma unroll
+                for (int i4 = 0; i4 < IP / 4; ++i4) {
+                    const float4 xa = reinterpret_cast<const float4*>(xs[e])[i4];
+                    const float4 xb = reinterpret_cast<const float4*>(xs[e + 1])[i4];
+                    acc[e] = fmaf(xa.x, wi[4 * i4], acc[e]);
+                    acc[e + 1] = fmaf(xb.x, wi[4 * i4], acc[e + 1]);
+                    acc[e] = fmaf(xa.y, wi[4 * i4 + 1], acc[e]);
+                    acc[e + 1] = fmaf(xb.y, wi[4 * i4 + 1], acc[e + 1]);
+                    acc[e] = fmaf(xa.z, wi[4 * i4 + 2], acc[e]);
+                    acc[e + 1] = fmaf(xb.z, wi[4 * i4 + 2], acc[e + 1]);
+                    acc[e] = fmaf(xa.w, wi[4 * i4 + 3], acc[e]);
+                    acc[e + 1] = fmaf(xb.w, wi[4 * i4 + 3], acc[e + 1]);
+                }
+                asm volatile("" ::: "memory");
+            }
         }
         // env pairs: two interleaved FMA chains (the compiler barrier keeps one pair's LDS
         // reads in flight at a time instead of hoisting all EB*H/4 of them)
@@ -123,7 +202,7 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
         for (int e = 0; e < EB; ++e) {
             const int ge = e0 + e;
             ga[e][j] = acc[e];
-            if (gact && ge < B) gact[((size_t)t * B + ge) * G + j] = acc[e];
+            if (a.gact && ge < B) a.gact[((size_t)t * B + ge) * G + j] = acc[e];
         }
         __syncthreads();
 #pragma unroll
@@ -136,8 +215,8 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
             cs[e][k] = c;
             hs[e][k] = h;
             const size_t o = ((size_t)t * B + ge) * H + k;
-            if (h_out) h_out[o] = h;
-            if (c_out) c_out[o] = c;
+            if (a.h_out) a.h_out[o] = h;
+            if (a.c_out) a.c_out[o] = c;
         }
         __syncthreads();
     }
@@ -145,8 +224,8 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(int T, int B, const float* _
     for (int p = 0; p < PE; ++p) {
         const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
         if (ge >= B) continue;
-        if (h_last) h_last[(size_t)ge * H + k] = hs[e][k];
-        if (c_last) c_last[(size_t)ge * H + k] = cs[e][k];
+        if (a.h_last) a.h_last[(size_t)ge * H + k] = hs[e][k];
+        if (a.c_last) a.c_last[(size_t)ge * H + k] = cs[e][k];
     }
 }
 
@@ -273,17 +352,22 @@ int fail(const std::string& m) {
     return -1;
 }
 
-template <int H>
-int fwd_h(int T, int B, const float* gx, const float* whh, const float* h0, const float* c0, const uint8_t* reset,
-          float* h_out, float* c_out, float* gact, float* h_last, float* c_last, hipStream_t s) {
-    if ((B + EB_MAX - 1) / EB_MAX >= 512)
-        hipLaunchKernelGGL((k_lstm_fwd<H, EB_MAX>), dim3((B + EB_MAX - 1) / EB_MAX), dim3(4 * H), 0, s, T, B, gx, whh,
-                           h0, c0, reset, h_out, c_out, gact, h_last, c_last);
+template <int H, int IP>
+int fwd_launch(const FwdArgs& a, hipStream_t s) {
+    if ((a.B + EB_MAX - 1) / EB_MAX >= 512)
+        hipLaunchKernelGGL((k_lstm_fwd<H, EB_MAX, IP>), dim3((a.B + EB_MAX - 1) / EB_MAX), dim3(4 * H), 0, s, a);
     else
-        hipLaunchKernelGGL((k_lstm_fwd<H, 4>), dim3((B + 3) / 4), dim3(4 * H), 0, s, T, B, gx, whh, h0, c0, reset,
-                           h_out, c_out, gact, h_last, c_last);
+        hipLaunchKernelGGL((k_lstm_fwd<H, 4, IP>), dim3((a.B + 3) / 4), dim3(4 * H), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd: ") + hipGetErrorString(e));
+}
+
+template <int H>
+int fwd_h(const FwdArgs& a, hipStream_t s) {
+    if (!a.x) return fwd_launch<H, 0>(a, s);
+    if (a.I <= 32) return fwd_launch<H, 32>(a, s);
+    if (a.I <= 48) return fwd_launch<H, 48>(a, s);
+    return fwd_launch<H, 64>(a, s);
 }
 
 template <int H>
@@ -305,18 +389,34 @@ PMLP_API const char* pmlp_lstm_last_error(void) { return g_err.c_str(); }
 
 PMLP_API int pmlp_lstm_supported(int32_t hidden) { return hidden == 32 || hidden == 64 || hidden == 128; }
 
+static int fwd_dispatch(const FwdArgs& a, int H, hipStream_t s) {
+    switch (H) {
+    case 32: return fwd_h<32>(a, s);
+    case 64: return fwd_h<64>(a, s);
+    case 128: return fwd_h<128>(a, s);
+    default: return fail("pmlp_lstm_fwd: hidden size must be 32, 64 or 128");
+    }
+}
+
 PMLP_API int pmlp_lstm_fwd(int32_t T, int32_t B, int32_t H, const float* gx, const float* whh, const float* h0,
                            const float* c0, const uint8_t* reset, float* h_out, float* c_out, float* gact,
                            float* h_last, float* c_last, void* stream) {
     if (T <= 0 || B <= 0 || !gx || !whh) return fail("pmlp_lstm_fwd: empty sequence or null gx/whh");
     if (((uintptr_t)whh & 15u) != 0) return fail("pmlp_lstm_fwd: whh must be 16-byte aligned");
-    hipStream_t s = (hipStream_t)stream;
-    switch (H) {
-    case 32: return fwd_h<32>(T, B, gx, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, s);
-    case 64: return fwd_h<64>(T, B, gx, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, s);
-    case 128: return fwd_h<128>(T, B, gx, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, s);
-    default: return fail("pmlp_lstm_fwd: hidden size must be 32, 64 or 128");
-    }
+    FwdArgs a{T, B, 0, gx, nullptr, nullptr, nullptr, nullptr, whh, h0, c0, reset, h_out, c_out, gact,
+              h_last, c_last, nullptr};
+    return fwd_dispatch(a, H, (hipStream_t)stream);
+}
+
+PMLP_API int pmlp_lstm_fwd_x(int32_t T, int32_t B, int32_t H, int32_t I, const float* x, const float* wih,
+                             const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
+                             const uint8_t* reset, float* h_out, float* c_out, float* gact, float* h_last,
+                             float* c_last, float* xh, void* stream) {
+    if (T <= 0 || B <= 0 || !x || !wih || !whh) return fail("pmlp_lstm_fwd_x: empty sequence or null x/wih/whh");
+    if (I <= 0 || I > 64) return fail("pmlp_lstm_fwd_x: input size must be 1..64");
+    if (((uintptr_t)whh & 15u) != 0) return fail("pmlp_lstm_fwd_x: whh must be 16-byte aligned");
+    FwdArgs a{T, B, I, nullptr, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, xh};
+    return fwd_dispatch(a, H, (hipStream_t)stream);
 }
 
 PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0, const uint8_t* reset,

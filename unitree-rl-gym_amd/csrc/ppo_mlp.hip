@@ -1033,6 +1033,26 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_final(LossArgs a, const fl
 #define PMLP_OPT_THREADS 256
 #define PMLP_OPT_PARTS 256
 
+// The per-step bookkeeping of a torch-optimizer PPO step in one thread: the logged
+// losses and the KL-adaptive learning rate (rsl_rl v1.0.2 PPO.update), from the fused
+// loss's stats = [surrogate, value, kl, entropy] (the ~10 small torch ops it replaces
+// are each a launch).
+__global__ void k_loss_bookkeeping(const float* __restrict__ stats, float* lr, float* acc, float desired_kl,
+                                   int adaptive) {
+    if (threadIdx.x != 0) return;
+    if (acc) {
+        acc[0] += stats[1];
+        acc[1] += stats[0];
+    }
+    if (adaptive) {
+        const float kl = stats[2];
+        float l = lr[0];
+        if (kl > desired_kl * 2.f) l = fmaxf(l / 1.5f, 1e-5f);
+        else if (kl < desired_kl / 2.f && kl > 0.f) l = fminf(l * 1.5f, 1e-2f);
+        lr[0] = l;
+    }
+}
+
 // partial[b] = sum of (scale*g)^2 over block b's grid-stride share; block 0 also
 // advances Adam's step and, from stats = [surrogate, value, kl, entropy] (sums over
 // ranks when scale = 1/world), accumulates the logged losses and adapts the LR.
@@ -1778,6 +1798,15 @@ PMLP_API int pmlp_opt_prepare(const float* grad, int64_t n, float grad_scale, fl
     hipLaunchKernelGGL(k_opt_prepare, dim3(PMLP_OPT_PARTS), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, grad, n,
                        grad_scale, partial, step, stats, lr, acc, desired_kl, adaptive);
     PMLP_CHECK_LAUNCH("pmlp_opt_prepare");
+    return 0;
+}
+
+PMLP_API int pmlp_loss_bookkeeping(const float* stats, float* lr, float* acc, float desired_kl, int32_t adaptive,
+                                   void* stream) {
+    if (!stats || (adaptive && !lr)) return fail(-1, "pmlp_loss_bookkeeping: null stats (or lr with adaptive)");
+    hipLaunchKernelGGL(k_loss_bookkeeping, dim3(1), dim3(64), 0, (hipStream_t)stream, stats, lr, acc, desired_kl,
+                       adaptive);
+    PMLP_CHECK_LAUNCH("pmlp_loss_bookkeeping");
     return 0;
 }
 

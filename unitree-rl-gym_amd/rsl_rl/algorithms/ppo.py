@@ -293,7 +293,15 @@ class PPO:
                                             advantages_batch, returns_batch, target_values_batch, self.clip_param,
                                             self.use_clipped_value_loss, self.value_loss_coef, self.entropy_coef)
             surrogate_loss, value_loss = stats[0], stats[1]
-            if self.desired_kl is not None and self.schedule == "adaptive":
+            adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+            if self.world_size == 1 and self._lr_is_tensor and self._diag is None:
+                # the logged losses and the adaptive LR in one launch (pmlp_loss_bookkeeping)
+                mfma_mlp._ok(mfma_mlp.load().pmlp_loss_bookkeeping(
+                    mfma_mlp._p(stats), mfma_mlp._p(self._lr), mfma_mlp._p(acc),
+                    float(self.desired_kl) if adaptive else 0.0, int(adaptive), mfma_mlp._stream()),
+                    "pmlp_loss_bookkeeping")
+                acc = None
+            elif adaptive:
                 self._adapt_lr(stats[2])
         else:
             loss, surrogate_loss, value_loss = self._reference_loss(
@@ -310,8 +318,9 @@ class PPO:
         nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
         self.optimizer.step()
         with torch.no_grad():
-            acc[0] += value_loss.detach()
-            acc[1] += surrogate_loss.detach()
+            if acc is not None:
+                acc[0] += value_loss.detach()
+                acc[1] += surrogate_loss.detach()
             if self._diag is not None:  # debugging aid: per-step losses (also inside a captured graph)
                 row = self._diag[self._diag_i % self._diag.shape[0]]
                 row[:2].copy_(torch.stack([value_loss.detach(), surrogate_loss.detach()]))

@@ -14,6 +14,7 @@ around pmlp_lstm_fwd / pmlp_lstm_bwd plus three GEMMs for the weight gradients);
 ``lstm_dense_reference`` is the same recurrence in plain torch ops (CPU, tests).
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -31,6 +32,7 @@ def _lib():
         L.pmlp_lstm_supported.argtypes = [i32]
         L.pmlp_lstm_fwd.argtypes = [i32, i32, i32] + [vp] * 10 + [vp]
         L.pmlp_lstm_bwd.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
+        L.pmlp_lstm_fwd_x.argtypes = [i32, i32, i32, i32] + [vp] * 14 + [vp]
         _bound = True
     return L
 
@@ -51,9 +53,13 @@ def _gx(x, w_ih, b_ih, b_hh):
     return torch.addmm(b_ih + b_hh, x.reshape(T * B, I), w_ih.t()).view(T, B, w_ih.shape[0])
 
 
-def _rows_tn(g, x, chunk=2048):
+_ROWS_CHUNK = int(os.environ.get("LSTM_ROWS_CHUNK", "1024"))  # (A/B knob: tools/gpu_chunk_ab.sh)
+
+
+def _rows_tn(g, x, chunk=None):
     """g^T x for tall g [m, p], x [m, q]: a batched product over row chunks, then the sum
     over chunks (fp32 throughout)."""
+    chunk = chunk or _ROWS_CHUNK
     m = g.shape[0]
     c = m // chunk
     if c < 2:
@@ -67,41 +73,49 @@ def _rows_tn(g, x, chunk=2048):
 class _LSTMDense(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, h0, c0, reset, w_ih, w_hh, b_ih, b_hh):
-        T, B, _ = x.shape
+        T, B, I = x.shape
         H = w_hh.shape[1]
         whh = w_hh.detach().contiguous()
-        gx = _gx(x.detach(), w_ih.detach(), b_ih.detach(), b_hh.detach())
         h_out = torch.empty(T, B, H, device=x.device)
         c_out = torch.empty(T, B, H, device=x.device)
         gact = torch.empty(T, B, 4 * H, device=x.device)
+        # [x | h_prev | 1] per row: the operand of all three weight gradients
+        xh = torch.empty(T, B, I + H + 1, device=x.device)
         p = mm._p
-        _ok(_lib().pmlp_lstm_fwd(T, B, H, p(gx), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out), p(gact), None,
-                                 None, mm._stream()), "pmlp_lstm_fwd")
-        ctx.save_for_backward(x, h0, c0, reset, whh, h_out, c_out, gact)
+        if I <= 64:  # the input projection inside the sequence kernel, which also writes xh
+            _ok(_lib().pmlp_lstm_fwd_x(T, B, H, I, p(x), p(w_ih.detach().contiguous()), p(b_ih.detach()),
+                                       p(b_hh.detach()), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out), p(gact),
+                                       None, None, p(xh), mm._stream()), "pmlp_lstm_fwd_x")
+        else:
+            gx = _gx(x.detach(), w_ih.detach(), b_ih.detach(), b_hh.detach())
+            _ok(_lib().pmlp_lstm_fwd(T, B, H, p(gx), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out), p(gact),
+                                     None, None, mm._stream()), "pmlp_lstm_fwd")
+            xh[..., :I].copy_(x)
+            if h0 is None:
+                xh[0, :, I:I + H].zero_()
+            else:
+                xh[0, :, I:I + H].copy_(h0)
+            xh[1:, :, I:I + H].copy_(h_out[:-1])
+            if reset is not None:
+                xh[..., I:I + H].masked_fill_(reset.bool().unsqueeze(-1), 0.0)
+            xh[..., I + H].fill_(1.0)
+        ctx.save_for_backward(xh, c0, reset, whh, c_out, gact)
+        ctx.I = I
         return h_out
 
     @staticmethod
     def backward(ctx, dh_out):
-        x, h0, c0, reset, whh, h_out, c_out, gact = ctx.saved_tensors
-        T, B, I = x.shape
+        xh, c0, reset, whh, c_out, gact = ctx.saved_tensors
+        I = ctx.I
+        T, B, _ = xh.shape
         H = whh.shape[1]
-        dgx = torch.empty(T, B, 4 * H, device=x.device)
+        dgx = torch.empty(T, B, 4 * H, device=xh.device)
         p = mm._p
         _ok(_lib().pmlp_lstm_bwd(T, B, H, p(whh), p(c0), p(reset), p(c_out), p(gact), p(dh_out.contiguous()), p(dgx),
                                  mm._stream()), "pmlp_lstm_bwd")
         # all three weight gradients from ONE product dgx^T [x | h_prev | 1] over the T*B
         # rows, split over the rows (a library GEMM puts a 49k-long reduction on a few
         # output tiles: 170 us per call at H1 scale)
-        xh = torch.empty(T, B, I + H + 1, device=x.device)
-        xh[..., :I].copy_(x)
-        if h0 is None:
-            xh[0, :, I:I + H].zero_()
-        else:
-            xh[0, :, I:I + H].copy_(h0)
-        xh[1:, :, I:I + H].copy_(h_out[:-1])
-        if reset is not None:
-            xh[..., I:I + H].masked_fill_(reset.bool().unsqueeze(-1), 0.0)
-        xh[..., I + H].fill_(1.0)
         dw = _rows_tn(dgx.view(T * B, 4 * H), xh.view(T * B, I + H + 1))
         dw_ih, dw_hh, db = dw[:, :I].contiguous(), dw[:, I:I + H].contiguous(), dw[:, I + H].contiguous()
         return None, None, None, None, dw_ih, dw_hh, db, db
@@ -147,9 +161,11 @@ def lstm_step_(rnn, x, h, c):
     and overwritten by the kernel (capturable); returns h (the step's output, [1,B,H])."""
     B = x.shape[0]
     H = rnn.hidden_size
-    gx = torch.addmm(rnn.bias_ih_l0 + rnn.bias_hh_l0, x, rnn.weight_ih_l0.t())
     p = mm._p
     with torch.no_grad():
+        # (one step: the GEMM + sequence kernel beats the fused input projection, whose
+        # per-workgroup W_ih row loads dominate at T = 1: 28 vs 43 us at 8192 envs)
+        gx = torch.addmm(rnn.bias_ih_l0 + rnn.bias_hh_l0, x, rnn.weight_ih_l0.t())
         _ok(_lib().pmlp_lstm_fwd(1, B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), None, None,
                                  None, None, p(h), p(c), mm._stream()), "pmlp_lstm_fwd")
     return h

@@ -90,6 +90,7 @@ def load():
         i64 = C.c_int64
         L.pmlp_opt_parts.restype = i32
         L.pmlp_opt_prepare.argtypes = [vp, i64, f32, vp, vp, vp, vp, vp, f32, i32, vp]
+        L.pmlp_loss_bookkeeping.argtypes = [vp, vp, vp, C.c_float, i32, vp]
         L.pmlp_adam.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, vp]
         L.pmlp_adam_mirror.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, i32,
                                        C.POINTER(MirrorJob), vp]
