@@ -11,6 +11,9 @@ ROCm-specific changes that do not change the maths:
   are normalised with global statistics — so N ranks behave like one batch of
   N x num_envs envs.
 """
+import os
+import warnings
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -75,7 +78,8 @@ class PPO:
         self.use_graph = on_gpu and (not getattr(self.actor_critic, "is_recurrent", False) or
                                      self._dense_recurrent) and \
             self.optimizer.defaults.get("capturable", False) and \
-            (self.world_size == 1 or dist.get_backend() == "nccl")
+            (self.world_size == 1 or (dist.get_backend() == "nccl" and
+                                      os.environ.get("PPO_CAPTURE_COLLECTIVES", "1") != "0"))
         self._graph = None
         # fused PPO-loss kernels for the Gaussian MLP policy on a GPU (fused_loss=False:
         # the torch statement of the loss, _reference_loss)
@@ -388,10 +392,23 @@ class PPO:
         if self._fgraph is None:
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
-            self._fgraph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._fgraph, stream=side):
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph, stream=side):
+                    body()
+            except RuntimeError as e:
+                # data-parallel: the gradient all-reduce is captured with the steps; a
+                # collective library that refuses capture must not end the run (nothing
+                # inside a failed capture has executed, so the update simply runs eagerly)
+                if self.world_size == 1:
+                    raise
+                warnings.warn(f"PPO: capturing the update with its all-reduce failed ({e}); updating eagerly")
+                torch.cuda.synchronize(self.device)
+                self.use_graph = False
                 body()
+                return self._facc
             torch.cuda.current_stream(self.device).wait_stream(side)
+            self._fgraph = graph
         self._fgraph.replay()
         return self._facc
 
