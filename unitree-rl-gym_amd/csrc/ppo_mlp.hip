@@ -923,14 +923,41 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
     float d[AM];
     float surr = 0.f, vl = 0.f, kl = 0.f, dlogp = 0.f;
     if (valid) {
+        // the row's records: 16-byte loads when A is a multiple of 4 (every record then
+        // starts on 16 bytes), else one float per entry
+        float rmu[AM], ract[AM], ros[AM], rom[AM];
+        if ((A & 3) == 0) {
+#pragma unroll
+            for (int k = 0; k < AM; k += 4) {
+                if (k < A) {
+                    const float4 m4 = *(const float4*)(a.mu + (size_t)i * A + k);
+                    const float4 a4 = *(const float4*)(a.actions + si * A + k);
+                    const float4 s4 = *(const float4*)(a.old_sigma + si * A + k);
+                    const float4 o4 = *(const float4*)(a.old_mu + si * A + k);
+                    rmu[k] = m4.x; rmu[k + 1] = m4.y; rmu[k + 2] = m4.z; rmu[k + 3] = m4.w;
+                    ract[k] = a4.x; ract[k + 1] = a4.y; ract[k + 2] = a4.z; ract[k + 3] = a4.w;
+                    ros[k] = s4.x; ros[k + 1] = s4.y; ros[k + 2] = s4.z; ros[k + 3] = s4.w;
+                    rom[k] = o4.x; rom[k + 1] = o4.y; rom[k + 2] = o4.z; rom[k + 3] = o4.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < AM; ++k)
+                if (k < A) {
+                    rmu[k] = a.mu[(size_t)i * A + k];
+                    ract[k] = a.actions[si * A + k];
+                    ros[k] = a.old_sigma[si * A + k];
+                    rom[k] = a.old_mu[si * A + k];
+                }
+        }
         float logp = 0.f;
 #pragma unroll
         for (int k = 0; k < AM; ++k) {
             if (k < A) {
-                const float mu = a.mu[(size_t)i * A + k];
-                d[k] = a.actions[si * A + k] - mu;
+                const float mu = rmu[k];
+                d[k] = ract[k] - mu;
                 logp += -(d[k] * d[k]) * c_h[k] - c_lg[k] - kHalfLog2Pi;
-                const float os = a.old_sigma[si * A + k], om = a.old_mu[si * A + k] - mu;
+                const float os = ros[k], om = rom[k] - mu;
                 kl += logf(c_sg[k] / os + 1.0e-5f) + (os * os + om * om) * c_h[k] - 0.5f;
             } else {
                 d[k] = 0.f;
