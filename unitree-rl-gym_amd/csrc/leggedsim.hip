@@ -63,6 +63,10 @@ __device__ unsigned long long* g_phase_buf;
 #ifndef LGS_WAVES_PER_EU
 #define LGS_WAVES_PER_EU 4
 #endif
+// the 48-row (humanoid) variant: A stays in registers, so its LDS allows 3 waves/SIMD
+#ifndef LGS_WAVES_PER_EU_48
+#define LGS_WAVES_PER_EU_48 3
+#endif
 #define MAXB LGS_MAX_BODIES
 #define MAXD LGS_MAX_DEPTH
 #define WAVE 64
@@ -351,9 +355,7 @@ struct Smem {
             float Fj[D][6];
         } dyn;
         struct {
-            float Y[ROWS][NP];
-            // <= 32 rows: A never leaves registers (one MFMA tile, columns per lane)
-            float A[ROWS > 32 ? ROWS : 1][ROWS > 32 ? AS : 1];
+            float Y[ROWS][NP];  // (A never leaves registers: MFMA tiles, columns per lane)
         } con;
         struct {  // FK scratch: per-DOF joint rotation R(axis, q)
             float Ra[D > 0 ? D : 1][9];
@@ -1079,36 +1081,43 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         }
         STAMP(11);
     } else {
+        // up to 64 rows, one env: two 32-column blocks.  Lane l owns column l; for each row
+        // block ti the wave computes the tiles (ti, 0) and (ti, 1) -- the symmetric one
+        // too, so that every lane's column comes out of accumulators: in tile (ti, tj) lane
+        // l holds column 32 tj + (l & 31), rows (t&3)+8(t>>2)+4(l>>5), and its partner
+        // l ^ 32 the other half.  (A^T tile entries are the same products in the same order:
+        // bit-identical to the mirrored tile.)  A never goes through LDS.
         const int hi_row = nlimit > 0 ? 3 * CM + nlimit : 3 * nc;
         const int nt = (hi_row + 31) >> 5;
-        for (int ti = 0; ti < nt; ++ti) {
-            for (int tj = 0; tj <= ti; ++tj) {
-                const int ra = 32 * ti + li, rb = 32 * tj + li;
-                floatx16 acc;
+        const bool up = threadIdx.x >= 32;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+        for (int r = 0; r < ROWS; ++r) acol[r] = 0.f;
 #pragma unroll
-                for (int st = 0; st < (n + 1) / 2; ++st) {
-                    const int kk = 2 * st + lk;
-                    const float a = (ra < ROWS && kk < n) ? s.u.con.Y[ra][kk] : 0.f;
-                    const float b = (rb < ROWS && kk < n) ? s.u.con.Y[rb][kk] : 0.f;
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-                }
+        for (int ti = 0; ti < (ROWS + 31) / 32; ++ti) {
+            if (ti >= nt) break;  // (uniform)
+            floatx16 acc0, acc1;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int R_ = 32 * ti + (t & 3) + 8 * (t >> 2) + 4 * lk;
-                    const int C_ = 32 * tj + li;
-                    if (R_ < ROWS && C_ < ROWS) {
-                        s.u.con.A[R_][C_] = acc[t];
-                        if (ti != tj) s.u.con.A[C_][R_] = acc[t];
-                    }
-                }
+            for (int t = 0; t < 16; ++t) { acc0[t] = 0.f; acc1[t] = 0.f; }
+            const int ra = 32 * ti + li;
+#pragma unroll
+            for (int st = 0; st < (n + 1) / 2; ++st) {
+                const int kk = 2 * st + lk;
+                const float a = (ra < ROWS && kk < n) ? s.u.con.Y[ra][kk] : 0.f;
+                const float b0 = (li < ROWS && kk < n) ? s.u.con.Y[li][kk] : 0.f;
+                const float b1 = (32 + li < ROWS && kk < n) ? s.u.con.Y[32 + li][kk] : 0.f;
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int r0 = 32 * ti + (t & 3) + 8 * (t >> 2);
+                const float o0 = __shfl_xor(acc0[t], 32), o1 = __shfl_xor(acc1[t], 32);
+                const float own = up ? acc1[t] : acc0[t], other = up ? o1 : o0;
+                if (r0 < ROWS) acol[r0] = up ? other : own;
+                if (r0 + 4 < ROWS) acol[r0 + 4] = up ? own : other;
             }
         }
-        __syncthreads();
         STAMP(11);
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) acol[r] = (lane < ROWS) ? s.u.con.A[r][lane < ROWS ? lane : 0] : 0.f;
     }
     float lam = 0.f;  // one env per wave: lane r holds lambda_r (one VGPR; broadcast when read)
     // two envs per wave: every lane holds every lambda of its env (the values are uniform
@@ -1850,8 +1859,10 @@ enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MO
 
 // EPW envs per workgroup (one wave): env EPW * xcd_env(block) + hh; with EPW = 2 the grid
 // has N / 2 workgroups (N even) and every wave carries two envs.
-template <int D, int B, int ROWS, int CH, int EPW>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(EPW == 2 ? 2 : (ROWS <= 32 ? LGS_WAVES_PER_EU : 2)))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
+// WPE > 0: the waves/SIMD the build targets (the 48-row variant at <= 4096 envs takes 4:
+// one round of waves, worth its spills; 8192 envs run 3, fewer spills)
+template <int D, int B, int ROWS, int CH, int EPW, int WPE = 0>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (EPW == 2 ? 2 : (ROWS <= 32 ? LGS_WAVES_PER_EU : LGS_WAVES_PER_EU_48))))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step, int mode) {
     __shared__ Smem<D, B, ROWS> sm[EPW];
     __shared__ ModelCache<D, B> mc;
@@ -2022,15 +2033,30 @@ static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 
             hipLaunchKernelGGL((KERNEL<D_, B_, R_, 0, EPW_>), dim3((sim)->N / EPW_), dim3(WAVE), 0,        \
                                (sim)->stream, __VA_ARGS__);                                               \
     } while (0)
+// the 48-row variants: 4 waves/SIMD when all envs fit one round of them, else the default
+#define LGS_LAUNCH_48W(sim, KERNEL, D_, B_, WPE_, ...)                                                    \
+    do {                                                                                                  \
+        if ((sim)->chain == variant_chain(pick(sim)))                                                     \
+            hipLaunchKernelGGL((KERNEL<D_, B_, 48, (D_ == 10 ? 5 : (B_ == 13 ? 6 : 3)), 1, WPE_>),        \
+                               dim3((sim)->N), dim3(WAVE), 0, (sim)->stream, __VA_ARGS__);                \
+        else                                                                                              \
+            hipLaunchKernelGGL((KERNEL<D_, B_, 48, 0, 1, WPE_>), dim3((sim)->N), dim3(WAVE), 0,           \
+                               (sim)->stream, __VA_ARGS__);                                               \
+    } while (0)
+#define LGS_LAUNCH_48(sim, KERNEL, D_, B_, ...)                                                           \
+    do {                                                                                                  \
+        if ((sim)->N <= 4 * 1024) LGS_LAUNCH_48W(sim, KERNEL, D_, B_, 4, __VA_ARGS__);                    \
+        else LGS_LAUNCH_48W(sim, KERNEL, D_, B_, 0, __VA_ARGS__);                                         \
+    } while (0)
 #define LGS_DISPATCH_STEP(sim, KERNEL, ...)                                                               \
     switch (pick(sim)) {                                                                                  \
     case V_12_19:                                                                                         \
         if ((sim)->epw == 2) LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 2, __VA_ARGS__);                     \
         else LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 1, __VA_ARGS__);                                     \
         break;                                                                                            \
-    case V_12_13: LGS_LAUNCH_EPW(sim, KERNEL, 12, 13, 48, 1, __VA_ARGS__); break;                         \
-    case V_10_11: LGS_LAUNCH_EPW(sim, KERNEL, 10, 11, 48, 1, __VA_ARGS__); break;                         \
-    case V_12_19_48: LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 48, 1, __VA_ARGS__); break;                      \
+    case V_12_13: LGS_LAUNCH_48(sim, KERNEL, 12, 13, __VA_ARGS__); break;                                 \
+    case V_10_11: LGS_LAUNCH_48(sim, KERNEL, 10, 11, __VA_ARGS__); break;                                 \
+    case V_12_19_48: LGS_LAUNCH_48(sim, KERNEL, 12, 19, __VA_ARGS__); break;                              \
     default: return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");                                 \
     }
 #define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
