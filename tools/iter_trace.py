@@ -18,8 +18,13 @@ prev_end = max(i for i in range(first) if rows[i][2].startswith("void k_step")) 
 # the iteration starts after the previous k_step's update: take the first kernel after the previous
 # iteration's update, approximated as the first of the T act kernels before k_step #first
 start = first
-while start > prev_end + 1 and not rows[start - 1][2].startswith("void k_step") and rows[first][0] - rows[start - 1][0] < 2e6:
-    start -= 1
+adam = [i for i in range(prev_end, first) if rows[i][2].startswith("k_adam")]
+if adam:  # the collection starts right after the previous update's last optimizer step
+    start = adam[-1] + 1
+else:
+    while start > prev_end + 1 and not rows[start - 1][2].startswith("void k_step") and \
+            rows[first][0] - rows[start - 1][0] < 2e6:
+        start -= 1
 upd0 = steps[-1] + 1
 end = len(rows)
 
