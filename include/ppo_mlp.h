@@ -271,6 +271,11 @@ PMLP_API int pmlp_lstm_fwd_x(int32_t T, int32_t B, int32_t H, int32_t I, const f
                              const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
                              const uint8_t* reset, float* h_out, float* c_out, float* gact, float* h_last,
                              float* c_last, float* xh, void* stream);
+/* One rollout step in place (T = 1): h, c [B,H] are read and overwritten; h_save / c_save
+ * (optional) receive the state the step started from (the rollout storage's saved hidden
+ * state, RolloutStorage._save_hidden_states). */
+PMLP_API int pmlp_lstm_step(int32_t B, int32_t H, const float* gx, const float* whh, float* h, float* c,
+                            float* h_save, float* c_save, void* stream);
 PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0, const uint8_t* reset,
                            const float* c_out, const float* gact, const float* dh_out, float* dgx, void* stream);
 

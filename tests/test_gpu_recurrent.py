@@ -229,3 +229,32 @@ def test_recurrent_rollout_graph_matches_eager(tmp_path):
         assert torch.equal(e[k], g[k]), k
     for a, b in zip(e["params"], g["params"]):
         assert torch.equal(a, b)
+
+
+def test_recurrent_rollout_saves_the_pre_step_state_from_the_kernel():
+    """RecurrentRollout: the storage slot of step t holds the memory state the step started
+    from (written by the LSTM step kernel itself), as RolloutStorage._save_hidden_states
+    would copy it; step 0 of the first rollout starts from zeros."""
+    torch.manual_seed(3)
+    N, T, O, P, A, H = 256, 4, 47, 50, 12, 64
+    ac = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                              rnn_hidden_size=H, rnn_num_layers=1).cuda()
+    alg = PPO(ac, device="cuda")
+    alg.init_storage(N, T, [O], [P], [A])
+    assert alg._rollout is not None
+    st = alg.storage
+    for t in range(T):
+        obs, cobs = torch.randn(N, O, device="cuda"), torch.randn(N, P, device="cuda")
+        prev = [None if s is None else s.clone() for s in (ac.memory_a.hidden_states or (None, None))] + \
+               [None if s is None else s.clone() for s in (ac.memory_c.hidden_states or (None, None))]
+        with torch.inference_mode():
+            alg.act(obs, cobs)
+            alg.process_env_step(torch.randn(N, device="cuda"), torch.rand(N, device="cuda") < 0.2,
+                                 {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+        got = [st.saved_hidden_states_a[0][t], st.saved_hidden_states_a[1][t], st.saved_hidden_states_c[0][t],
+               st.saved_hidden_states_c[1][t]]
+        for g, p in zip(got, prev):
+            if p is None:
+                assert bool((g == 0).all())
+            else:
+                assert torch.equal(g, p)

@@ -58,6 +58,8 @@ struct FwdArgs {
     float* h_last;
     float* c_last;
     float* xh;
+    float* h_save;  // (optional) copies of h0 / c0 as read: the rollout storage's saved state
+    float* c_save;
 };
 
 template <int H, int EB, int IP>
@@ -89,8 +91,12 @@ __global__ __launch_bounds__(4 * H) void k_lstm_fwd(FwdArgs a) {
 #pragma unroll
     for (int p = 0; p < PE; ++p) {
         const int i = j + p * G, e = i / H, k = i % H, ge = e0 + e;
-        hs[e][k] = (ge < B && a.h0) ? a.h0[(size_t)ge * H + k] : 0.f;
-        cs[e][k] = (ge < B && a.c0) ? a.c0[(size_t)ge * H + k] : 0.f;
+        const float hv = (ge < B && a.h0) ? a.h0[(size_t)ge * H + k] : 0.f;
+        const float cv = (ge < B && a.c0) ? a.c0[(size_t)ge * H + k] : 0.f;
+        hs[e][k] = hv;
+        cs[e][k] = cv;
+        if (ge < B && a.h_save) a.h_save[(size_t)ge * H + k] = hv;
+        if (ge < B && a.c_save) a.c_save[(size_t)ge * H + k] = cv;
     }
     const int kind = j / H;  // 0 i, 1 f, 2 g (tanh), 3 o
     float gxn[IP > 0 ? 1 : EB];
@@ -404,7 +410,16 @@ PMLP_API int pmlp_lstm_fwd(int32_t T, int32_t B, int32_t H, const float* gx, con
     if (T <= 0 || B <= 0 || !gx || !whh) return fail("pmlp_lstm_fwd: empty sequence or null gx/whh");
     if (((uintptr_t)whh & 15u) != 0) return fail("pmlp_lstm_fwd: whh must be 16-byte aligned");
     FwdArgs a{T, B, 0, gx, nullptr, nullptr, nullptr, nullptr, whh, h0, c0, reset, h_out, c_out, gact,
-              h_last, c_last, nullptr};
+              h_last, c_last, nullptr, nullptr, nullptr};
+    return fwd_dispatch(a, H, (hipStream_t)stream);
+}
+
+PMLP_API int pmlp_lstm_step(int32_t B, int32_t H, const float* gx, const float* whh, float* h, float* c,
+                            float* h_save, float* c_save, void* stream) {
+    if (B <= 0 || !gx || !whh || !h || !c) return fail("pmlp_lstm_step: empty batch or null gx/whh/h/c");
+    if (((uintptr_t)whh & 15u) != 0) return fail("pmlp_lstm_step: whh must be 16-byte aligned");
+    FwdArgs a{1, B, 0, gx, nullptr, nullptr, nullptr, nullptr, whh, h, c, nullptr, nullptr, nullptr, nullptr,
+              h, c, nullptr, h_save, c_save};
     return fwd_dispatch(a, H, (hipStream_t)stream);
 }
 
@@ -415,7 +430,8 @@ PMLP_API int pmlp_lstm_fwd_x(int32_t T, int32_t B, int32_t H, int32_t I, const f
     if (T <= 0 || B <= 0 || !x || !wih || !whh) return fail("pmlp_lstm_fwd_x: empty sequence or null x/wih/whh");
     if (I <= 0 || I > 64) return fail("pmlp_lstm_fwd_x: input size must be 1..64");
     if (((uintptr_t)whh & 15u) != 0) return fail("pmlp_lstm_fwd_x: whh must be 16-byte aligned");
-    FwdArgs a{T, B, I, nullptr, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, xh};
+    FwdArgs a{T, B, I, nullptr, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, h_last, c_last, xh,
+              nullptr, nullptr};
     return fwd_dispatch(a, H, (hipStream_t)stream);
 }
 

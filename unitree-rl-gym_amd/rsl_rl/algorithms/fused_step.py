@@ -426,9 +426,19 @@ class RecurrentRollout:
 
     def act(self, obs, cobs, storage, t):
         ac = self.alg.actor_critic
-        storage._save_hidden_states(ac.get_hidden_states())  # the state BEFORE this step
-        mu = ac.actor(ac.memory_a(obs).squeeze(0)).contiguous()
-        value = ac.critic(ac.memory_c(cobs).squeeze(0)).contiguous()
+        ma, mc = ac.memory_a, ac.memory_c
+        H = ma.rnn.hidden_size
+        if isinstance(ma.rnn, torch.nn.LSTM) and isinstance(mc.rnn, torch.nn.LSTM):
+            # the state BEFORE this step goes to the storage slot from inside the step kernel
+            shape = (1, self.N, H)
+            sa, sc = storage.hidden_state_slots(t, [shape, shape], [(1, self.N, mc.rnn.hidden_size)] * 2)
+            ha = ma.step_(obs, save=(sa[0], sa[1]))
+            hc = mc.step_(cobs, save=(sc[0], sc[1]))
+        else:
+            storage._save_hidden_states(ac.get_hidden_states())
+            ha, hc = ma(obs), mc(cobs)
+        mu = ac.actor(ha.squeeze(0)).contiguous()
+        value = ac.critic(hc.squeeze(0)).contiguous()
         A = self.actions.shape[1]
         priv = storage.privileged_observations
         P = mm._p

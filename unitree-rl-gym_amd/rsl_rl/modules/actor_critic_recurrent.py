@@ -91,16 +91,21 @@ class Memory(torch.nn.Module):
             out, _ = self.rnn(input, hidden_states)
             out = unpad_trajectories(out, masks)
         elif lstm_seq.usable(self.rnn, input):  # rollout mode on the kernel: state updated in place
-            B, H = input.shape[0], self.rnn.hidden_size
-            hs = self.hidden_states
-            if hs is None or not isinstance(hs, tuple) or hs[0].shape != (1, B, H) or hs[0].device != input.device:
-                with torch.inference_mode(False):
-                    self.hidden_states = (torch.zeros(1, B, H, device=input.device),
-                                          torch.zeros(1, B, H, device=input.device))
-            out = lstm_seq.lstm_step_(self.rnn, input, self.hidden_states[0], self.hidden_states[1])
+            out = self.step_(input)
         else:  # rollout mode: one step, keep the state
             out, self.hidden_states = self.rnn(input.unsqueeze(0), self.hidden_states)
         return out
+
+    def step_(self, input, save=None):
+        """Rollout step on the LSTM kernel, the state buffers updated in place (created as
+        zeros on first use); save = (h_dst, c_dst) receives the state the step starts from."""
+        B, H = input.shape[0], self.rnn.hidden_size
+        hs = self.hidden_states
+        if hs is None or not isinstance(hs, tuple) or hs[0].shape != (1, B, H) or hs[0].device != input.device:
+            with torch.inference_mode(False):
+                self.hidden_states = (torch.zeros(1, B, H, device=input.device),
+                                      torch.zeros(1, B, H, device=input.device))
+        return lstm_seq.lstm_step_(self.rnn, input, self.hidden_states[0], self.hidden_states[1], save=save)
 
     def dense(self, input, hidden_states, reset):
         """[T,B,I] -> [T,B,H]: all T steps from hidden_states (the state saved at t = 0),

@@ -33,6 +33,7 @@ def _lib():
         L.pmlp_lstm_fwd.argtypes = [i32, i32, i32] + [vp] * 10 + [vp]
         L.pmlp_lstm_bwd.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
         L.pmlp_lstm_fwd_x.argtypes = [i32, i32, i32, i32] + [vp] * 14 + [vp]
+        L.pmlp_lstm_step.argtypes = [i32, i32] + [vp] * 6 + [vp]
         _bound = True
     return L
 
@@ -156,9 +157,11 @@ def lstm_dense_reference(rnn, x, h0, c0, reset):
     return torch.stack(out)
 
 
-def lstm_step_(rnn, x, h, c):
+def lstm_step_(rnn, x, h, c, save=None):
     """One rollout step in place: h, c [1,B,H] static buffers (the policy's memory) are read
-    and overwritten by the kernel (capturable); returns h (the step's output, [1,B,H])."""
+    and overwritten by the kernel (capturable); returns h (the step's output, [1,B,H]).
+    save = (h_dst, c_dst): the state the step starts from is also written there (the rollout
+    storage's saved hidden state) by the same kernel."""
     B = x.shape[0]
     H = rnn.hidden_size
     p = mm._p
@@ -166,6 +169,7 @@ def lstm_step_(rnn, x, h, c):
         # (one step: the GEMM + sequence kernel beats the fused input projection, whose
         # per-workgroup W_ih row loads dominate at T = 1: 28 vs 43 us at 8192 envs)
         gx = torch.addmm(rnn.bias_ih_l0 + rnn.bias_hh_l0, x, rnn.weight_ih_l0.t())
-        _ok(_lib().pmlp_lstm_fwd(1, B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), None, None,
-                                 None, None, p(h), p(c), mm._stream()), "pmlp_lstm_fwd")
+        hs, cs = (None, None) if save is None else save
+        _ok(_lib().pmlp_lstm_step(B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), p(hs), p(cs),
+                                  mm._stream()), "pmlp_lstm_step")
     return h

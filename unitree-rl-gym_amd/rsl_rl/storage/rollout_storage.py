@@ -80,6 +80,16 @@ class RolloutStorage:
             self.saved_hidden_states_a[i][self.step].copy_(hid_a[i])
             self.saved_hidden_states_c[i][self.step].copy_(hid_c[i])
 
+    def hidden_state_slots(self, t, shapes_a, shapes_c):
+        """The storage slots of step t for the saved (h, c) of both memories (the buffers
+        are created as zeros on first use, as _save_hidden_states creates them)."""
+        if self.saved_hidden_states_a is None:
+            with torch.inference_mode(False):
+                T = self.observations.shape[0]
+                self.saved_hidden_states_a = [torch.zeros(T, *s, device=self.device) for s in shapes_a]
+                self.saved_hidden_states_c = [torch.zeros(T, *s, device=self.device) for s in shapes_c]
+        return [h[t] for h in self.saved_hidden_states_a], [h[t] for h in self.saved_hidden_states_c]
+
     def clear(self):
         self.step = 0
 
