@@ -87,3 +87,18 @@ def test_adam_mirror_checks_its_jobs(lib):
     for jobs, n_jobs in (((mm.MirrorJob * 1)(over), 1), ((mm.MirrorJob * 9)(*([ok] * 9)), 9)):
         rc = lib.pmlp_adam_mirror(16, 16, 16, 16, 16, 1.0, 16, 16, 16, 1.0, 0.9, 0.999, 1e-8, n_jobs, jobs, None)
         assert rc != 0 and b"pmlp_adam_mirror" in lib.pmlp_last_error()
+
+
+def test_recurrent_and_bookkeeping_entries_refuse_bad_arguments(lib):
+    """The LSTM entries and the loss bookkeeping check their arguments before any launch."""
+    from rsl_rl.modules import lstm_seq
+    L = lstm_seq._lib()
+    assert L.pmlp_lstm_step(0, 64, 16, 16, 16, 16, None, None, None) != 0  # empty batch
+    assert L.pmlp_lstm_step(8, 64, 16, 8, 16, 16, None, None, None) != 0  # whh not 16-byte aligned
+    assert b"pmlp_lstm_step" in L.pmlp_lstm_last_error()
+    assert L.pmlp_lstm_fwd_x(4, 8, 64, 65, 16, 16, None, None, 16, None, None, None, None, None, None, None, None,
+                             None, None) != 0  # input wider than 64
+    assert b"input size" in L.pmlp_lstm_last_error()
+    lib.pmlp_loss_bookkeeping.restype = C.c_int
+    assert lib.pmlp_loss_bookkeeping(None, None, None, C.c_float(0.01), 1, None) != 0
+    assert b"pmlp_loss_bookkeeping" in lib.pmlp_last_error()
