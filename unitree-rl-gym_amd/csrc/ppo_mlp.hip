@@ -47,6 +47,14 @@ static int fail(int code, const std::string& m) {
     } while (0)
 
 // LDS stages of the GEMM main loop (2: one barrier per k-tile)
+// diagnostic builds (never shipped): PMLP_DIAG_NOSTORE skips the GEMM's global result
+// stores behind a condition the compiler cannot fold (the work is still done)
+#ifdef PMLP_DIAG_NOSTORE
+#define PMLP_STORE_OK (g.K < 0)
+#else
+#define PMLP_STORE_OK true
+#endif
+
 #ifndef PMLP_NBUF
 #define PMLP_NBUF 1
 #endif
@@ -175,6 +183,9 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 
     uint4 ra[PF][AL], rb[PF][BL];
     auto gload = [&](int p, int k0) {
+#ifdef PMLP_DIAG_NOLOAD
+        if (k0 != kb) return;  // diagnostic build: operands of the first k-tile only
+#endif
         if constexpr (TNL) {
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
@@ -428,7 +439,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const int row = rbase + (t & 3) + 8 * (t >> 2);
-                    if (row < g.M) slab[(size_t)row * g.ldcf + col] = acc[i][j][t];
+                    if (row < g.M && PMLP_STORE_OK) slab[(size_t)row * g.ldcf + col] = acc[i][j][t];
                 }
             } else if (EPI == PMLP_EPI_FWD_OUT) {
                 const float b = g.bias ? g.bias[col] : 0.f;
@@ -475,7 +486,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
             for (int c = tid; c < RCH; c += NT) {
                 const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
                 const int row = m0 + lr, col = n0 + lc;
-                if (row >= g.M || col >= g.N) continue;
+                if (row >= g.M || col >= g.N || !PMLP_STORE_OK) continue;
                 const bf16* src = smem + lr * CS + lc;
                 if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
                     *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
@@ -507,7 +518,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
             for (int c = tid; c < RCH; c += NT) {
                 const int lc = c / (BM / 8), lr = (c % (BM / 8)) * 8;
                 const int col = n0 + lc, row = m0 + lr;
-                if (col >= g.N || row >= g.M) continue;
+                if (col >= g.N || row >= g.M || !PMLP_STORE_OK) continue;
                 const bf16* src = smem + lc * TS + lr;
                 if (row + 8 <= g.M && (g.ldct % 8) == 0) {
                     *(uint4*)(g.ct + (size_t)col * g.ldct + row) = *(const uint4*)src;
