@@ -328,3 +328,64 @@ def test_fused_update_tn_is_bitwise_transposed_copies(monkeypatch):
         assert l0 == l1
         for a, b in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,A,Ap", [(24576, 12, 16), (1000 + 37, 12, 16), (517, 8, 8), (2048, 10, 16)])
+def test_loss_step_kernel_matches_fp32_autograd(M, A, Ap):
+    """pmlp_ppo_loss_step (the quad-per-row kernel for A % 4 == 0, the one-lane-per-row
+    kernel for A = 10) against rsl_rl v1.0.2's loss statement in fp32 autograd, rollout
+    inputs gathered through a mini-batch index: the logged statistics, the std gradient
+    (with the entropy term) and the bf16 output gradients of mu and the value."""
+    g = torch.Generator(device="cuda").manual_seed(M + A)
+    dev, R, clip, vcoef, ecoef = "cuda", M + 311, 0.2, 1.0, 0.01
+    rn = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    mu = rn(M, A)
+    std = 0.5 + torch.rand(A, device=dev, generator=g)
+    value = rn(M, 1)
+    act, old_mu = rn(R, A), rn(R, A)
+    old_sigma = 0.5 + torch.rand(R, A, device=dev, generator=g)
+    adv, ret = rn(R, 1), rn(R, 1)
+    target = ret + 0.3 * rn(R, 1)
+    rows = torch.randperm(R, device=dev, generator=g)[:M].contiguous()
+    # old log-probs near the current ones: ratios spread across the clip range
+    old_logp = rn(R, 1)
+    old_logp[rows] = (torch.distributions.Normal(mu, std).log_prob(act[rows]).sum(-1, keepdim=True)
+                      + 0.15 * rn(M, 1))
+
+    # torch statement (rsl_rl v1.0.2 PPO.update, clipped value loss)
+    tm, ts, tv = (t.clone().requires_grad_(True) for t in (mu, std, value))
+    ga = lambda t: t[rows]  # noqa: E731
+    dist = torch.distributions.Normal(tm, tm * 0 + ts)
+    logp = dist.log_prob(ga(act)).sum(-1)
+    ratio = torch.exp(logp - ga(old_logp).squeeze(-1))
+    a_ = ga(adv).squeeze(-1)
+    surr = torch.max(-a_ * ratio, -a_ * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+    tgt, rt = ga(target), ga(ret)
+    vc = tgt + (tv - tgt).clamp(-clip, clip)
+    vl = torch.max((tv - rt).pow(2), (vc - rt).pow(2)).mean()
+    ent = dist.entropy().sum(-1).mean()
+    (surr + vcoef * vl - ecoef * ent).backward()
+    with torch.no_grad():
+        os_, om = ga(old_sigma), ga(old_mu)
+        kl = torch.sum(torch.log(ts / os_ + 1e-5) + (os_ ** 2 + (om - tm) ** 2) / (2 * ts ** 2) - 0.5, -1).mean()
+
+    L = mfma_mlp.load()
+    P = mfma_mlp._p
+    Vp = 8
+    partial = torch.empty(L.pmlp_ppo_loss_step_parts(M, A), device=dev)
+    stats, dstd = torch.empty(4, device=dev), torch.empty(A, device=dev)
+    dmu = torch.full((M, Ap), float("nan"), dtype=torch.bfloat16, device=dev)
+    dv = torch.full((M, Vp), float("nan"), dtype=torch.bfloat16, device=dev)
+    mfma_mlp._ok(L.pmlp_ppo_loss_step(P(mu), P(std), P(value), P(act), P(old_logp), P(old_mu), P(old_sigma), P(adv),
+                                      P(ret), P(target), P(rows), M, A, clip, 1, vcoef, ecoef, P(partial), P(stats),
+                                      P(dstd), P(dmu), None, Ap, P(dv), None, Vp, mfma_mlp._stream()),
+                 "pmlp_ppo_loss_step")
+    torch.cuda.synchronize()
+    want = torch.stack([surr.detach(), vl.detach(), kl, ent.detach()])
+    torch.testing.assert_close(stats, want, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(dstd, ts.grad, rtol=1e-4, atol=1e-7)
+    # bf16 outputs: one rounding of the fp32 gradient; padding columns exactly zero
+    torch.testing.assert_close(dmu[:, :A].float(), tm.grad.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-9)
+    assert torch.count_nonzero(dmu[:, A:].float()) == 0
+    torch.testing.assert_close(dv[:, :1].float(), tv.grad.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-9)
+    assert torch.count_nonzero(dv[:, 1:].float()) == 0

@@ -1042,6 +1042,129 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
     }
 }
 
+// The same step with four lanes per row (lane q of a quad owns action entries 4q..4q+3: one
+// 16-byte load per record instead of A/4 serial ones) in 256-thread blocks of 64 rows, so
+// the 24,576-row mini-batch is 1,536 waves instead of 384 and each lane has a quarter of
+// the gathers in flight.  Quad sums combine a row's logp / KL; the block's partials are
+// summed per wave (rows in xor order), then over the 4 waves in order (deterministic; the
+// same partials layout as k_ppo_loss_step_reg: one record of 3 + A per 64 rows).
+// Needs A % 4 == 0, A <= 16, Ap <= 16 and Ap % 4 == 0.
+__global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut o) {
+    __shared__ float c_h[16], c_i2[16], c_i3[16], c_i1[16], c_lg[16], c_sg[16];
+    __shared__ float wpart[4][3 + 16];
+    const int A = a.A, W = 3 + A, tid = threadIdx.x, q = tid & 3, k0 = 4 * q;
+    if (tid < A) {
+        const float sg = a.stdv[tid];
+        c_sg[tid] = sg;
+        c_h[tid] = 1.f / (2.f * sg * sg);
+        c_i2[tid] = 1.f / (sg * sg);
+        c_i3[tid] = 1.f / (sg * sg * sg);
+        c_i1[tid] = 1.f / sg;
+        c_lg[tid] = logf(sg);
+    }
+    __syncthreads();
+    const int i = blockIdx.x * 64 + (tid >> 2);
+    const bool valid = i < a.M;
+    const bool own = k0 < A;  // quad-uniform per lane, same for every row
+    const size_t si = valid ? a.src(i) : 0;
+    float d[4] = {0.f, 0.f, 0.f, 0.f};
+    float surr = 0.f, vl = 0.f, kl = 0.f, dlogp = 0.f;
+    if (valid) {
+        float lp = 0.f, kp = 0.f;
+        if (own) {
+            const float4 m4 = *(const float4*)(a.mu + (size_t)i * A + k0);
+            const float4 a4 = *(const float4*)(a.actions + si * A + k0);
+            const float4 s4 = *(const float4*)(a.old_sigma + si * A + k0);
+            const float4 o4 = *(const float4*)(a.old_mu + si * A + k0);
+            const float rmu[4] = {m4.x, m4.y, m4.z, m4.w}, ract[4] = {a4.x, a4.y, a4.z, a4.w};
+            const float ros[4] = {s4.x, s4.y, s4.z, s4.w}, rom[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u;
+                d[u] = ract[u] - rmu[u];
+                lp += -(d[u] * d[u]) * c_h[k] - c_lg[k] - kHalfLog2Pi;
+                const float os = ros[u], om = rom[u] - rmu[u];
+                kp += logf(c_sg[k] / os + 1.0e-5f) + (os * os + om * om) * c_h[k] - 0.5f;
+            }
+        }
+        lp += __shfl_xor(lp, 1);
+        lp += __shfl_xor(lp, 2);
+        kp += __shfl_xor(kp, 1);
+        kp += __shfl_xor(kp, 2);
+        const float ratio = expf(lp - a.old_logp[si]);
+        const float adv = a.adv[si];
+        const float lo = 1.f - a.clip, hi = 1.f + a.clip;
+        const float s1 = -adv * ratio, s2 = -adv * fminf(fmaxf(ratio, lo), hi);
+        float w1, w2;
+        max_weights(s1, s2, w1, w2);
+        const float dclamp = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        dlogp = (1.f / (float)a.M) * (-adv) * (w1 + w2 * dclamp) * ratio;
+        if (k0 < o.Ap) {
+            bf16x4 g;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = (bf16)(own ? dlogp * d[u] * c_i2[k0 + u] : 0.f);
+            *(bf16x4*)(o.dmu_b + (size_t)i * o.Ap + k0) = g;
+            if (o.dmu_t) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o.dmu_t[(size_t)(k0 + u) * a.M + i] = g[u];
+            }
+        }
+        const float v = a.value[i], r = a.ret[si];
+        float dv;
+        const float gvc = a.vcoef / (float)a.M;
+        float vq;
+        if (a.clipped_value) {
+            const float t = a.target[si];
+            const float vc = t + fminf(fmaxf(v - t, -a.clip), a.clip);
+            vq = fmaxf((v - r) * (v - r), (vc - r) * (vc - r));
+            float u1, u2;
+            max_weights((v - r) * (v - r), (vc - r) * (vc - r), u1, u2);
+            const float dcv = (v - t >= -a.clip && v - t <= a.clip) ? 1.f : 0.f;
+            dv = gvc * (u1 * 2.f * (v - r) + u2 * 2.f * (vc - r) * dcv);
+        } else {
+            vq = (r - v) * (r - v);
+            dv = gvc * 2.f * (v - r);
+        }
+        for (int k = q; k < o.Vp; k += 4) {
+            o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
+            if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+        }
+        if (q == 0) {  // the row's scalars counted once
+            surr = fmaxf(s1, s2);
+            vl = vq;
+            kl = kp;
+        }
+    }
+    // per wave: sums over its 16 rows (xor 4..32 keeps the quad position), then the
+    // scalars (nonzero on q == 0 only) over the quad
+    auto rsum = [](float x) {
+#pragma unroll
+        for (int off = 4; off < 64; off <<= 1) x += __shfl_xor(x, off);
+        return x;
+    };
+    surr = rsum(surr);
+    vl = rsum(vl);
+    kl = rsum(kl);
+    float c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u;
+        c[u] = rsum(valid && own ? dlogp * (d[u] * d[u] * c_i3[k] - c_i1[k]) : 0.f);
+    }
+    const int w = tid >> 6, lane = tid & 63;
+    if (lane == 0) {
+        wpart[w][0] = surr;
+        wpart[w][1] = vl;
+        wpart[w][2] = kl;
+    }
+    if (lane < 4 && own) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wpart[w][3 + k0 + u] = c[u];
+    }
+    __syncthreads();
+    if (tid < W) o.partial[(size_t)blockIdx.x * W + tid] = (wpart[0][tid] + wpart[1][tid]) + (wpart[2][tid] + wpart[3][tid]);
+}
+
 // stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term.
 // One wave per reduced quantity q (block q): the per-wave partials of k_ppo_loss_step summed
 // in a fixed order (deterministic), all quantities at once.
@@ -1157,7 +1280,9 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
         for (int j = 0; j < mj.n; ++j) {  // the bf16 GEMM operand copy of a weight
             const int64_t o = i - mj.off[j];
             if (o >= 0 && o < (int64_t)mj.rows[j] * mj.cols[j]) {
-                const int r = (int)(o / mj.cols[j]), c = (int)(o % mj.cols[j]);
+                // a weight has < 2^31 entries: 32-bit division (the 64-bit one is a long
+                // VALU sequence per element)
+                const int oi = (int)o, r = oi / mj.cols[j], c = oi - r * mj.cols[j];
                 mj.dst[j][(size_t)r * mj.ld[j] + c] = (bf16)pi;
             }
         }
@@ -2013,7 +2138,13 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
     const int nb = (M + 63) / 64;
-    if (A <= 16 && Ap % 8 == 0)
+    static const bool quad = [] {
+        const char* e = getenv("PMLP_LOSS_QUAD");  // 0: the one-lane-per-row kernel (A/B)
+        return !(e && e[0] == '0');
+    }();
+    if (quad && A % 4 == 0 && A <= 16 && Ap <= 16 && Ap % 4 == 0)
+        hipLaunchKernelGGL(k_ppo_loss_step_q, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, o);
+    else if (A <= 16 && Ap % 8 == 0)
         hipLaunchKernelGGL(k_ppo_loss_step_reg<16>, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
     else
         hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
