@@ -2003,7 +2003,14 @@ PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, f
             return fail(-1, "pmlp_adam_mirror: bad mirror job " + std::to_string(j));
         mj.off[j] = J.offset; mj.rows[j] = J.rows; mj.cols[j] = J.cols; mj.ld[j] = J.ld; mj.dst[j] = (bf16*)J.dst;
     }
-    const int blocks = (int)std::min<int64_t>(1024, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
+    // grid cap 1024 blocks: for the Go2 parameters (1,486 blocks at one element per thread)
+    // uncapped / 1024 / 512 / 256 measured 9.2-9.5 / 7.5-8.1 / 8.5-10.0 / 12.1-12.7 us
+    // (profiles/round2/update/adam_grid_ab.txt); PMLP_ADAM_BLOCKS overrides it (A/B knob)
+    static const int cap = [] {
+        const char* v = getenv("PMLP_ADAM_BLOCKS");
+        return v ? std::max(1, atoi(v)) : 1024;
+    }();
+    const int blocks = (int)std::min<int64_t>(cap, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
     hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
                        exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps, mj);
     PMLP_CHECK_LAUNCH("pmlp_adam_mirror");
