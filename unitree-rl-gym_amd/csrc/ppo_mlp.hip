@@ -586,35 +586,53 @@ struct RedJob {
     float* bias_out;
     int64_t stride, n;
     int nslabs, cols_in, cols_out;
+    int groups;  // slab groups per element quad (threads summing disjoint slab subsets)
 };
 struct RedJobs {
     RedJob j[PMLP_MAX_JOBS];
     int start[PMLP_MAX_JOBS + 1];  // first block of each job (1-D grid)
     int njobs;
 };
-// out = sum over slabs (slab order, per element: deterministic).  With bias_out: the slab
+// out = sum over slabs (fixed order per element: deterministic).  With bias_out: the slab
 // is [rows, cols_in]; columns < cols_out go to out[rows, cols_out] and column cols_out
 // (the ones-row product) to bias_out[rows].  Four consecutive elements per thread (16-byte
 // loads), the slab loop unrolled so the loads of several slabs are in flight together.
+// A job with many slabs (the small layers' weight gradients: 64-96 slabs) splits them over
+// G = J.groups threads per element quad (slabs g, g+G, ...), summed through LDS in group
+// order: its serial chain of dependent adds is G times shorter.
 __global__ __launch_bounds__(256) void k_reduce_jobs(RedJobs jobs) {
+    __shared__ float4 red[256];
     int jb = 0;
     while (jb + 1 < jobs.njobs && (int)blockIdx.x >= jobs.start[jb + 1]) ++jb;
     const RedJob J = jobs.j[jb];
-    const int64_t i0 = 4 * ((int64_t)(blockIdx.x - jobs.start[jb]) * blockDim.x + threadIdx.x);
-    if (i0 >= J.n) return;
+    const int G = J.groups, EQ = 256 / G;  // block-uniform
+    const int sg = threadIdx.x / EQ, eq = threadIdx.x % EQ;
+    const int64_t i0 = 4 * ((int64_t)(blockIdx.x - jobs.start[jb]) * EQ + eq);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    if (i0 + 4 <= J.n && (J.stride % 4) == 0 && ((uintptr_t)J.slab & 15) == 0) {
-        const float4* p = (const float4*)(J.slab + i0);
-        const int64_t st = J.stride / 4;
+    if (i0 < J.n) {
+        if (i0 + 4 <= J.n && (J.stride % 4) == 0 && ((uintptr_t)J.slab & 15) == 0) {
+            const float4* p = (const float4*)(J.slab + i0);
+            const int64_t st = J.stride / 4;
 #pragma unroll 8
-        for (int k = 0; k < J.nslabs; ++k) {
-            const float4 v = p[(size_t)k * st];
+            for (int k = sg; k < J.nslabs; k += G) {
+                const float4 v = p[(size_t)k * st];
+                s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+            }
+        } else {
+            for (int k = sg; k < J.nslabs; k += G)
+                for (int e = 0; e < 4 && i0 + e < J.n; ++e) s[e] += J.slab[(size_t)k * J.stride + i0 + e];
+        }
+    }
+    if (G > 1) {
+        red[threadIdx.x] = make_float4(s[0], s[1], s[2], s[3]);
+        __syncthreads();
+        if (sg != 0) return;
+        for (int g = 1; g < G; ++g) {
+            const float4 v = red[g * EQ + eq];
             s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
         }
-    } else {
-        for (int k = 0; k < J.nslabs; ++k)
-            for (int e = 0; e < 4 && i0 + e < J.n; ++e) s[e] += J.slab[(size_t)k * J.stride + i0 + e];
     }
+    if (i0 >= J.n) return;
     for (int e = 0; e < 4 && i0 + e < J.n; ++e) {
         const int64_t i = i0 + e;
         int64_t o = i;
@@ -1872,9 +1890,20 @@ PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void*
         if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n ||
             (J.bias_out && (J.cols_in <= J.cols_out || J.cols_out <= 0 || J.n % J.cols_in)))
             return fail(-1, "pmlp_reduce_slabs: bad job " + std::to_string(i));
-        rj.j[i] = RedJob{J.slab, J.out, J.bias_out, J.stride, J.n, J.nslabs, J.cols_in, J.cols_out};
+        static const bool split = [] {
+            const char* v = getenv("PMLP_REDUCE_GROUPS");  // 0: one thread per quad (A/B knob)
+            return !(v && v[0] == '0');
+        }();
+        static const int spt = [] {  // target slabs per thread (A/B knob)
+            const char* v = getenv("PMLP_REDUCE_SPT");
+            return v ? std::max(1, atoi(v)) : 8;
+        }();
+        int G = 1;  // <= spt slabs per thread, at most 32 groups
+        while (split && G < 32 && J.nslabs > spt * G) G *= 2;
+        rj.j[i] = RedJob{J.slab, J.out, J.bias_out, J.stride, J.n, J.nslabs, J.cols_in, J.cols_out, G};
         rj.start[i] = (int)nb;
-        nb += (J.n + 4 * 256 - 1) / (4 * 256);
+        const int64_t eqb = 256 / G;  // element quads per block
+        nb += ((J.n + 3) / 4 + eqb - 1) / eqb;
     }
     rj.start[njobs] = (int)nb;
     rj.njobs = njobs;
