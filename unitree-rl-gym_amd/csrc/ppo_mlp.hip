@@ -1191,6 +1191,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_final(LossArgs a, const fl
                                                             float* __restrict__ dstd) {
     const int W = 3 + a.A, q = blockIdx.x;
     float x = 0.f;
+#pragma unroll 8
     for (int b = threadIdx.x; b < nblocks; b += 64) x += partial[(size_t)b * W + q];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -1241,6 +1242,9 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_opt_prepare(const float* _
                                                                   float desired_kl, int adaptive) {
     __shared__ float sh[4];
     float s = 0.f;
+    // unrolled so that several of a thread's loads are in flight (a rolled loop is a chain
+    // of dependent round trips)
+#pragma unroll 8
     for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * PMLP_OPT_THREADS) {
         const float v = g[i] * scale;
