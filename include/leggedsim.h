@@ -89,6 +89,10 @@ typedef struct lgs_model_desc {
     const int32_t* pt_body;   /* [P]                                     */
     const float* pt_pos;      /* [P][3] body frame                        */
     const float* pt_radius;   /* [P]                                     */
+    /* names, copied at lgs_create_sim (get_asset_rigid_body_names / get_asset_dof_names,
+     * legged_robot.py:342-343); either may be NULL (the queries then return NULL / -1) */
+    const char* const* body_names; /* [B] */
+    const char* const* dof_names;  /* [D] */
 } lgs_model_desc;
 
 /* ---- simulation parameters: cfg.sim + cfg.sim.physx + cfg.asset
@@ -329,8 +333,19 @@ LGS_API int lgs_set_heightfield(lgs_sim* sim, const int16_t* heights, int32_t ro
  * proxies and pairs of every env (host descriptor, copied; NULL or num_pairs = 0: off) */
 LGS_API int lgs_set_self_collision(lgs_sim* sim, const lgs_self_collision_desc* desc);
 
-/* name/index queries */
+/* name/index queries (legged_robot.py:332-343, 388-407):
+ *  lgs_get_counts     <- get_asset_dof_count / get_asset_rigid_body_count (:332-333)
+ *  lgs_get_body_name  <- get_asset_rigid_body_names()[i] (:342); NULL when out of range or unnamed
+ *  lgs_get_dof_name   <- get_asset_dof_names()[i] (:343); NULL likewise.  The strings are owned by
+ *                        the sim and live until lgs_destroy_sim.
+ *  lgs_find_body      <- find_actor_rigid_body_handle(env, actor, name) (:388-407): the body index
+ *                        (bodies are env-major, so the index is the same in every env), -1 if absent
+ *  lgs_find_dof       <- find_actor_dof_handle: the DOF index, -1 if absent                         */
 LGS_API int lgs_get_counts(lgs_sim* sim, int32_t* num_envs, int32_t* num_bodies, int32_t* num_dofs);
+LGS_API const char* lgs_get_body_name(lgs_sim* sim, int32_t index);
+LGS_API const char* lgs_get_dof_name(lgs_sim* sim, int32_t index);
+LGS_API int32_t lgs_find_body(lgs_sim* sim, const char* name);
+LGS_API int32_t lgs_find_dof(lgs_sim* sim, const char* name);
 
 /* diagnostics: per-phase s_memtime cycle sums [N][24] of the last lgs_step
  * (only in a library built with -DLGS_PHASE_STAMPS; otherwise LGS_ERR_STATE) */

@@ -1140,6 +1140,23 @@ void orc_post_physics_env(const lgs_model_desc* md, const lgs_task_params* T, in
     for (int i = 0; i < 6; ++i) E->last_root_vel[6 * e + i] = root[7 + i];
 }
 
+/* _push_robots (:549-550) + bookkeeping (:709) across envs: when ANY env was pushed this
+ * step, the reference writes root_states[:, 7:9] of every env (one draw per env; only the
+ * pushed envs are sent to the simulation, :553-555) and last_root_vel then copies that
+ * tensor.  The simulated state keeps the velocities of the envs not pushed; last_root_vel
+ * takes the draws of all envs.  Pushed envs are those with ep_len % interval == 0 after the
+ * step (the ones reset this step included). */
+static void push_last_root_vel(const lgs_task_params* T, int N, const lgs_env_buffers* E, int64_t step_counter) {
+    if (!T->push_robots) return;
+    int any = 0;
+    for (int e = 0; e < N && !any; ++e) any = (E->episode_length[e] % T->push_interval) == 0;
+    if (!any) return;
+    for (int e = 0; e < N; ++e)
+        for (int j = 0; j < 2; ++j)
+            E->last_root_vel[6 * e + j] = rand_range(-T->max_push_vel_xy, T->max_push_vel_xy,
+                                                     orc_uniform(T->seed, e, (uint32_t)step_counter, LGS_STREAM_PUSH, j));
+}
+
 /* ====================================================== entry points === */
 
 /* one substep for all envs (lgs_simulate) */
@@ -1172,6 +1189,7 @@ void orc_step(const lgs_model_desc* md, const lgs_sim_params* sp, const lgs_task
         ostate st = {root, dofs, cforce, T->write_body_states ? rbs : NULL};
         orc_post_physics_env(md, T, N, e, &st, E, step_counter);
     }
+    push_last_root_vel(T, N, E, step_counter);
 }
 
 /* lgs_step_physics: clip + decimation x (PD + substep) + body states, no post-physics */
@@ -1209,6 +1227,7 @@ void orc_post_physics(const lgs_model_desc* md, const lgs_task_params* T, int N,
         ostate st = {root, dofs, cforce, rbs};
         orc_post_physics_env(md, T, N, e, &st, E, step_counter);
     }
+    push_last_root_vel(T, N, E, step_counter);
 }
 
 void orc_compute_torques(const lgs_task_params* T, int N, int D, const float* act, const float* dofs,

@@ -47,3 +47,13 @@ def test_error_path_without_gpu_is_a_status_not_a_crash():
     h = C.c_void_p()
     rc = lib.lgs_create_sim(None, None, 0, 0, C.byref(h))
     assert rc != 0 and lib.lgs_last_error()
+
+
+def test_name_queries_without_a_sim_are_null_not_a_crash():
+    """lgs_get_body_name / lgs_get_dof_name / lgs_find_body / lgs_find_dof (the gym name
+    queries of legged_robot.py:342-343, 388-407) on a NULL sim: NULL / -1 and an error text."""
+    from leggedsim import native
+    lib = native.load()
+    assert lib.lgs_get_body_name(None, 0) is None and lib.lgs_last_error()
+    assert lib.lgs_get_dof_name(None, 0) is None
+    assert lib.lgs_find_body(None, b"base") == -1 and lib.lgs_find_dof(None, b"x") == -1

@@ -2,11 +2,14 @@
 one flat-bucket gradient all-reduce per optimizer step gives every rank the
 mean gradient and identical parameters."""
 import os
+import sys
 import socket
 
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -70,3 +73,54 @@ def test_two_rank_gradient_allreduce_and_identical_params():
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert all(same for _, _, same in res), res
+
+
+def _check_recurrent_two_ranks(device, rel_tol):
+    import numpy as np
+    import dp_recurrent as dr
+    res = dr.two_ranks(device, _free_port())
+    # identical parameters and learning rate on both ranks after the update
+    assert np.array_equal(res[0][1], res[1][1])
+    assert res[0][2] == res[1][2]
+    # == one rank over both shards (interleaved so its mini-batches are the ranks' unions)
+    flat1, lr1, losses1 = dr.run(dr.interleaved(), device)
+    assert lr1 == res[0][2]  # the same KL decisions (global mini-batch KL, in the gradient bucket)
+    p0 = dr.initial_params().numpy()
+    d1, d2 = flat1.numpy() - p0, res[0][1] - p0
+    assert np.abs(d1).max() > 0
+    lr = 1e-3
+    bad = (np.abs(d1 - d2) > rel_tol * lr).mean()
+    assert bad < 0.02, bad
+    assert np.abs(d1 - d2).max() <= 2 * dr.EPOCHS * dr.MINI_BATCHES * 1.5 * lr
+
+
+def test_two_rank_recurrent_update_equals_one_rank_of_both_shards():
+    """configs[3]/[4]'s data-parallel LSTM update (dense form, torch statement on the CPU):
+    one bucket all-reduce per optimizer step carries the gradient AND the mini-batch KL."""
+    _check_recurrent_two_ranks("cpu", 0.01)
+
+
+def _any_rank_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(here, "..", "unitree-rl-gym_amd"), here]
+    from rsl_rl.algorithms import PPO
+    from rsl_rl.modules import ActorCritic
+    ppo = PPO(ActorCritic(6, 6, 3, [16], [16]), device="cpu")
+    # a capture that failed on rank 0 only: every rank must fall back together
+    q.put((rank, ppo._any_rank(rank == 0), ppo._any_rank(False)))
+    dist.destroy_process_group()
+
+
+def test_capture_fallback_is_decided_by_all_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_any_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(a is True and b is False for _, a, b in res), res

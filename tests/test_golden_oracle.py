@@ -93,6 +93,12 @@ def test_post_physics_matches_reference(task, oracle_lib):
         np.testing.assert_allclose(b["priv_obs"], g["out_priv"], **TOL)
     np.testing.assert_allclose(b["last_actions"], g["out_last_actions"], **TOL)
     np.testing.assert_allclose(b["last_dof_vel"], g["out_last_dof_vel"], **TOL)
+    # the fixture has a push step (ep_len at the push boundary, resets): last_root_vel takes
+    # the reference's all-env draw of root_states[:, 7:9] (:549-550, :709) ...
+    assert (g["out_root_tensor"][:, 7:9] != g["out_root"][:, 7:9]).any()
+    np.testing.assert_allclose(b["last_root_vel"], g["out_last_root_vel"], **TOL)
+    # ... while the state (what the simulation integrates next) keeps the envs not pushed
+    # (out_root: what set_actor_root_state_tensor_indexed sent to the sim, :553-555)
     nsum = len(s.sum_names)
     means = b["episode_acc"][:nsum] / max(b["episode_acc"][nsum], 1.0) / s.max_episode_length_s
     np.testing.assert_allclose(means, g["out_extras_episode"], **TOL)

@@ -9,12 +9,15 @@ KL for the adaptive learning rate), within the bf16 GEMMs' reduction-order toler
 """
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 N, T, O, A = 512, 8, 48, 12
 HID = [512, 256, 128]
@@ -160,3 +163,27 @@ def test_rccl_all_reduce_replays_inside_a_captured_graph():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     r = subprocess.run([sys.executable, "-c", _CAPTURE_PROBE], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "captured all-reduce OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_two_rank_recurrent_update_equals_one_rank_of_both_shards():
+    """BASELINE configs[3]/[4] (H1 / H1_2 x 8 GPUs train ActorCriticRecurrent): two ranks of
+    the dense recurrent update on the GPU (LSTM sequence kernels, fused PPO loss, GAE with the
+    moments all-reduce; gloo on CUDA tensors, both ranks on cuda:0, no capture) at H1 shapes.
+    One all-reduce per optimizer step carries the gradient bucket and the mini-batch KL.
+    The ranks end bit-identical, and 2 x N envs == one rank of the same 2N envs (interleaved
+    so its mini-batches are the ranks' unions) within the recurrent update's tolerance."""
+    import dp_recurrent as dr
+    res = dr.two_ranks("cuda", _free_port())
+    assert np.array_equal(res[0][1], res[1][1])
+    assert res[0][2] == res[1][2]
+    flat1, lr1, losses1 = dr.run(dr.interleaved(), "cuda")
+    assert lr1 == pytest.approx(res[0][2], rel=1e-6)
+    # each rank logs its own mini-batch means; their average is the union's mean
+    np.testing.assert_allclose(0.5 * (np.array(res[0][3]) + np.array(res[1][3])), losses1, rtol=1e-3, atol=1e-5)
+    p0 = dr.initial_params().numpy()
+    d1, d2 = flat1.numpy() - p0, res[0][1] - p0
+    lr = 1e-3
+    assert np.abs(d1).max() > 0
+    bad = (np.abs(d1 - d2) > 0.1 * lr).mean()
+    assert bad < 0.02, bad
+    assert np.abs(d1 - d2).max() <= 2 * dr.EPOCHS * dr.MINI_BATCHES * 1.5 * lr

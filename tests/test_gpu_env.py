@@ -411,3 +411,21 @@ def test_rollout_graph_matches_eager_rollouts(tmp_path):
     assert any(k[0] == "Train/mean_reward" for k in e["scalars"])
     for k, v in e["scalars"].items():
         assert v == pytest.approx(g["scalars"][k], rel=1e-6, abs=1e-7), k
+
+
+@pytest.mark.parametrize("task", ["go2", "h1"])
+def test_name_queries_match_the_model(task):
+    """The C ABI's name queries return the URDF body/DOF names in the simulator's order, and
+    find_body resolves the env's feet / contact indices (find_actor_rigid_body_handle)."""
+    import isaacgym  # noqa: F401
+    from legged_gym.envs import task_registry
+    from legged_gym.utils import get_args
+    env, _ = task_registry.make_env(name=task, args=get_args(["--task", task, "--num_envs", "8", "--headless"]))
+    assert env.sim.body_names() == list(env.model.body_names)
+    assert env.sim.dof_names() == list(env.model.dof_names)
+    for i in env.feet_indices.tolist():
+        assert env.sim.find_body(env.model.body_names[i]) == i
+    assert env.sim.find_body("no_such_link") == -1
+    assert env.sim.find_dof(env.model.dof_names[-1]) == len(env.model.dof_names) - 1
+    lib = env.sim.lib
+    assert lib.lgs_get_body_name(env.sim.handle, len(env.model.body_names)) is None

@@ -389,3 +389,104 @@ def test_loss_step_kernel_matches_fp32_autograd(M, A, Ap):
     assert torch.count_nonzero(dmu[:, A:].float()) == 0
     torch.testing.assert_close(dv[:, :1].float(), tv.grad.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-9)
     assert torch.count_nonzero(dv[:, 1:].float()) == 0
+
+
+def test_refused_update_capture_falls_back_to_the_eager_update(monkeypatch):
+    """A capture that raises (as a collective library refusing capture would) leaves the
+    update eager and training: the update runs, parameters move, no graph is kept; the same
+    for the recurrent (autograd) update graph."""
+    from contextlib import contextmanager
+    from rsl_rl.modules import ActorCriticRecurrent
+
+    @contextmanager
+    def refused(*a, **k):
+        raise RuntimeError("capture refused (test)")
+        yield  # noqa
+
+    torch.manual_seed(0)
+    N, T, O, A = 512, 8, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [128, 64], [128, 64]).cuda(), num_learning_epochs=1, num_mini_batches=2,
+              device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    _fill_storage(alg, T, N, O, A, seed=4)
+    alg.update()  # eager first call
+    monkeypatch.setattr(torch.cuda, "graph", refused)
+    _fill_storage(alg, T, N, O, A, seed=5)
+    p0 = [p.detach().clone() for p in alg.actor_critic.parameters()]
+    with pytest.warns(UserWarning, match="capturing the update failed"):
+        losses = alg.update()
+    assert alg._fgraph is None and not alg.use_graph and np.isfinite(losses).all()
+    assert any(not torch.equal(p, q) for p, q in zip(alg.actor_critic.parameters(), p0))
+    # recurrent: the warm-up pass is undone, then the eager update runs once
+    ac = ActorCriticRecurrent(O, O + 3, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                              rnn_hidden_size=64, rnn_num_layers=1).cuda()
+    ralg = PPO(ac, num_learning_epochs=1, num_mini_batches=2, device="cuda")
+    ralg.init_storage(N, T, [O], [O + 3], [A])
+    assert ralg.use_graph
+    for it in range(2):
+        st = ralg.storage
+        g = torch.Generator(device="cuda").manual_seed(it)
+        for k in ("observations", "privileged_observations", "actions", "mu", "values", "rewards"):
+            getattr(st, k).copy_(torch.randn(getattr(st, k).shape, device="cuda", generator=g))
+        st.sigma.fill_(1.0)
+        st.actions_log_prob.copy_(torch.distributions.Normal(st.mu, st.sigma).log_prob(st.actions).sum(-1, keepdim=True))
+        st.hidden_state_slots(0, [(1, N, 64)] * 2, [(1, N, 64)] * 2)
+        st.step = T
+        ralg.compute_returns(torch.randn(N, O + 3, device="cuda", generator=g))
+        p0 = [p.detach().clone() for p in ac.parameters()]
+        if it == 1:
+            with pytest.warns(UserWarning, match="capturing the update failed"):
+                losses = ralg.update()
+            assert ralg._graph is None and not ralg.use_graph
+        else:
+            losses = ralg.update()
+        assert np.isfinite(losses).all()
+        assert any(not torch.equal(p, q) for p, q in zip(ac.parameters(), p0))
+
+
+def test_deep_mlp_keeps_the_autograd_update():
+    """More Linear layers per net than the Adam mirror takes (PMLP_MAX_MIRROR jobs): the fused
+    step is refused at construction and the autograd update trains instead."""
+    torch.manual_seed(0)
+    N, T, O, A = 256, 8, 48, 12
+    hid = [64, 64, 64, 64]  # 5 Linear layers per net: 10 bf16 weight copies > 8
+    alg = PPO(ActorCritic(O, O, A, hid, hid).cuda(), num_learning_epochs=1, num_mini_batches=2, device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    assert alg._fused is None
+    _fill_storage(alg, T, N, O, A, seed=6)
+    p0 = [p.detach().clone() for p in alg.actor_critic.parameters()]
+    assert np.isfinite(alg.update()).all()
+    assert all(not torch.equal(p, q) for p, q in zip(alg.actor_critic.parameters(), p0))
+
+
+def test_load_between_learn_calls_reaches_the_captured_rollout(tmp_path):
+    """OnPolicyRunner.load() after the rollout graph was captured: the next replayed rollout
+    samples from the LOADED policy (the graph reads the bf16 weight copies, which the runner
+    refreshes before the replay), not from the weights the copies held before the load."""
+    import isaacgym  # noqa: F401
+    from legged_gym.envs import task_registry
+    from legged_gym.utils import get_args
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    args = get_args(["--task", "go2", "--num_envs", "512", "--headless"])
+    env, _ = task_registry.make_env(name="go2", args=args)
+    _, train_cfg = task_registry.get_cfgs("go2")
+    cfg = class_to_dict(train_cfg)
+    torch.manual_seed(1)
+    donor = OnPolicyRunner(env, cfg, log_dir=None, device="cuda:0")
+    with torch.no_grad():
+        for p in donor.alg.actor_critic.actor.parameters():
+            p.mul_(-1.5)  # far from the runner's own policy
+    path = str(tmp_path / "ck.pt")
+    donor.save(path)
+    want_actor = copy.deepcopy(donor.alg.actor_critic.actor).float()
+    torch.manual_seed(2)
+    runner = OnPolicyRunner(env, cfg, log_dir=None, device="cuda:0")
+    runner.learn(2)
+    assert runner._rollout_graph is not None
+    runner.load(path)
+    runner.learn(1)  # replays the captured rollout, then updates
+    st = runner.alg.storage
+    with torch.no_grad():
+        mu = want_actor(st.observations[:4].reshape(-1, st.observations.shape[-1]))
+    torch.testing.assert_close(st.mu[:4].reshape(mu.shape), mu, rtol=0.05, atol=0.05)  # bf16 GEMMs

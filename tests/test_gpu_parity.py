@@ -312,6 +312,16 @@ def test_heightfield_step_matches_oracle_bitwise(task):
     bridge.set_ground(bridge.ensure_built())
 
 
+def test_g1_rough_at_its_baseline_size_matches_oracle_bitwise():
+    """BASELINE configs[2] as benched: G1, 4096 envs, the default curriculum map (10 x 20
+    tiles of 8 m at 0.1 m + 25 m border: int16 1300 x 2100, legged_robot_config.py:63-87),
+    envs spread over every tile row (rows = difficulty levels)."""
+    env, g = warm("g1_rough", 4096, steps=8, seed=4096)
+    assert env.height_samples.shape == (1300, 2100)
+    fused_vs_oracle(env, g, 2, "g1_rough x4096 default map")
+    bridge.set_ground(bridge.ensure_built())
+
+
 @pytest.mark.parametrize("task", ["go2", "h1"])
 def test_reset_idx_subset_matches_oracle(task):
     """reset_idx(env_ids) for a random subset (legged_robot.py:723-768): the masked launch

@@ -91,3 +91,40 @@ def test_reset_idx_subset_through_the_python_api():
     got = np.array([float(env.extras["episode"]["rew_" + k]) for k in env._sum_names])
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
     env.step(torch.zeros(256, 12, device="cuda"))  # the env keeps stepping normally
+
+
+def _extra_term(k):
+    def term(self):
+        return (k + 1) * torch.square(self.base_lin_vel[:, 2]) + 0.01 * k
+    return term
+
+
+Go2ManyTerms = type("Go2ManyTerms", (LeggedRobot,),
+                    {f"_reward_extra_{k:02d}": _extra_term(k) for k in range(26)})
+
+
+def test_many_python_reward_terms_on_two_envs_per_wave():
+    """Go2 runs two envs per wave (32 lanes per env): with 10 native + 26 Python terms the
+    episode-sum rows (36) exceed the lanes of one env, and every row must still join the
+    reset-time extras and be zeroed on reset (post_physics strides the rows)."""
+    def edit(cfg):
+        for k in range(26):
+            setattr(cfg.rewards.scales, f"extra_{k:02d}", 0.1)
+    env = _make("go2_many_terms", Go2ManyTerms, edit)
+    assert env.task_params.num_extra_sums == 26
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(10):
+        env.step(0.5 * torch.randn(256, 12, device="cuda", generator=g))
+    names = list(env._sum_names)
+    assert len(names) >= 36
+    before = {k: env.episode_sums[k].clone() for k in names}
+    # a whole batch of time-outs: every env resets at the next step
+    env.episode_length_buf = torch.full_like(env.episode_length_buf, int(env.max_episode_length))
+    _, _, _, _, extras = env.step(0.5 * torch.randn(256, 12, device="cuda", generator=g))
+    assert env.reset_buf.all()
+    for k in names:
+        # the resetting step adds its own term, hands the sums to the extras, then zeroes them
+        assert (env.episode_sums[k] == 0).all(), k
+        if k.startswith("extra_"):  # positive terms: a row left out of the extras would read 0
+            assert float(extras["episode"]["rew_" + k]) > float(before[k].mean()) / env.max_episode_length_s * 0.99, k

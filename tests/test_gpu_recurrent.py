@@ -258,3 +258,54 @@ def test_recurrent_rollout_saves_the_pre_step_state_from_the_kernel():
                 assert bool((g == 0).all())
             else:
                 assert torch.equal(g, p)
+
+
+@pytest.mark.parametrize("robot", ["g1", "h1", "h1_2"])
+def test_hip_lstm_matches_pretrained_policy_golden(robot):
+    """The reference's own pretrained recurrent policies (deploy/pre_train/<robot>/motion.pt,
+    extracted to tests/golden/lstm_policy_<robot>.npz: weights + the 20-step outputs from a
+    fresh memory and again after reset_memory) through the HIP LSTM kernels:
+    (a) the in-place rollout step (Memory.step_ -> pmlp_lstm_step, what act_inference and the
+        captured rollout run), with a reset of the memory rows before the second sequence;
+    (b) the dense sequence kernel of the update (lstm_dense), with the reset mask.
+    The golden sequence sits in a few rows of a batch of random envs (the kernels index envs
+    correctly) and must match at 1e-5 (helpers.py:163-189 PolicyExporterLSTM semantics)."""
+    import os
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, f"lstm_policy_{robot}.npz"))
+    n_in = g["w.memory.weight_ih_l0"].shape[1]
+    n_act = g["w.actor.2.weight"].shape[0]
+    ac = ActorCriticRecurrent(n_in, n_in + 3, n_act, actor_hidden_dims=[32], critic_hidden_dims=[32],
+                              rnn_type="lstm", rnn_hidden_size=64, rnn_num_layers=1, init_noise_std=0.8)
+    sd = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w.")}
+    ac.actor.load_state_dict({k[len("actor."):]: v for k, v in sd.items() if k.startswith("actor.")})
+    ac.memory_a.rnn.load_state_dict({k[len("memory."):]: v for k, v in sd.items() if k.startswith("memory.")})
+    ac = ac.cuda().eval()
+    xs = torch.from_numpy(g["inputs"]).cuda()  # [20, n_in]
+    steps, B, rows = xs.shape[0], 1000, [0, 517, 999]
+    torch.manual_seed(11)
+    seq = torch.randn(steps + 5, B, n_in, device="cuda")
+    for r in rows:
+        seq[:steps, r] = xs
+        seq[steps:, r] = xs[:5]
+    reset = torch.zeros(steps + 5, B, dtype=torch.uint8, device="cuda")
+    reset[steps, rows] = 1
+    want = torch.from_numpy(np.concatenate([g["outputs"], g["outputs_after_reset"]])).cuda()
+    # (a) rollout steps in place (act_inference: Memory.forward -> lstm_seq.lstm_step_)
+    ac.memory_a.hidden_states = None
+    got = []
+    with torch.no_grad():
+        for t in range(steps + 5):
+            if t == steps:
+                ac.memory_a.reset(reset[t].bool())
+            got.append(ac.act_inference(seq[t]))
+    got = torch.stack(got)
+    assert lstm_seq.usable(ac.memory_a.rnn, seq[0])
+    for r in rows:
+        torch.testing.assert_close(got[:, r], want, rtol=1e-5, atol=1e-5)
+    # (b) the dense sequence kernel (the update's forward), zero state at t = 0
+    with torch.no_grad():
+        h = lstm_seq.lstm_dense(ac.memory_a.rnn, seq, None, None, reset)
+        mu = ac.actor(h.reshape(-1, 64)).view(steps + 5, B, n_act)
+    for r in rows:
+        torch.testing.assert_close(mu[:, r], want, rtol=1e-5, atol=1e-5)

@@ -239,3 +239,36 @@ def test_recurrent_rollout_saves_pre_step_hidden_states():
     d = ppo.storage.dones[:, :, 0].bool()
     for t in range(1, 6):  # after a done the stored state is zero
         assert saved[t, 0][d[t - 1]].abs().sum() == 0
+
+
+def test_gru_policy_trains_on_the_padded_generator():
+    """ActorCriticRecurrent(rnn_type='gru'): the dense (LSTM-only) update form is not taken;
+    the update runs rsl_rl's padded-trajectory generator and trains."""
+    env = FakeEnv(num_envs=8, num_privileged_obs=9, ep_len=5)
+    ac = ActorCriticRecurrent(6, 9, 3, actor_hidden_dims=[16], critic_hidden_dims=[16], rnn_type="gru",
+                              rnn_hidden_size=8, rnn_num_layers=1)
+    ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=2, device="cpu")
+    assert not ppo._dense_recurrent
+    ppo.init_storage(8, 6, [6], [9], [3])
+    obs, priv = env.reset()
+    with torch.inference_mode():
+        for _ in range(6):
+            a = ppo.act(obs, priv)
+            obs, priv, r, d, info = env.step(a)
+            ppo.process_env_step(r, d, info)
+        ppo.compute_returns(priv)
+    p0 = [p.detach().clone() for p in ac.parameters()]
+    losses = ppo.update()
+    assert np.isfinite(losses).all()
+    assert any(not torch.equal(p, q) for p, q in zip(ac.parameters(), p0))
+
+
+def test_fused_step_refuses_nets_deeper_than_the_adam_mirror():
+    """FusedPPOStep raises ValueError (which init_storage catches) for more Linear layers per
+    net than PMLP_MAX_MIRROR / 2, before it allocates anything."""
+    from rsl_rl.algorithms import fused_step
+    from rsl_rl.modules import mfma_mlp
+    hid = [16] * mfma_mlp.PMLP_MAX_MIRROR  # PMLP_MAX_MIRROR + 1 Linear layers per net
+    ppo = PPO(ActorCritic(6, 6, 3, hid, hid), device="cpu")
+    with pytest.raises(ValueError, match="Linear layers"):
+        fused_step.FusedPPOStep(ppo, 64)

@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/leggedsim.h"
 #include "lgs_detmath.h"
@@ -1789,15 +1790,16 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         if (lane < 6) s.root[7 + lane] = rv;
         if (reset_mode == RESET_IDS && lane == 0) E.reset[e] = 1;  // reset_buf[env_ids] = 1 (:758)
         if (reset_mode != RESET_ALL) {
+            // (strided: two envs per wave leave 32 lanes per env, and a task may have more sums)
             const int nsum = num_sums(T);
-            if (lane < nsum) {
-                atomicAdd(E.episode_acc + lane, E.episode_sums[(size_t)lane * N + e]);
-                E.episode_sums[(size_t)lane * N + e] = 0.f;
+            for (int k = lane; k < nsum; k += WAVE / EPW) {
+                atomicAdd(E.episode_acc + k, E.episode_sums[(size_t)k * N + e]);
+                E.episode_sums[(size_t)k * N + e] = 0.f;
             }
             if (lane == 0) atomicAdd(E.episode_acc + nsum, 1.f);
         } else {
             const int nsum = num_sums(T);
-            if (lane < nsum) E.episode_sums[(size_t)lane * N + e] = 0.f;
+            for (int k = lane; k < nsum; k += WAVE / EPW) E.episode_sums[(size_t)k * N + e] = 0.f;
         }
         if (lane == 0) {
             resample_commands(T, E.commands + 4 * e, seed, (uint32_t)e, step, LGS_STREAM_RESET_CMD);
@@ -1946,13 +1948,31 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
 // episode means over the envs reset this step, carried when none reset, and the
 // carried time-out flags — then episode_acc zeroed for the next step and the
 // device step counter advanced (the Philox key of graph-replayed steps).
+// advance = 1 (after a control step) also finishes _push_robots (:540-555): when ANY env
+// was pushed, the reference writes root_states[:, 7:9] of EVERY env with one draw per env
+// and only the pushed envs reach the simulation; bookkeeping (:709) then copies that
+// tensor into last_root_vel.  root_states here IS the simulation state, so it keeps the
+// simulated velocities of the envs not pushed; last_root_vel[:, 0:2] takes
+// the draws for every env, as in the reference (the pushed envs' draws are the ones
+// k_step applied: same Philox key).
 __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
-                                                      int N, int advance) {
+                                                      int N, int advance, uint32_t step) {
     const lgs_task_params& T = *Tp;
     const int nsum = num_sums(T);
     const float cnt = E.episode_acc[nsum];
     const bool any = cnt > 0.f;
     const int t = threadIdx.x;
+    if (E.step_counter) step = (uint32_t)*E.step_counter;  // the key k_step used (read before the advance)
+    if (advance && T.push_robots && E.last_root_vel) {
+        // pushed envs: episode_length % push_interval == 0 after this step (reset ones at 0)
+        int pushed = 0;
+        for (int e = t; e < N && !pushed; e += blockDim.x) pushed = (E.episode_length[e] % T.push_interval) == 0;
+        if (__syncthreads_or(pushed))
+            for (int e = t; e < N; e += blockDim.x)
+                for (int j = 0; j < 2; ++j)
+                    E.last_root_vel[6 * e + j] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy,
+                                                            philox_uniform(T.seed, e, step, LGS_STREAM_PUSH, j));
+    }
     if (E.ep_means && t < nsum) {
         float m = E.ep_means[t];
         if (any) m = E.episode_acc[t] / fmaxf(cnt, 1.f) / T.max_episode_length_s;
@@ -1996,6 +2016,7 @@ struct lgs_sim {
     int rows = 32;
     int chain = 0;  // dof_chain_length of the model
     int epw = 1;    // envs per wave of k_step (2 for the 32-row variant at even N)
+    std::vector<std::string> body_names, dof_names;  // name queries (empty when not given)
 };
 
 // Compiled (dofs, max bodies, constraint-row capacity, chain length) variants.  The
@@ -2142,6 +2163,10 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
         }
     }
     const int B = s->B, D = s->D, P = s->P;
+    if (m->body_names)
+        for (int b = 0; b < B; ++b) s->body_names.emplace_back(m->body_names[b] ? m->body_names[b] : "");
+    if (m->dof_names)
+        for (int j = 0; j < D; ++j) s->dof_names.emplace_back(m->dof_names[j] ? m->dof_names[j] : "");
     // pack the model into one device allocation
     size_t ints = (size_t)B * (4 + LGS_MAX_DEPTH) + (size_t)P;
     size_t floats = (size_t)B * (9 + 3 + 3 + 1 + 3 + 6) + (size_t)D * 3 + (size_t)P * 4;
@@ -2368,7 +2393,8 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     HIP_TRY(hipGetLastError());
     if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
-        hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1);
+        hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
+                           (uint32_t)step_counter);
         HIP_TRY(hipGetLastError());
     }
     return LGS_OK;
@@ -2410,7 +2436,8 @@ LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t*
     LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, env_mask);
     HIP_TRY(hipGetLastError());
     // extras["episode"] over the reset envs and extras["time_outs"]; no step-counter advance
-    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0);
+    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0,
+                       (uint32_t)step_counter);
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
@@ -2425,6 +2452,26 @@ LGS_API int lgs_debug_set_phase_buffer(void* dev_ptr) {
     return set_err(LGS_ERR_STATE, "library built without -DLGS_PHASE_STAMPS");
 #endif
 }
+
+LGS_API const char* lgs_get_body_name(lgs_sim* s, int32_t i) {
+    if (!s || i < 0 || i >= (int32_t)s->body_names.size()) { set_err(LGS_ERR_ARG, "lgs_get_body_name: no such body"); return nullptr; }
+    return s->body_names[i].c_str();
+}
+
+LGS_API const char* lgs_get_dof_name(lgs_sim* s, int32_t i) {
+    if (!s || i < 0 || i >= (int32_t)s->dof_names.size()) { set_err(LGS_ERR_ARG, "lgs_get_dof_name: no such dof"); return nullptr; }
+    return s->dof_names[i].c_str();
+}
+
+static int32_t find_name(const std::vector<std::string>& names, const char* name) {
+    if (!name) return -1;
+    for (size_t i = 0; i < names.size(); ++i)
+        if (names[i] == name) return (int32_t)i;
+    return -1;
+}
+
+LGS_API int32_t lgs_find_body(lgs_sim* s, const char* name) { return s ? find_name(s->body_names, name) : -1; }
+LGS_API int32_t lgs_find_dof(lgs_sim* s, const char* name) { return s ? find_name(s->dof_names, name) : -1; }
 
 LGS_API int lgs_get_counts(lgs_sim* s, int32_t* n, int32_t* b, int32_t* d) {
     if (!s) return set_err(LGS_ERR_ARG, "null sim");

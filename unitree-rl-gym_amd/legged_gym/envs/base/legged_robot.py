@@ -119,6 +119,14 @@ class LeggedRobot(BaseTask):
                                       max_rows=self.max_rows, ground_friction=float(self.cfg.terrain.static_friction))
         self._lgs_params = sp
         self.sim = native.Sim(model, sp, self.num_envs, self.sim_device_id)
+        # names and body handles through the simulator, as the reference asks gym for them
+        # (get_asset_rigid_body_names / get_asset_dof_names :342-343, find_actor_rigid_body_handle :388-407)
+        self.body_names, self.dof_names = self.sim.body_names(), self.sim.dof_names()
+        for attr in ("feet_indices", "penalised_contact_indices", "termination_contact_indices"):
+            idx = getattr(self, attr)
+            found = [self.sim.find_body(spec.body_names[int(i)]) for i in idx.tolist()]
+            if found != idx.tolist():
+                raise RuntimeError(f"{attr}: simulator body handles {found} != model indices {idx.tolist()}")
         self.sim.set_env_properties(friction, added_mass)
         self.shape_friction = friction
         # create_actor(..., self_collisions, 0) (:373-374): 0 lets the links of one robot collide

@@ -47,7 +47,7 @@ class ModelDesc(C.Structure):
         ("joint_rot", f32p), ("joint_pos", f32p), ("axis", f32p), ("mass", f32p), ("com", f32p),
         ("inertia", f32p), ("dof_body", i32p), ("dof_lower", f32p), ("dof_upper", f32p),
         ("dof_effort", f32p), ("dof_velocity", f32p), ("pt_body", i32p), ("pt_pos", f32p),
-        ("pt_radius", f32p),
+        ("pt_radius", f32p), ("body_names", C.POINTER(C.c_char_p)), ("dof_names", C.POINTER(C.c_char_p)),
     ]
 
 
@@ -150,7 +150,13 @@ class ModelHandle:
             fp("mass", m.mass), fp("com", m.com), fp("inertia", m.inertia), ip("dof_body", m.dof_body),
             fp("dof_lower", m.dof_lower), fp("dof_upper", m.dof_upper), fp("dof_effort", m.dof_effort),
             fp("dof_velocity", m.dof_velocity), ip("pt_body", m.pt_body), fp("pt_pos", m.pt_pos),
-            fp("pt_radius", m.pt_radius))
+            fp("pt_radius", m.pt_radius), self._names("body_names", m.body_names),
+            self._names("dof_names", m.dof_names))
+
+    def _names(self, key, names):
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        self._keep[key] = arr
+        return C.cast(arr, C.POINTER(C.c_char_p))
 
 
 def sim_params_from_cfg(sim_cfg=None, asset_cfg=None, **over):

@@ -70,6 +70,12 @@ def load():
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     lib.lgs_set_self_collision.argtypes = [vp, C.POINTER(cabi.SelfCollisionDesc)]
+    for name in ("lgs_get_body_name", "lgs_get_dof_name"):
+        getattr(lib, name).argtypes = [vp, C.c_int32]
+        getattr(lib, name).restype = C.c_char_p
+    for name in ("lgs_find_body", "lgs_find_dof"):
+        getattr(lib, name).argtypes = [vp, C.c_char_p]
+        getattr(lib, name).restype = C.c_int32
     for name in ("lgs_create_sim", "lgs_destroy_sim", "lgs_set_stream", "lgs_synchronize", "lgs_set_env_properties",
                  "lgs_bind_state", "lgs_refresh", "lgs_set_dof_actuation_force", "lgs_simulate",
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
@@ -92,7 +98,7 @@ EXPORTED_SYMBOLS = [
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
-    "lgs_set_self_collision",
+    "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
 ]
 
 
@@ -195,6 +201,24 @@ class Sim:
     def set_dof_indexed(self, src, ids_i32, n):
         check(self.lib, self.lib.lgs_set_dof_state_indexed(self.handle, src.data_ptr(), ids_i32.data_ptr(), n),
               "set_dof_state_indexed")
+
+    # name queries (gym.get_asset_rigid_body_names / get_asset_dof_names /
+    # find_actor_rigid_body_handle, legged_robot.py:342-343, 388-407)
+    def body_names(self):
+        n, b, d = C.c_int32(), C.c_int32(), C.c_int32()
+        check(self.lib, self.lib.lgs_get_counts(self.handle, C.byref(n), C.byref(b), C.byref(d)), "lgs_get_counts")
+        return [self.lib.lgs_get_body_name(self.handle, i).decode() for i in range(b.value)]
+
+    def dof_names(self):
+        n, b, d = C.c_int32(), C.c_int32(), C.c_int32()
+        check(self.lib, self.lib.lgs_get_counts(self.handle, C.byref(n), C.byref(b), C.byref(d)), "lgs_get_counts")
+        return [self.lib.lgs_get_dof_name(self.handle, i).decode() for i in range(d.value)]
+
+    def find_body(self, name):
+        return int(self.lib.lgs_find_body(self.handle, name.encode()))
+
+    def find_dof(self, name):
+        return int(self.lib.lgs_find_dof(self.handle, name.encode()))
 
     def close(self):
         if getattr(self, "handle", None):

@@ -46,6 +46,10 @@ class FusedPPOStep:
         self.lins = [[m for m in s if isinstance(m, nn.Linear)] for s in seqs]
         if len(self.lins[0]) != len(self.lins[1]):
             raise ValueError("fused PPO step: actor and critic must have the same depth")
+        if 2 * len(self.lins[0]) > mm.PMLP_MAX_MIRROR:
+            # every weight's bf16 copy is one Adam mirror job (include/ppo_mlp.h); a deeper
+            # net keeps the autograd update (PPO.init_storage catches this)
+            raise ValueError(f"fused PPO step: at most {mm.PMLP_MAX_MIRROR // 2} Linear layers per net")
         params = [p for ls in self.lins for lin in ls for p in (lin.weight, lin.bias)] + [ac.std]
         if sorted(map(id, params)) != sorted(map(id, ac.parameters())):
             raise ValueError("fused PPO step: unexpected parameter set")

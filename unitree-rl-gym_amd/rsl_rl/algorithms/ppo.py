@@ -72,9 +72,13 @@ class PPO:
         # (library bf16 GEMMs under autocast drift inside a captured graph on this ROCm;
         #  the MFMA MLP kernels are deterministic and capture cleanly)
         # recurrent policies train in the dense form (storage.recurrent_dense_mini_batch_generator,
-        # modules/lstm_seq.py): fixed shapes and no host sync, so their update captures too
+        # modules/lstm_seq.py): fixed shapes and no host sync, so their update captures too.
+        # The dense form covers one-layer LSTMs; a GRU (or a deeper LSTM) keeps rsl_rl's
+        # padded-trajectory generator and the eager update.
         self._dense_recurrent = getattr(self.actor_critic, "is_recurrent", False) and \
-            hasattr(self.actor_critic, "act_dense")
+            hasattr(self.actor_critic, "act_dense") and \
+            all(isinstance(getattr(getattr(self.actor_critic, m, None), "rnn", None), nn.LSTM) and
+                getattr(self.actor_critic, m).rnn.num_layers == 1 for m in ("memory_a", "memory_c"))
         self.use_graph = on_gpu and (not getattr(self.actor_critic, "is_recurrent", False) or
                                      self._dense_recurrent) and \
             self.optimizer.defaults.get("capturable", False) and \
@@ -91,6 +95,7 @@ class PPO:
         self._diag, self._diag_i = None, 0
         self._graph_calls = 0
         self._capturing = False
+        self._gflat = None  # world > 1: the gradient bucket (_grad_bucket)
         if self.world_size > 1:
             for p in params:  # identical initial policy on every rank
                 dist.broadcast(p.data, src=0)
@@ -197,9 +202,39 @@ class PPO:
         stats = self._global_adv_stats if self.world_size > 1 else None
         self.storage.compute_returns(last_values, self.gamma, self.lam, adv_stats=stats)
 
-    def _allreduce_grads(self):
-        grads = [p.grad for p in self.actor_critic.parameters() if p.grad is not None]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+    def _grad_bucket(self):
+        """world > 1: ONE flat buffer whose views are every parameter's .grad, plus a
+        one-float tail for the mini-batch KL.  backward() accumulates into the views in
+        place, so the optimizer step's single all-reduce covers the gradient and the KL
+        that drives the adaptive learning rate (no cat/copy-back, no second collective)."""
+        params = list(self.actor_critic.parameters())
+        if self._gflat is None:
+            self._gflat = torch.zeros(sum(p.numel() for p in params) + 1, device=self.device)
+            off = 0
+            self._gviews = []
+            for p in params:
+                self._gviews.append(self._gflat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        for p, v in zip(params, self._gviews):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+        return self._gflat
+
+    def _allreduce_grads(self, kl=None):
+        """Mean of the gradients over the ranks in one all-reduce.  kl (a 0-d tensor, this
+        rank's mini-batch KL) rides in the same bucket; returns the ranks' mean KL."""
+        params = [p for p in self.actor_critic.parameters() if p.grad is not None]
+        b = self._gflat
+        if b is not None and len(params) == len(self._gviews) and \
+                all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(params, self._gviews)):
+            if kl is not None:
+                b[-1:].copy_(kl.reshape(1))
+            dist.all_reduce(b)
+            b.div_(self.world_size)
+            return b[-1] if kl is not None else None
+        # gradients that are not bucket views (a caller's own backward): cat, reduce, copy back
+        grads = [p.grad for p in params]
+        flat = torch.cat([g.reshape(-1) for g in grads] + ([kl.reshape(1)] if kl is not None else []))
         dist.all_reduce(flat)
         flat /= self.world_size
         off = 0
@@ -207,6 +242,7 @@ class PPO:
             n = g.numel()
             g.copy_(flat[off:off + n].view_as(g))
             off += n
+        return flat[-1] if kl is not None else None
 
     def _reference_loss(self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
                         returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch,
@@ -237,12 +273,13 @@ class PPO:
         sigma_batch = self.actor_critic.action_std
         entropy_batch = self.actor_critic.entropy
 
+        self._kl_mean = None  # the adaptive-LR input; _minibatch_step applies it
         if self.desired_kl is not None and self.schedule == "adaptive":
             with torch.no_grad():
                 kl = torch.sum(torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
                                + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
                                / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
-                self._adapt_lr(torch.mean(kl))
+                self._kl_mean = torch.mean(kl)
 
         ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
         surrogate = -torch.squeeze(advantages_batch) * ratio
@@ -261,11 +298,9 @@ class PPO:
         return loss, surrogate_loss, value_loss
 
     def _adapt_lr(self, kl_mean):
-        """KL-adaptive learning rate (rsl_rl v1.0.2), on device: no host sync."""
+        """KL-adaptive learning rate (rsl_rl v1.0.2), on device: no host sync.  kl_mean is
+        already the ranks' mean at world > 1 (it rides in the gradient bucket)."""
         with torch.no_grad():
-            if self.world_size > 1:
-                dist.all_reduce(kl_mean)
-                kl_mean = kl_mean / self.world_size
             lr = self._lr
             new_lr = torch.where(kl_mean > self.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
                                  torch.where((kl_mean < self.desired_kl / 2.0) & (kl_mean > 0.0),
@@ -298,6 +333,7 @@ class PPO:
                                             self.use_clipped_value_loss, self.value_loss_coef, self.entropy_coef)
             surrogate_loss, value_loss = stats[0], stats[1]
             adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+            kl_mean = None
             if self.world_size == 1 and self._lr_is_tensor and self._diag is None:
                 # the logged losses and the adaptive LR in one launch (pmlp_loss_bookkeeping)
                 mfma_mlp._ok(mfma_mlp.load().pmlp_loss_bookkeeping(
@@ -306,19 +342,30 @@ class PPO:
                     "pmlp_loss_bookkeeping")
                 acc = None
             elif adaptive:
-                self._adapt_lr(stats[2])
+                kl_mean = stats[2]
         else:
             loss, surrogate_loss, value_loss = self._reference_loss(
                 obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
                 old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch)
+            kl_mean = self._kl_mean
 
-        # set_to_none: backward then hands its fresh gradient buffers to .grad (no
-        # zero-fill + accumulate kernels); inside the captured update these are
-        # graph-pool buffers at fixed addresses, which the captured Adam step reads
-        self.optimizer.zero_grad(set_to_none=True)
-        loss.backward()
-        if self.world_size > 1:
-            self._allreduce_grads()
+        if self.world_size == 1:
+            if kl_mean is not None:  # before this step's Adam, as rsl_rl adapts it
+                self._adapt_lr(kl_mean)
+            # set_to_none: backward then hands its fresh gradient buffers to .grad (no
+            # zero-fill + accumulate kernels); inside the captured update these are
+            # graph-pool buffers at fixed addresses, which the captured Adam step reads
+            self.optimizer.zero_grad(set_to_none=True)
+            loss.backward()
+        else:
+            # data-parallel: backward accumulates into the views of one bucket, whose
+            # single all-reduce also carries the KL; the LR then adapts to the ranks' mean
+            # KL, still before this step's Adam
+            self._grad_bucket().zero_()
+            loss.backward()
+            kl_mean = self._allreduce_grads(kl_mean)
+            if kl_mean is not None:
+                self._adapt_lr(kl_mean)
         nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
         self.optimizer.step()
         with torch.no_grad():
@@ -393,24 +440,41 @@ class PPO:
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             graph = torch.cuda.CUDAGraph()
-            try:
-                with torch.cuda.graph(graph, stream=side):
-                    body()
-            except RuntimeError as e:
-                # data-parallel: the gradient all-reduce is captured with the steps; a
-                # collective library that refuses capture must not end the run (nothing
-                # inside a failed capture has executed, so the update simply runs eagerly)
-                if self.world_size == 1:
-                    raise
-                warnings.warn(f"PPO: capturing the update with its all-reduce failed ({e}); updating eagerly")
-                torch.cuda.synchronize(self.device)
-                self.use_graph = False
+            if not self._capture(graph, side, body):
                 body()
                 return self._facc
             torch.cuda.current_stream(self.device).wait_stream(side)
             self._fgraph = graph
         self._fgraph.replay()
         return self._facc
+
+    def _capture(self, graph, stream, body):
+        """Record body() into graph on stream.  A capture that fails (e.g. a collective
+        library that refuses capture of the data-parallel update's all-reduce) must not
+        end the run: nothing inside a failed capture has executed, so the update runs
+        eagerly from then on.  At world > 1 the ranks decide together (an all-reduce of
+        the failure flag after the attempt), so no rank replays a graph while another
+        runs the same collectives eagerly.  Returns True when the graph is usable."""
+        err = None
+        try:
+            with torch.cuda.graph(graph, stream=stream):
+                body()
+        except RuntimeError as e:
+            err = e
+        failed = self._any_rank(err is not None)
+        if failed:
+            warnings.warn(f"PPO: capturing the update failed ({err or 'on another rank'}); updating eagerly")
+            torch.cuda.synchronize(self.device)
+            self.use_graph = False
+        return not failed
+
+    def _any_rank(self, flag):
+        """True on every rank when flag is True on any rank (one all-reduce at world > 1)."""
+        if self.world_size == 1:
+            return bool(flag)
+        t = torch.tensor([1.0 if flag else 0.0], device=self.device)
+        dist.all_reduce(t)
+        return bool(t.item() > 0)
 
     def _update_graphed(self):
         """All num_epochs x num_mini_batches optimizer steps replayed as ONE HIP graph.
@@ -457,8 +521,7 @@ class PPO:
             self._capturing = True
             with torch.cuda.stream(self._side):
                 body()  # warm-up on the capture stream (allocator + autograd state)
-                with torch.cuda.graph(self._graph, stream=self._side):
-                    body()
+                captured = self._capture(self._graph, self._side, body)
             self._capturing = False
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             with torch.no_grad():
@@ -469,6 +532,10 @@ class PPO:
                         if torch.is_tensor(v):
                             v.copy_(snap_o[id(p_)][k])
                 self._lr.copy_(snap_lr)
+            if not captured:
+                self._graph = None
+                body()
+                return self._acc
         if st.advantages.data_ptr() != self._adv_static.data_ptr():
             self._adv_static.copy_(st.advantages)
             st.advantages = self._adv_static

@@ -66,6 +66,7 @@ class Mlp4Job(C.Structure):
 
 
 MAX_JOBS, MAX_GEMM_JOBS = 16, 4
+PMLP_MAX_MIRROR = 8  # include/ppo_mlp.h: bf16 weight copies one Adam launch writes
 MLP4_HIDDEN = ((512, 256, 128), (256, 128, 64))
 
 

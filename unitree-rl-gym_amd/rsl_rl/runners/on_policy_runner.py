@@ -170,6 +170,9 @@ class OnPolicyRunner:
                     graph = self._rollout_graph = _RolloutGraph(self, obs, critic_obs, cur_reward_sum,
                                                                 cur_episode_length)
                 if graph is not None:
+                    fused = getattr(self.alg, "_fused", None)
+                    if fused is not None:  # a load() since the capture: the graph reads the bf16 copies
+                        fused.ensure_weights()
                     obs, critic_obs = graph.replay()
                     if self.log_dir is not None:
                         ep_infos.extend(graph.ep_infos)
@@ -293,6 +296,9 @@ class OnPolicyRunner:
             self.alg._fused.weights_changed = True
         if load_optimizer:
             self.alg.optimizer.load_state_dict(loaded["optimizer_state_dict"])
+            # a captured autograd update reads the previous Adam state tensors: recapture
+            if getattr(self.alg, "_graph", None) is not None:
+                self.alg._graph = None
         self.current_learning_iteration = loaded["iter"]
         return loaded["infos"]
 
