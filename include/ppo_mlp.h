@@ -98,6 +98,10 @@ typedef struct {
     int32_t ldaf, kaf, ldxa, b_kn, sum_col;
 } pmlp_gemm_job;
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
+/* operand staging of pmlp_gemm's k-loop: 1 (default; env PMLP_GLDS) = LDS-DMA into two LDS buffers,
+ * one barrier per k-tile, wherever the shapes allow (whole 64-deep k-tiles); 0 = register staging.
+ * Both compute the same MFMA chain (bitwise equal).  Returns the previous setting. */
+PMLP_API int pmlp_set_gemm_staging(int32_t glds);
 
 /* out[i] = sum_s slab[s*stride + i], i < n (fp32): the split-K combine.
  * bias_out (optional): the slab is [n/cols_in, cols_in]; columns < cols_out go to
@@ -214,23 +218,6 @@ PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, co
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream);
-
-/* Register-chained forward of a 4-layer Linear/ELU MLP (policy inference:
- * PPO.act, the value of compute_returns): out = W3 ELU(W2 ELU(W1 ELU(W0 x + b0)
- * + b1) + b2) + b3 with fp32 x[M,K0] (K0 <= 128), fp32 weights W0[H0,K0],
- * W1[H1,H0], W2[H2,H1], W3[NO,H2] (NO <= 32; rows 16-byte aligned for l >= 1),
- * fp32 out[M,NO].  bf16 operands, fp32 accumulation; activations never leave
- * registers.  (H0,H1,H2) in {(512,256,128), (256,128,64)}; up to 2 jobs (actor
- * and critic) share the launch.                                              */
-typedef struct {
-    const float* x;
-    const float* W[4];
-    const float* b[4];
-    float* out;
-    int32_t ldx, K0, ldo, NO;
-} pmlp_mlp4_job;
-PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t M, int32_t H0, int32_t H1,
-                               int32_t H2, void* stream);
 
 /* The same loss for the fused optimizer step (gradient of the loss itself):
  * one pass writes the output gradients straight into the MLP backward's bf16

@@ -224,30 +224,6 @@ def test_fused_rollout_act_and_store_match_reference_semantics():
         alg.act(obs, obs)
 
 
-@pytest.mark.parametrize("rows", [4096, 1000, 32, 7])
-@pytest.mark.parametrize("hidden", [(512, 256, 128), (256, 128, 64)])
-def test_register_chained_mlp_forward_matches_fp32_torch(rows, hidden):
-    """pmlp_mlp4_forward (activations in registers, permuted-k weight operands) vs the
-    same nn.Sequentials in fp32: bf16 rounding only (2e-2 of the output scale)."""
-    from rsl_rl.modules.actor_critic import mlp, get_activation
-    torch.manual_seed(0)
-    nets = [mlp(48, list(hidden), 12, get_activation("elu")).cuda(), mlp(45, list(hidden), 1, get_activation("elu")).cuda()]
-    for net in nets:  # larger biases/weights than the init: exercise ELU's negative branch
-        for m in net:
-            if isinstance(m, torch.nn.Linear):
-                m.bias.data.normal_(0, 0.5)
-    assert mfma_mlp.mlp4_supported(nets[:1]) and mfma_mlp.mlp4_supported(nets[1:])
-    xs = [torch.randn(rows, 48, device="cuda"), torch.randn(rows, 45, device="cuda")]
-    outs = [torch.full((rows, 12), float("nan"), device="cuda"), torch.full((rows, 1), float("nan"), device="cuda")]
-    mfma_mlp.mlp4_forward(nets, xs, outs)
-    with torch.no_grad():
-        for net, x, out in zip(nets, xs, outs):
-            ref = net(x)
-            assert torch.isfinite(out).all()
-            err = (out - ref).abs().max() / ref.abs().max()
-            assert err <= 2e-2, float(err)
-
-
 @pytest.mark.parametrize("K,ks", [(24576, 1152), (1000, 320)])
 def test_partial_tn_gemm_matches_transposed_partial_and_fp32(K, ks):
     """Weight-gradient GEMM read from the row-major activations (PARTIAL_TN, LDS-transposed

@@ -370,3 +370,42 @@ def test_two_envs_per_wave_is_bitwise_one_env_per_wave(monkeypatch):
         outs.append(env_arrays(env))
         env.close()
     assert_exact(outs[1], outs[0], STATE + POST, 512, "two envs per wave vs one")
+
+
+# --------------------------------------------------- another robot (plugin) --
+def _register_g1_23dof():
+    """A plugin task on a robot the built-in kernels do not cover: the G1 23-DOF description
+    the reference ships (resources/robots/g1_description/g1_23dof.urdf; the bundled model
+    leggedsim/models/g1_23dof.npz is compiled from it).  Its (23 DOFs, 24 bodies) shape comes
+    from the library's build-time instantiation hook (LGS_EXTRA_SHAPES in csrc/leggedsim.hip)."""
+    import copy
+    from legged_gym.envs.g1.g1_config import G1RoughCfg, G1RoughCfgPPO
+    from legged_gym.envs.g1.g1_env import G1Robot
+    if "g1_23dof" in task_registry.task_classes:
+        return
+    cfg = copy.deepcopy(G1RoughCfg())
+    cfg.asset.file = "{LEGGED_GYM_ROOT_DIR}/resources/robots/g1_description/g1_23dof.urdf"
+    cfg.asset.self_collisions = 1
+    arms = {"waist_yaw_joint": 0.0}
+    for side in ("left", "right"):
+        arms.update({f"{side}_shoulder_pitch_joint": 0.3, f"{side}_shoulder_roll_joint": 0.25 * (1 if side == "left" else -1),
+                     f"{side}_shoulder_yaw_joint": 0.0, f"{side}_elbow_joint": 0.9, f"{side}_wrist_roll_joint": 0.0})
+    cfg.init_state.default_joint_angles = dict(cfg.init_state.default_joint_angles, **arms)
+    cfg.control.stiffness = dict(cfg.control.stiffness, waist=150, shoulder=40, elbow=40, wrist=20)
+    cfg.control.damping = dict(cfg.control.damping, waist=3, shoulder=1, elbow=1, wrist=0.5)
+    cfg.env.num_actions = 23
+    cfg.env.num_observations = 9 + 3 * 23 + 2
+    cfg.env.num_privileged_obs = 12 + 3 * 23 + 2
+    task_registry.register("g1_23dof", G1Robot, cfg, G1RoughCfgPPO())
+
+
+@pytest.mark.parametrize("n", [37, 1024])
+def test_other_robot_shape_registers_and_matches_oracle_bitwise(n):
+    """configs' robots aside: a task on another robot (23 DOFs, 24 bodies, humanoid
+    observations of 80 / 83 entries) registers, steps through the same C ABI and is
+    bit-exact with the oracle; name queries resolve its bodies."""
+    _register_g1_23dof()
+    env, g = warm("g1_23dof", n, steps=6, seed=n)
+    assert env.num_dof == 23 and env.num_bodies == 24 and env.obs_buf.shape == (n, 80)
+    assert env.sim.find_body("torso_link") == env.model.body_names.index("torso_link")
+    fused_vs_oracle(env, g, 2, f"g1_23dof x{n}")

@@ -15,7 +15,9 @@ sys.path.insert(0, os.path.join(HERE, "..", "unitree-rl-gym_amd"))
 
 from leggedsim.model import MODELS_DIR, load_model  # noqa: E402
 
-ROBOTS = ["go2/urdf/go2.urdf", "g1_description/g1_12dof.urdf", "h1/urdf/h1.urdf", "h1_2/h1_2_12dof.urdf"]
+ROBOTS = ["go2/urdf/go2.urdf", "g1_description/g1_12dof.urdf", "h1/urdf/h1.urdf", "h1_2/h1_2_12dof.urdf",
+          # another robot the reference ships, for the plugin-task test of the build-time shape hook
+          "g1_description/g1_23dof.urdf"]
 
 
 def main(root):

@@ -2023,16 +2023,35 @@ struct lgs_sim {
 // row capacity sets the LDS footprint (Y, A): the 32-row variant is the Go2 one.  The
 // chain length CH is the sparsity the Cholesky exploits (l_nz); a tree that is not
 // D/CH equal chains hanging from the base takes the dense (CH = 0) variant.
-enum Variant { V_12_19, V_12_13, V_10_11, V_12_19_48, V_NONE };
+enum Variant { V_12_19, V_12_13, V_10_11, V_12_19_48, V_EXTRA, V_NONE };
+
+// Build-time instantiation hook for other robots: every X(D, B) listed here compiles the
+// 48-row, one-env-per-wave kernels (dense Cholesky) for models with exactly D DOFs and at
+// most B bodies (D <= LGS_MAX_DOFS, B <= LGS_MAX_BODIES).  Add a shape here, or pass
+//   make LGS_EXTRA_SHAPES='X(23,24) X(18,19)'
+// and rebuild; lgs_create_sim then accepts the robot.  The default adds the G1 23-DOF
+// description the reference ships (resources/robots/g1_description/g1_23dof.urdf: 23 DOFs,
+// 24 bodies after fixed-joint collapse).
+#ifndef LGS_EXTRA_SHAPES
+#define LGS_EXTRA_SHAPES X(23, 24)
+#endif
+
+static bool extra_shape(const lgs_sim* s) {
+#define X(D_, B_) if (s->D == D_ && s->B <= B_) return true;
+    LGS_EXTRA_SHAPES
+#undef X
+    return false;
+}
 
 static Variant pick(const lgs_sim* s) {
     if (s->D == 12 && s->B <= 19 && s->rows <= 32) return V_12_19;
     if (s->D == 12 && s->B <= 13) return V_12_13;
     if (s->D == 12 && s->B <= 19) return V_12_19_48;
     if (s->D == 10 && s->B <= 11) return V_10_11;
+    if (extra_shape(s)) return V_EXTRA;
     return V_NONE;
 }
-static int variant_rows(Variant v) { return v == V_12_19 ? 32 : 48; }
+static int variant_rows(Variant v) { return v == V_12_19 ? 32 : 48; }  // (V_EXTRA: 48)
 static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 5 : 3); }
 
 #define LGS_LAUNCH(sim, KERNEL, D_, B_, R_, ...)                                                         \
@@ -2069,6 +2088,52 @@ static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 
         if ((sim)->N <= 4 * 1024) LGS_LAUNCH_48W(sim, KERNEL, D_, B_, 4, __VA_ARGS__);                    \
         else LGS_LAUNCH_48W(sim, KERNEL, D_, B_, 0, __VA_ARGS__);                                         \
     } while (0)
+// the extra shapes' launches (one env per wave, 48 rows, CH = 0)
+template <int D, int B>
+static void ex_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
+                    lgs_env_buffers E, int N, uint32_t step, int mode) {
+    hipLaunchKernelGGL((k_step<D, B, 48, 0, 1, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, tp, E, N, step, mode);
+}
+template <int D, int B>
+static void ex_simulate(const lgs_sim* s, DevModel md, DevSim sp, DevState st, int N) {
+    hipLaunchKernelGGL((k_simulate<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, N);
+}
+template <int D, int B>
+static void ex_fk(const lgs_sim* s, DevModel md, DevState st, int N) {
+    hipLaunchKernelGGL((k_fk<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, st, N);
+}
+template <int D, int B>
+static void ex_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_task_params* tp, lgs_env_buffers E, int N,
+                     uint32_t step, const uint8_t* mask) {
+    hipLaunchKernelGGL((k_reset_all<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, st, tp, E, N, step, mask);
+}
+static int extra_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
+                      lgs_env_buffers E, int N, uint32_t step, int mode) {
+#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_step<D_, B_>(s, md, sp, st, tp, E, N, step, mode); return LGS_OK; }
+    LGS_EXTRA_SHAPES
+#undef X
+    return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
+}
+static int extra_simulate(const lgs_sim* s, DevModel md, DevSim sp, DevState st, int N) {
+#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_simulate<D_, B_>(s, md, sp, st, N); return LGS_OK; }
+    LGS_EXTRA_SHAPES
+#undef X
+    return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
+}
+static int extra_fk(const lgs_sim* s, DevModel md, DevState st, int N) {
+#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_fk<D_, B_>(s, md, st, N); return LGS_OK; }
+    LGS_EXTRA_SHAPES
+#undef X
+    return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
+}
+static int extra_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_task_params* tp, lgs_env_buffers E,
+                       int N, uint32_t step, const uint8_t* mask) {
+#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_reset<D_, B_>(s, md, st, tp, E, N, step, mask); return LGS_OK; }
+    LGS_EXTRA_SHAPES
+#undef X
+    return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
+}
+
 #define LGS_DISPATCH_STEP(sim, KERNEL, ...)                                                               \
     switch (pick(sim)) {                                                                                  \
     case V_12_19:                                                                                         \
@@ -2334,7 +2399,12 @@ LGS_API int lgs_simulate(lgs_sim* s) {
     if (!s || !s->root) return set_err(LGS_ERR_STATE, "lgs_simulate: state not bound");
     if (!s->torques) return set_err(LGS_ERR_STATE, "lgs_simulate: no actuation force set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_simulate, s->md, s->sp, st, s->N);
+    if (pick(s) == V_EXTRA) {
+        const int rc = extra_simulate(s, s->md, s->sp, st, s->N);
+        if (rc != LGS_OK) return rc;
+    } else {
+        LGS_DISPATCH(s, k_simulate, s->md, s->sp, st, s->N);
+    }
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
@@ -2342,7 +2412,12 @@ LGS_API int lgs_simulate(lgs_sim* s) {
 LGS_API int lgs_forward_kinematics(lgs_sim* s) {
     if (!s || !s->root) return set_err(LGS_ERR_STATE, "state not bound");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_fk, s->md, st, s->N);
+    if (pick(s) == V_EXTRA) {
+        const int rc = extra_fk(s, s->md, st, s->N);
+        if (rc != LGS_OK) return rc;
+    } else {
+        LGS_DISPATCH(s, k_fk, s->md, st, s->N);
+    }
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
@@ -2390,7 +2465,12 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     if (!s || !env) return set_err(LGS_ERR_ARG, std::string(what) + ": null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, std::string(what) + ": state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
+    if (pick(s) == V_EXTRA) {
+        const int rc = extra_step(s, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
+        if (rc != LGS_OK) return rc;
+    } else {
+        LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
+    }
     HIP_TRY(hipGetLastError());
     if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
@@ -2424,7 +2504,12 @@ LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_c
     if (!s || !env) return set_err(LGS_ERR_ARG, "null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_reset_all: state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, (const uint8_t*)nullptr);
+    if (pick(s) == V_EXTRA) {
+        const int rc = extra_reset(s, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, nullptr);
+        if (rc != LGS_OK) return rc;
+    } else {
+        LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, (const uint8_t*)nullptr);
+    }
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
@@ -2433,7 +2518,12 @@ LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t*
     if (!s || !env || !env_mask) return set_err(LGS_ERR_ARG, "lgs_reset_idx: null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_reset_idx: state not bound or task not set");
     DevState st = state_of(s);
-    LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, env_mask);
+    if (pick(s) == V_EXTRA) {
+        const int rc = extra_reset(s, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, env_mask);
+        if (rc != LGS_OK) return rc;
+    } else {
+        LGS_DISPATCH(s, k_reset_all, s->md, st, s->task_dev, *env, s->N, (uint32_t)step_counter, env_mask);
+    }
     HIP_TRY(hipGetLastError());
     // extras["episode"] over the reset envs and extras["time_outs"]; no step-counter advance
     hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0,

@@ -102,10 +102,39 @@ __device__ __forceinline__ shortx4 lds_read_tr(const bf16* p) {
 // and staged k-major like PARTIAL_TN's operands (the input gradient reads W[out][in]
 // itself: no transposed weight copy).
 //
-// PF > 1: the k-loop keeps PF k-tiles of global loads in flight (a ring of register
-// stages): a grid of about one block per CU (the split-K weight gradients) is otherwise
-// bound by one load round trip per k-tile.
-template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0, int PF = 1>
+// LDS-DMA (global_load_lds_dwordx4): one wave-instruction writes 64 x 16 B contiguously from
+// a wave-uniform LDS base; the source address is per lane (guide §5 'Async global->LDS copy').
+__device__ __forceinline__ void glds16(const void* src, bf16* lds_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// ds_read_b64_tr_b16 in inline asm (the GL ring): hipcc waits vmcnt(0) before any LDS read
+// it may alias with an LDS-DMA still in flight, which drains the ring every k-step; the
+// ring orders its reads itself (counted vmcnt + barrier) and waits lgkmcnt by hand (gl_wait)
+__device__ __forceinline__ shortx4 lds_read_tr_asm(const bf16* p) {
+    shortx4 v;
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+// k-major GL image: the 64-B chunk permutation of k-row r for R-wide rows
+template <int R>
+__device__ __forceinline__ int gl_swz(int r) { return R == 128 ? (r & 3) : ((r >> 1) & 1); }
+
+// GL = 1: the k-loop stages both operands by LDS-DMA into two LDS buffers (no VGPR staging, no
+// ds_write), one barrier per k-tile: the DMA of k-tile t+1 is issued right after the barrier
+// that retires k-tile t and lands while tile t's MFMAs run.  The images are unpadded and
+// XOR-swizzled on the SOURCE address (the DMA destination is lane-linear; guide rule 21):
+//   rows form  [R][64] (k contiguous, 128-B rows): 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+//              -> conflict-free ds_read_b128 fragment reads;
+//   k-major    [64][R] (R contiguous, 2R-B rows): 64-B chunk c of k-row r at c ^ swz(r)
+//              (R = 128: r & 3; R = 64: (r >> 1) & 1) -> conflict-free ds_read_b64_tr_b16 reads.
+// Needs whole 64-deep k-tiles (K, and the split-K slab, multiples of 64) and, for a k-major
+// operand, R a multiple of the tile (rows-form tiles past M / N read a clamped row instead;
+// those outputs are never stored).  Same MFMA order as GL = 0: bitwise the same results.
+template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0, int GL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (b % 8), each
     // with its own L2; give every XCD a contiguous range of logical tiles, ordered so that
@@ -135,7 +164,6 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     constexpr bool AF32 = (MODE & 1) != 0;
     constexpr bool BKN = TNL || (MODE & 2) != 0;  // B staged from [K][N]
     static_assert(!BKN || PMLP_NBUF == 1, "k-major B stages one k-tile");
-    static_assert(PF == 1 || PMLP_NBUF == 1, "the load ring feeds one LDS stage");
     constexpr int BK = 64, LS = BK + 8;  // LDS row stride (bf16 elements, 144 B)
     constexpr int CPR = BK / 8;          // 16-byte chunks per staged row
     // TN images [BK][BM + 32]: a row stride of 16 (mod 64) dwords puts the four rows of
@@ -150,7 +178,12 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
     constexpr int CS = BN + 8;  // row-major epilogue tile [BM][CS] (bf16)
     constexpr int TS = BM + 8;  // transposed epilogue tile [BN][TS]: 16-B aligned rows, 2-way b64 writes
-    constexpr int STAGE = (ATILE + BTILE) * PMLP_NBUF, CTILE = BM * CS, TTILE = BN * TS;
+    constexpr int GSTAGE = (BM + BN) * BK;  // GL: one unpadded k-tile of both operands (bf16)
+    constexpr int GNS = GL == 2 ? 4 : 2;     // GL: LDS buffers (GL = 2: a ring, 2 k-tiles in flight)
+    static_assert(GL != 2 || GNS == 4, "the ring's vmcnt counts assume 4 buffers");
+    constexpr int STAGE = GL ? GNS * GSTAGE : (ATILE + BTILE) * PMLP_NBUF, CTILE = BM * CS, TTILE = BN * TS;
+    static_assert(!GL || (!AF32 && PMLP_NBUF == 1 && NKS == 4), "GL: bf16 operands, whole k-tiles");
+    static_assert(!GL || ((TNL ? BM : 64) % 64 == 0 && (BKN ? BN : 64) % 64 == 0), "GL k-major tiles: 64 or 128");
     constexpr int SMEM = PART ? STAGE
                               : (STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE));
     __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
@@ -181,7 +214,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) accs[i][t] = 0.f;
 
-    uint4 ra[PF][AL], rb[PF][BL];
+    uint4 ra[1][AL], rb[1][BL];
     auto gload = [&](int p, int k0) {
 #ifdef PMLP_DIAG_NOLOAD
         if (k0 != kb) return;  // diagnostic build: operands of the first k-tile only
@@ -285,10 +318,52 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     // k = 8(l>>5)..+7) = two transposed reads of k rows 8(l>>5) + {0..3, 4..7}
     const int tr_off = 8 * (lane >> 5) + ((lane >> 2) & 3);  // k row within a 16-step
     const int tr_col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    int gstage = 0;  // GL: the LDS buffer of the k-tile being computed
     auto kstep = [&](int s) {
         bf16x8 af[FM], bfr[FN];
         const int ko = s * 16 + (lane >> 5) * 8;
-        if constexpr (TNL) {
+        if constexpr (GL) {
+            const bf16* Ag = smem + gstage * GSTAGE;
+            const bf16* Bg = Ag + BM * BK;
+            const int kr = s * 16 + tr_off;  // k-major: this lane's first k row (the second is +4)
+            auto trd = [](const bf16* p) { return GL == 2 ? lds_read_tr_asm(p) : lds_read_tr(p); };
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                if constexpr (TNL) {
+                    const int ch = (wm * TM + i * 32) >> 5;
+                    const bf16* p0 = Ag + kr * BM + ((ch ^ gl_swz<BM>(kr)) << 5) + tr_col;
+                    const bf16* p1 = Ag + (kr + 4) * BM + ((ch ^ gl_swz<BM>(kr + 4)) << 5) + tr_col;
+                    const shortx4 lo = trd(p0), hi = trd(p1);
+                    af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                } else {
+                    const int r = wm * TM + i * 32 + (lane & 31), c = ko >> 3;
+                    af[i] = *(const bf16x8*)(Ag + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                if constexpr (BKN) {
+                    const int ch = (wn * TN + j * 32) >> 5;
+                    const bf16* p0 = Bg + kr * BN + ((ch ^ gl_swz<BN>(kr)) << 5) + tr_col;
+                    const bf16* p1 = Bg + (kr + 4) * BN + ((ch ^ gl_swz<BN>(kr + 4)) << 5) + tr_col;
+                    const shortx4 lo = trd(p0), hi = trd(p1);
+                    bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                } else {
+                    const int r = wn * TN + j * 32 + (lane & 31), c = ko >> 3;
+                    bfr[j] = *(const bf16x8*)(Bg + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+                }
+            }
+            if constexpr (GL == 2) {  // the asm reads' results: wait here, tied to the fragments
+                static_assert(TNL && BKN && FM <= 2 && FN <= 2, "GL ring: k-major operands, <= 2x2 fragments");
+                if constexpr (FM == 1 && FN == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(bfr[0]));
+                else if constexpr (FM == 2 && FN == 1)
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[0]));
+                else if constexpr (FM == 1 && FN == 2)
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(bfr[0]), "+v"(bfr[1]));
+                else
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[0]), "+v"(bfr[1]));
+            }
+        } else if constexpr (TNL) {
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 const bf16* p = As + (s * 16 + tr_off) * SA + wm * TM + i * 32 + tr_col;
@@ -299,7 +374,9 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 #pragma unroll
             for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(As + (wm * TM + i * 32 + (lane & 31)) * LS + ko);
         }
-        if constexpr (BKN) {
+        if constexpr (GL) {
+            // (read above)
+        } else if constexpr (BKN) {
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 const bf16* p = Bs + (s * 16 + tr_off) * SB + wn * TN + j * 32 + tr_col;
@@ -350,7 +427,61 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         __syncthreads();
     }
 #else
-    if constexpr (PF == 1) {
+    if constexpr (GL) {
+        // DMA issue of one k-tile into LDS buffer st: operand X (rows R0.., ld) in the rows
+        // form [R][64] or the k-major form [64][R]; NW waves share its wave-instructions
+        auto gl_issue = [&](int st, int k0) {
+            bf16* base = smem + st * GSTAGE;
+            auto op = [&](const bf16* X, int ld, int r0, int nrows, bool kmaj, int R, bf16* img) {
+                const int ninst = R * BK * 2 / 1024;  // 1 KiB per wave-instruction
+                for (int q = wid; q < ninst; q += WM * WN) {
+                    const int o = q * 1024 + 16 * lane;  // byte offset of this lane in the image
+                    const bf16* src;
+                    if (kmaj) {
+                        const int rb = 2 * R, kr = o / rb, w = o % rb, c = (w >> 6) ^ (R == 128 ? (kr & 3) : ((kr >> 1) & 1));
+                        src = X + (size_t)(k0 + kr) * ld + r0 + c * 32 + ((w & 63) >> 1);
+                    } else {
+                        const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
+                        src = X + (size_t)min(r0 + r, nrows - 1) * ld + k0 + c * 8;
+                    }
+                    glds16(src, img + __builtin_amdgcn_readfirstlane(q) * 512);
+                }
+            };
+            op(g.A, g.lda, m0, g.M, TNL, BM, base);
+            op(g.B, g.ldb, n0, g.N, BKN, BN, base + BM * BK);
+        };
+        if constexpr (GL == 1) {
+            gl_issue(0, kb);
+            int st = 0;
+            for (int k0 = kb; k0 < ke; k0 += BK) {
+                __syncthreads();  // (vmcnt(0)) this k-tile landed for every wave; the other buffer's reads are done
+                if (k0 + BK < ke) gl_issue(st ^ 1, k0 + BK);
+                gstage = st;
+                compute(k0);
+                st ^= 1;
+            }
+        } else {
+            // GL = 2: a ring of GNS buffers, GNS - 2 k-tiles in flight behind the one computed.
+            // Each wave counts its own DMAs (GW per k-tile): vmcnt(GW * newer tiles) retires this
+            // k-tile's, the raw barrier (no vmcnt(0)) publishes it to every wave, and the
+            // lgkmcnt(0) before it retires this wave's reads of the buffer refilled next.
+            constexpr int GW = (BM + BN) * BK * 2 / 1024 / (WM * WN);
+            static_assert((BM + BN) * BK * 2 / 1024 % (WM * WN) == 0, "GL ring: whole DMAs per wave");
+            const int nt = (ke - kb) / BK;
+            for (int p = 0; p < GNS - 1 && p < nt; ++p) gl_issue(p, kb + p * BK);
+            for (int t = 0; t < nt; ++t) {
+                const int newer = min(GNS - 2, nt - 1 - t);
+                if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GW) : "memory");
+                else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GW) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (t + GNS - 1 < nt) gl_issue((t + GNS - 1) % GNS, kb + (t + GNS - 1) * BK);
+                gstage = t % GNS;
+                compute(0);
+            }
+        }
+    } else {
         gload(0, kb);
         for (int k0 = kb; k0 < ke; k0 += BK) {
             __syncthreads();
@@ -358,23 +489,6 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
             __syncthreads();
             if (k0 + BK < ke) gload(0, k0 + BK);
             compute(k0);
-        }
-    } else {
-#pragma unroll
-        for (int p = 0; p < PF; ++p)
-            if (kb + p * BK < ke) gload(p, kb + p * BK);
-        for (int k0 = kb; k0 < ke; k0 += PF * BK) {
-#pragma unroll
-            for (int p = 0; p < PF; ++p) {
-                const int kt = k0 + p * BK;  // block-uniform
-                if (kt < ke) {
-                    __syncthreads();
-                    lstore(p);
-                    __syncthreads();
-                    if (kt + PF * BK < ke) gload(p, kt + PF * BK);
-                    compute(kt);
-                }
-            }
         }
     }
 #endif
@@ -1545,174 +1659,68 @@ __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ re
     if (i == 0 && draw) *draw += 1;
 }
 
-// ------------------------------------------------ register-chained MLP forward --
-// Policy inference (PPO.act, compute_returns' value): y = W3 ELU(W2 ELU(W1 ELU(W0 x))).
-// A block of 4 waves owns 128 batch rows (32 per wave) and runs ALL layers with the
-// activations kept in registers: computing H^T = W . X^T, the 32x32 accumulator tile
-// of one layer (rows = features, column = batch row on the lane) is directly the B
-// operand of the next layer's MFMA (guide §3 "accumulator tile as the next MFMA's
-// operand"), the weights supplying the matching permuted k order.  The weights are
-// the only stream: 32-row x 128-k chunks (fp32 -> bf16) are staged through a double-
-// buffered LDS tile shared by the 4 waves, the next chunk's global loads in flight
-// while the MFMAs of this one run.  No intermediate HBM traffic.
-struct Mlp4Job {
-    const float* x;
-    const float* W[4];
-    const float* b[4];
-    float* out;
-    int ldx, K0, ldo, NO;
-};
-struct Mlp4Jobs {
-    Mlp4Job j[2];
-};
-
-#define MLP4_WAVES 4
-#define MLP4_KC 128             // k per staged chunk
-#define MLP4_LS (MLP4_KC + 4)   // LDS row stride (bf16): 264 B, == 8 mod 256 -> conflict-free b64 reads
-
-struct Mlp4Stage {
-    float4 v[4];  // 32 rows x 128 k fp32 / 256 threads
-};
-
-// global -> registers: rows n0..n0+31 (< nrows), k k0..k0+127 (< K) of W[., K]
-__device__ __forceinline__ void mlp4_load(Mlp4Stage& st, const float* __restrict__ W, int K, int nrows, int n0,
-                                          int k0) {
-    const int tid = threadIdx.x, row = tid >> 3, c = (tid & 7) * 16;
-    const int n = n0 + row;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = k0 + c + 4 * q;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (n < nrows) {
-            if (k + 3 < K && (K & 3) == 0) {
-                v = *(const float4*)(W + (size_t)n * K + k);
-            } else {
-                const float* w = W + (size_t)n * K;
-                v.x = k < K ? w[k] : 0.f;
-                v.y = k + 1 < K ? w[k + 1] : 0.f;
-                v.z = k + 2 < K ? w[k + 2] : 0.f;
-                v.w = k + 3 < K ? w[k + 3] : 0.f;
-            }
-        }
-        st.v[q] = v;
-    }
-}
-__device__ __forceinline__ void mlp4_store(const Mlp4Stage& st, bf16* __restrict__ tile) {
-    const int tid = threadIdx.x, row = tid >> 3, c = (tid & 7) * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        bf16x4 w;
-        w[0] = (bf16)st.v[q].x; w[1] = (bf16)st.v[q].y; w[2] = (bf16)st.v[q].z; w[3] = (bf16)st.v[q].w;
-        *(bf16x4*)(tile + row * MLP4_LS + c + 4 * q) = w;
-    }
-}
-
-// One layer: operand `xin` (KS k-steps; natural k order for the input layer, the
-// accumulator-permuted order otherwise) -> NT output tiles of 32 features, bias (+ ELU)
-// -> the next layer's operand `xout` (hidden) or out[] (last layer, NO features).
-// W: [NT*32 (rows < nrows valid), K] fp32.  Chunk c = (tile c / CPT, k-chunk c % CPT).
-template <int KS, int NT, bool NATURAL, bool LAST>
-__device__ __forceinline__ void mlp4_layer(const bf16x8 (&xin)[KS], bf16x8 (&xout)[LAST ? 1 : 2 * NT],
-                                           const float* __restrict__ W, const float* __restrict__ bias, int K,
-                                           int nrows, bf16* __restrict__ lds, float* __restrict__ out, int ldo,
-                                           int grow, int M) {
-    constexpr int SPC = MLP4_KC / 16;                 // k-steps per chunk
-    constexpr int CPT = (KS + SPC - 1) / SPC;         // chunks per tile
-    constexpr int NC = NT * CPT;
-    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    Mlp4Stage st;
-    mlp4_load(st, W, K, nrows, 0, 0);
-    floatx16 acc;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const int t = c / CPT, kc = c % CPT;
-        bf16* tile = lds + (c & 1) * 32 * MLP4_LS;
-        mlp4_store(st, tile);
-        __syncthreads();
-        if (c + 1 < NC) mlp4_load(st, W, K, nrows, 32 * ((c + 1) / CPT), MLP4_KC * ((c + 1) % CPT));
-        if (kc == 0) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) acc[u] = 0.f;
-        }
-#pragma unroll
-        for (int ss = 0; ss < SPC; ++ss) {
-            const int s = kc * SPC + ss;
-            if (s < KS) {
-                bf16x8 wa;
-                const bf16* wrow = tile + r * MLP4_LS + 16 * ss;
-                if (NATURAL) {
-                    wa = *(const bf16x8*)(wrow + 8 * h);
-                } else {
-                    const bf16x4 lo = *(const bf16x4*)(wrow + 4 * h);
-                    const bf16x4 hi = *(const bf16x4*)(wrow + 8 + 4 * h);
-                    wa[0] = lo[0]; wa[1] = lo[1]; wa[2] = lo[2]; wa[3] = lo[3];
-                    wa[4] = hi[0]; wa[5] = hi[1]; wa[6] = hi[2]; wa[7] = hi[3];
-                }
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, xin[s], acc, 0, 0, 0);
-            }
-        }
-        if (kc == CPT - 1) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int f = 32 * t + (u & 3) + 8 * (u >> 2) + 4 * h;
-                if (LAST) {
-                    if (f < nrows && grow < M) out[(size_t)grow * ldo + f] = acc[u] + bias[f];
-                } else {
-                    xout[LAST ? 0 : 2 * t + (u >> 3)][u & 7] = (bf16)elu(acc[u] + bias[f]);
-                }
-            }
-        }
-    }
-}
-
-template <int H0, int H1, int H2>
-__global__ __launch_bounds__(64 * MLP4_WAVES) void k_mlp4_fwd(Mlp4Jobs jobs, int M) {
-    __shared__ __attribute__((aligned(16))) bf16 lds[2 * 32 * MLP4_LS];
-    const Mlp4Job& J = jobs.j[blockIdx.y];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-    const int grow = blockIdx.x * 32 * MLP4_WAVES + 32 * wave + r;
-    // input operand, natural k order: lane (r, h) holds x[grow][16s + 8h + j]  (K0 <= 128)
-    bf16x8 x0[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = 16 * s + 8 * h + j;
-            x0[s][j] = (bf16)((grow < M && k < J.K0) ? J.x[(size_t)grow * J.ldx + k] : 0.f);
-        }
-    bf16x8 x1[H0 / 16];
-    if (J.K0 <= 64) mlp4_layer<4, H0 / 32, true, false>(*(const bf16x8(*)[4])x0, x1, J.W[0], J.b[0], J.K0, H0, lds,
-                                                        nullptr, 0, grow, M);
-    else mlp4_layer<8, H0 / 32, true, false>(x0, x1, J.W[0], J.b[0], J.K0, H0, lds, nullptr, 0, grow, M);
-    __syncthreads();
-    bf16x8 x2[H1 / 16];
-    mlp4_layer<H0 / 16, H1 / 32, false, false>(x1, x2, J.W[1], J.b[1], H0, H1, lds, nullptr, 0, grow, M);
-    __syncthreads();
-    bf16x8 x3[H2 / 16];
-    mlp4_layer<H1 / 16, H2 / 32, false, false>(x2, x3, J.W[2], J.b[2], H1, H2, lds, nullptr, 0, grow, M);
-    __syncthreads();
-    bf16x8 dummy[1];
-    mlp4_layer<H2 / 16, 1, false, true>(x3, dummy, J.W[3], J.b[3], H2, J.NO, lds, J.out, J.ldo, grow, M);
-}
-
-#ifndef PMLP_PF_TN_DEFAULT
-#define PMLP_PF_TN_DEFAULT 1
-#endif
-#ifndef PMLP_PF_DX_DEFAULT
-#define PMLP_PF_DX_DEFAULT 1
-#endif
-#ifndef PMLP_PF_FWD_DEFAULT
-#define PMLP_PF_FWD_DEFAULT 1
-#endif
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v ? atoi(v) : dflt;
+}
+
+// GEMM operand staging: 1 = LDS-DMA (GL) where the shapes allow it, 0 = register staging only
+// (PMLP_GLDS, or pmlp_set_gemm_staging for in-process A/B)
+static int g_glds = -1;
+static int glds_on() {
+    if (g_glds < 0) g_glds = env_int("PMLP_GLDS", 1);
+    return g_glds;
+}
+
+// every job of the batch fits the GL k-loop at this tile (whole 64-deep k-tiles; k-major
+// operands whole tiles wide)
+template <int BM, int BN>
+static bool gl_fits(int epi, int mode, const GemmBatch& gb, int njobs) {
+    if (!glds_on() || (mode & 1)) return false;
+    const bool tnl = epi == PMLP_EPI_PARTIAL_TN, bkn = tnl || (mode & 2);
+    if (glds_on() == 2 && !tnl) return false;  // 2: the LDS-DMA ring, split-K weight gradients only
+    if (glds_on() == 3 && !tnl && epi != PMLP_EPI_BWD_DX) return false;  // 3: + two buffers for BWD_DX
+    if (epi == PMLP_EPI_PARTIAL) return false;
+    if (tnl && (BM % 64 || BM > 128)) return false;
+    if (bkn && (BN % 64 || BN > 128)) return false;
+    for (int i = 0; i < njobs; ++i) {
+        const GemmArgs& g = gb.j[i];
+        if (g.K % 64 || (tnl && g.ksplit % 64)) return false;
+        if (tnl && (g.M % BM || g.lda < g.M)) return false;
+        if (bkn && (g.N % BN || g.ldb < g.N)) return false;
+    }
+    return true;
 }
 
 template <int BM, int BN, int WM, int WN>
 static void launch(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk, hipStream_t st) {
     dim3 grid((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs), block(64 * WM * WN);
     const bool af = (mode & 1) != 0, bkn = (mode & 2) != 0;
+    constexpr bool km_a = BM % 64 == 0 && BM <= 128, km_b = BN % 64 == 0 && BN <= 128;  // k-major GL images
+    if (gl_fits<BM, BN>(epi, mode, gb, njobs)) {
+        switch (epi) {
+        case PMLP_EPI_FWD_HIDDEN: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 0, 1>), grid, block, 0, st, gb); return;
+        case PMLP_EPI_FWD_OUT: hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 1, 4, 0, 1>), grid, block, 0, st, gb); return;
+        case PMLP_EPI_BWD_DX:
+            if (!bkn) {
+                hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 0, 1>), grid, block, 0, st, gb);
+                return;
+            }
+            if constexpr (km_b) {
+                hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2, 1>), grid, block, 0, st, gb);
+                return;
+            }
+            break;
+        case PMLP_EPI_PARTIAL_TN:
+            if constexpr (km_a && km_b) {
+                if (glds_on() >= 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 2>), grid, block, 0, st, gb);
+                else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 1>), grid, block, 0, st, gb);
+                return;
+            }
+            break;
+        default: break;
+        }
+    }
     // one short k-tile: only the k-steps that carry data (K = 48 forward, K = 16 input gradient)
     if (epi == PMLP_EPI_FWD_HIDDEN && maxk <= 48 && maxk > 32) {
         if (af) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 3, 1>), grid, block, 0, st, gb);
@@ -1722,25 +1730,6 @@ static void launch(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, 
     if (epi == PMLP_EPI_BWD_DX && maxk <= 16) {
         if (bkn) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1, 2>), grid, block, 0, st, gb);
         else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 1>), grid, block, 0, st, gb);
-        return;
-    }
-    // load-ring depth per epilogue (PMLP_PF_TN / PMLP_PF_DX / PMLP_PF_FWD, 1..3)
-    static const int pf_tn = env_int("PMLP_PF_TN", PMLP_PF_TN_DEFAULT);
-    static const int pf_dx = env_int("PMLP_PF_DX", PMLP_PF_DX_DEFAULT);
-    static const int pf_fw = env_int("PMLP_PF_FWD", PMLP_PF_FWD_DEFAULT);
-    if (PMLP_NBUF == 1 && epi == PMLP_EPI_PARTIAL_TN && pf_tn > 1) {
-        if (pf_tn == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 2>), grid, block, 0, st, gb);
-        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 4, 4, 0, 3>), grid, block, 0, st, gb);
-        return;
-    }
-    if (PMLP_NBUF == 1 && epi == PMLP_EPI_BWD_DX && bkn && pf_dx > 1) {
-        if (pf_dx == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2, 2>), grid, block, 0, st, gb);
-        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 2, 4, 2, 3>), grid, block, 0, st, gb);
-        return;
-    }
-    if (PMLP_NBUF == 1 && epi == PMLP_EPI_FWD_HIDDEN && !af && pf_fw > 1) {
-        if (pf_fw == 2) hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 0, 2>), grid, block, 0, st, gb);
-        else hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, 0, 4, 0, 3>), grid, block, 0, st, gb);
         return;
     }
     switch (epi) {
@@ -1766,6 +1755,12 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 extern "C" {
 
 PMLP_API const char* pmlp_last_error(void) { return g_err.c_str(); }
+
+PMLP_API int pmlp_set_gemm_staging(int32_t glds) {
+    const int prev = glds_on();
+    g_glds = glds < 0 ? 0 : (glds > 3 ? 3 : glds);
+    return prev;
+}
 
 PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* stream) {
     if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_convert: 1..PMLP_MAX_JOBS jobs");
@@ -1857,29 +1852,10 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         // 128x128 output tiles: 8 waves of 64x32 (accumulators in 32 VGPRs, no AGPRs:
         // 4 waves/SIMD resident instead of 3) for the epilogue-heavy short-K GEMMs; 4 waves
         // of 64x64 for the forward GEMMs with a long k-loop (K >= 256), where the 64x64
-        // wave tile's operand reuse wins (tools/gpu_tile_ab.sh: -18 us per optimizer step).
-        // PMLP_BIG_TILE=0/1/2 forces 4 waves / 8 waves 64x32 / 8 waves 32x64.
-        static const int big = [] {
-            const char* v = getenv("PMLP_BIG_TILE");
-            return v ? atoi(v) : -1;
-        }();
-        // 128 x 256 tiles (8 waves of 64x64) for the widest GEMMs (PMLP_WIDE_TILE=1): the A
-        // operand is re-read by half as many column tiles -- measured SLOWER (forward N = 256
-        // 30 -> 39 us, input gradient N = 512 39 -> 47 us: the re-reads hit L2, and 67 KB of
-        // LDS per block halves the resident blocks), so off by default
-        static const int wide_env = [] {
-            const char* v = getenv("PMLP_WIDE_TILE");
-            return v ? atoi(v) : 0;
-        }();
-        const bool wide = wide_env > 0 && big < 0 &&
-                          ((epi == PMLP_EPI_FWD_HIDDEN && maxn >= 256 && maxk >= 256) ||
-                           (epi == PMLP_EPI_BWD_DX && maxn >= 512) ||
-                           (epi == PMLP_EPI_PARTIAL_TN && maxn >= 256 && maxm >= 128));
-        const int pick = big >= 0 ? big : ((epi == PMLP_EPI_FWD_HIDDEN && maxk >= 256) ? 0 : 1);
-        if (wide) launch<128, 256, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
-        else if (pick == 1) launch<128, 128, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
-        else if (pick == 2) launch<128, 128, 4, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
-        else launch<128, 128, 2, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+        // wave tile's operand reuse wins (-18 us per optimizer step).  (Measured and dropped,
+        // 128 x 256 tiles, other 128 x 128 wave splits, register load rings.)
+        if (epi == PMLP_EPI_FWD_HIDDEN && maxk >= 256) launch<128, 128, 2, 2>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
+        else launch<128, 128, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
     }
     PMLP_CHECK_LAUNCH("pmlp_gemm");
     return 0;
@@ -2139,28 +2115,6 @@ PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const u
     return 0;
 }
 
-PMLP_API int pmlp_mlp4_forward(int32_t njobs, const pmlp_mlp4_job* jobs, int32_t M, int32_t H0, int32_t H1,
-                               int32_t H2, void* stream) {
-    if (njobs <= 0 || njobs > 2 || !jobs || M <= 0) return fail(-1, "pmlp_mlp4_forward: 1..2 jobs, M > 0");
-    Mlp4Jobs mj{};
-    for (int i = 0; i < njobs; ++i) {
-        const pmlp_mlp4_job& J = jobs[i];
-        bool ok = J.x && J.out && J.K0 > 0 && J.K0 <= 128 && J.ldx >= J.K0 && J.NO > 0 && J.NO <= 32 &&
-                  J.ldo >= J.NO;
-        for (int l = 0; l < 4; ++l) ok = ok && J.W[l] && J.b[l];
-        if (!ok) return fail(-1, "pmlp_mlp4_forward: bad job " + std::to_string(i));
-        mj.j[i] = Mlp4Job{J.x, {J.W[0], J.W[1], J.W[2], J.W[3]}, {J.b[0], J.b[1], J.b[2], J.b[3]}, J.out,
-                          J.ldx, J.K0, J.ldo, J.NO};
-    }
-    const int rows = 32 * MLP4_WAVES;
-    dim3 grid((M + rows - 1) / rows, njobs), block(64 * MLP4_WAVES);
-    hipStream_t st = (hipStream_t)stream;
-    if (H0 == 512 && H1 == 256 && H2 == 128) hipLaunchKernelGGL((k_mlp4_fwd<512, 256, 128>), grid, block, 0, st, mj, M);
-    else if (H0 == 256 && H1 == 128 && H2 == 64) hipLaunchKernelGGL((k_mlp4_fwd<256, 128, 64>), grid, block, 0, st, mj, M);
-    else return fail(-1, "pmlp_mlp4_forward: hidden sizes (512,256,128) or (256,128,64)");
-    PMLP_CHECK_LAUNCH("pmlp_mlp4_forward");
-    return 0;
-}
 
 PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A) { return ((M + 63) / 64) * (3 + A); }
 
@@ -2178,11 +2132,7 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
     const int nb = (M + 63) / 64;
-    static const bool quad = [] {
-        const char* e = getenv("PMLP_LOSS_QUAD");  // 0: the one-lane-per-row kernel (A/B)
-        return !(e && e[0] == '0');
-    }();
-    if (quad && A % 4 == 0 && A <= 16 && Ap <= 16 && Ap % 4 == 0)
+    if (A % 4 == 0 && A <= 16 && Ap <= 16 && Ap % 4 == 0)
         hipLaunchKernelGGL(k_ppo_loss_step_q, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, o);
     else if (A <= 16 && Ap % 8 == 0)
         hipLaunchKernelGGL(k_ppo_loss_step_reg<16>, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);

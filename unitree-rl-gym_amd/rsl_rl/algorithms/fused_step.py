@@ -85,10 +85,6 @@ class FusedPPOStep:
         for p in params:
             self._offset[id(p)] = off
             off += p.numel()
-        self._side = None  # side stream of the weight-gradient GEMMs (run())
-        # dW_l beside dX_l on a second stream: measured SLOWER (one update 6.44 -> 6.77 ms,
-        # tools/probes/update_env_ab.py), the two latency-bound GEMMs contend; off by default
-        self.dw_side_stream = os.environ.get("PMLP_DW_SIDE_STREAM", "0") == "1"
         # the bf16 weight copies (wb) are the GEMM operands of the rollout and the update;
         # every fused Adam step rewrites them (pmlp_adam_mirror).  weights_changed: they lag
         # the fp32 weights (construction, a checkpoint load, any update outside this path)
@@ -252,15 +248,10 @@ class FusedPPOStep:
                                       self.dz_out[0].shape[1], P(self.dz_out[1]), mm._p(self.dzt_out[1]),
                                       self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
-        #    dW_l (split-K slabs) and dX_l both read only dz_l; with dw_side_stream dW_l runs
-        #    on a second stream (a fork/join inside the captured graph) that rejoins before
-        #    the slab combine.
+        #    (dW_l beside dX_l on a second stream measured slower: the two latency-bound
+        #    GEMMs contend)
         dz, dzt = list(self.dz_out), list(self.dzt_out)
         red, copies = [], []
-        main = torch.cuda.current_stream(self.dev)
-        if self._side is None and self.dw_side_stream:
-            self._side = torch.cuda.Stream(self.dev)
-        side = self._side if self.dw_side_stream else main
         for l in range(L - 1, -1, -1):
             gj = []
             for n in range(2):
@@ -278,9 +269,7 @@ class FusedPPOStep:
                             kp + 8, kp))
                 if self.dw_stage[l][n] is not None:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
-            side.wait_stream(main)  # dz_l is ready
-            with torch.cuda.stream(side):
-                mm._gemm(mm.EPI_PARTIAL_TN if tn else mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
+            mm._gemm(mm.EPI_PARTIAL_TN if tn else mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
             if l > 0:
                 gj = []
                 for n in range(2):
@@ -291,7 +280,6 @@ class FusedPPOStep:
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
                 dzt = [self.dzt[n][l] for n in range(2)]
-        main.wait_stream(side)  # every slab written
         mm._reduce(red)
         for dst, srcv in copies:
             dst.copy_(srcv)
@@ -334,10 +322,6 @@ class FusedRollout:
         self.out = [torch.empty(N, ls[-1].out_features, device=dev) for ls in lins]
         self.actions = torch.empty(N, lins[0][-1].out_features, device=dev)
         self.draw = torch.zeros((), dtype=torch.int64, device=dev)
-        # The register-chained forward (pmlp_mlp4_forward) is exact to bf16 rounding but
-        # measured slower here (164 vs ~50 us at 4096 rows: one 16 KB weight chunk in
-        # flight per block leaves it L2-latency-bound), so the GEMM path stays the default.
-        self.regs = False
         self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
 
     def usable(self, obs, cobs, storage):
@@ -355,8 +339,6 @@ class FusedRollout:
         the first reading the fp32 observations itself.  The bf16 weight copies are current
         (the fused Adam step writes them); they are reconverted only when they lag."""
         f, N = self.f, self.N
-        if self.regs:  # one launch, activations in registers
-            return mm.mlp4_forward([self.f.ac.actor, self.f.ac.critic], [obs, cobs], self.out)
         f.ensure_weights()
         xs = [obs, cobs]
         for l in range(f.L):

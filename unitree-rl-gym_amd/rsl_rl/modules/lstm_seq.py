@@ -54,7 +54,7 @@ def _gx(x, w_ih, b_ih, b_hh):
     return torch.addmm(b_ih + b_hh, x.reshape(T * B, I), w_ih.t()).view(T, B, w_ih.shape[0])
 
 
-_ROWS_CHUNK = int(os.environ.get("LSTM_ROWS_CHUNK", "1024"))  # (A/B knob: tools/gpu_chunk_ab.sh)
+_ROWS_CHUNK = int(os.environ.get("LSTM_ROWS_CHUNK", "1024"))  # (A/B knob)
 
 
 def _rows_tn(g, x, chunk=None):

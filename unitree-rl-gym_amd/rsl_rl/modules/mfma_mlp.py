@@ -60,14 +60,8 @@ class RowsumJob(C.Structure):
                 ("ld", C.c_int32)]
 
 
-class Mlp4Job(C.Structure):
-    _fields_ = [("x", C.c_void_p), ("W", C.c_void_p * 4), ("b", C.c_void_p * 4), ("out", C.c_void_p),
-                ("ldx", C.c_int32), ("K0", C.c_int32), ("ldo", C.c_int32), ("NO", C.c_int32)]
-
-
 MAX_JOBS, MAX_GEMM_JOBS = 16, 4
 PMLP_MAX_MIRROR = 8  # include/ppo_mlp.h: bf16 weight copies one Adam launch writes
-MLP4_HIDDEN = ((512, 256, 128), (256, 128, 64))
 
 
 def load():
@@ -100,7 +94,6 @@ def load():
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
         L.pmlp_gae_local.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp, vp]
         L.pmlp_adv_normalize.argtypes = [vp, i64, vp, vp]
-        L.pmlp_mlp4_forward.argtypes = [i32, C.POINTER(Mlp4Job), i32, i32, i32, i32, vp]
         L.pmlp_ppo_loss_step_parts.argtypes = [i32, i32]
         L.pmlp_ppo_loss_step_parts.restype = i32
         L.pmlp_ppo_loss_step.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, i32, vp, vp,
@@ -207,15 +200,13 @@ def _tiles(M, N):
         bm, bn = 128, 32
     elif N <= 64:
         bm, bn = 128, 64
-    elif N >= 256 and os.environ.get("PMLP_WIDE_TILE", "0") == "1":  # (the weight gradient's wide tiles)
-        bm, bn = 128, 256
     else:
         bm, bn = 128, 128
     return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
 
 
 # ~128 workgroups per weight-gradient job: fewer slabs than 256 cut the slab combine
-# 16.8 -> 11.6 us per optimizer step at equal GEMM time (tools/gpu_update_ab.sh)
+# 16.8 -> 11.6 us per optimizer step at equal GEMM time
 _KS_TARGET = int(os.environ.get("PMLP_KSPLIT_TARGET", "128"))  # (A/B knobs of the split-K heuristic)
 _KS_BUDGET = int(os.environ.get("PMLP_KSPLIT_BUDGET_MB", "12")) << 20
 
@@ -349,38 +340,6 @@ class _MfmaMLPsFn(torch.autograd.Function):
         ctx.acts = ctx.acts_t = ctx.wt = None
         flat = [g for n in range(nnets) for g in grads[n]]
         return (None, None) + (None,) * nnets + tuple(flat)
-
-
-def mlp4_supported(seqs):
-    """Same-shape 4-layer Linear/ELU nets the register-chained forward handles."""
-    hs = None
-    for seq in seqs:
-        if not supported(seq):
-            return False
-        lins = [m for m in seq if isinstance(m, nn.Linear)]
-        if len(lins) != 4 or lins[0].in_features > 128 or lins[3].out_features > 32:
-            return False
-        h = tuple(lin.out_features for lin in lins[:3])
-        if h not in MLP4_HIDDEN or (hs is not None and h != hs):
-            return False
-        hs = h
-    return True
-
-
-def mlp4_forward(seqs, xs, outs):
-    """outs[i] = seqs[i](xs[i]) by the register-chained kernel (pmlp_mlp4_forward): one
-    launch for up to two nets on the same rows; no autograd (inference)."""
-    jobs = []
-    M = xs[0].shape[0]
-    for seq, x, out in zip(seqs, xs, outs):
-        lins = [m for m in seq if isinstance(m, nn.Linear)]
-        W = (C.c_void_p * 4)(*[_p(lin.weight) for lin in lins])
-        b = (C.c_void_p * 4)(*[_p(lin.bias) for lin in lins])
-        jobs.append(Mlp4Job(_p(x), W, b, _p(out), x.stride(0), x.shape[1], out.stride(0), out.shape[1]))
-    h = [m.out_features for m in seqs[0] if isinstance(m, nn.Linear)][:3]
-    arr = (Mlp4Job * len(jobs))(*jobs)
-    _ok(load().pmlp_mlp4_forward(len(jobs), arr, M, h[0], h[1], h[2], _stream()), "pmlp_mlp4_forward")
-    return outs
 
 
 def usable(seq, x):
