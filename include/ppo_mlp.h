@@ -219,6 +219,32 @@ PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const u
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream);
 
+/* The whole forward of 4-layer Linear/ELU MLPs (rsl_rl's actor and critic) in ONE launch
+ * (PPO.act's policy inference, the update's forward): per job
+ *   y0 = ELU(x W0^T + b0), y1 = ELU(y0 W1^T + b1), y2 = ELU(y1 W2^T + b2), out = y2 W3^T + b3
+ * with x fp32 (row m = x[rows ? rows[m] : m], columns >= kx read as 0, converted to bf16),
+ * bf16 W[l] = [N[l], K_l] (K_0 = K0, K_l = N[l-1]), fp32 b and out; the activations stay on
+ * chip (LDS) between layers.  Optional stores: xa = the bf16 input rows [M, K0] and y[l] = the
+ * bf16 hidden outputs (the backward's operands).  Bitwise equal to the per-layer pmlp_gemm
+ * forward (FWD_HIDDEN x3 with the af operand form, FWD_OUT).  Limits: K0 a multiple of 16,
+ * <= 64; N0, N2 <= 512 and N1 <= 256, multiples of 32; N3 <= 32; 1..2 jobs.              */
+typedef struct {
+    const float* x;
+    const int64_t* rows;
+    int32_t ldx, kx;
+    pmlp_bf16* xa;
+    int32_t ldxa;
+    const pmlp_bf16* W[4];
+    const float* b[4];
+    int32_t N[4];
+    int32_t K0;
+    pmlp_bf16* y[3];
+    int32_t ldy[3];
+    float* out;
+    int32_t ldo;
+} pmlp_mlp_fwd_job;
+PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream);
+
 /* The same loss for the fused optimizer step (gradient of the loss itself):
  * one pass writes the output gradients straight into the MLP backward's bf16
  * operands, dmu[M,Ap] + dmu_t[Ap,M] and dvalue[M,Vp] + dvalue_t[Vp,M]

@@ -466,3 +466,51 @@ def test_load_between_learn_calls_reaches_the_captured_rollout(tmp_path):
     with torch.no_grad():
         mu = want_actor(st.observations[:4].reshape(-1, st.observations.shape[-1]))
     torch.testing.assert_close(st.mu[:4].reshape(mu.shape), mu, rtol=0.05, atol=0.05)  # bf16 GEMMs
+
+
+@pytest.mark.parametrize("M,rows", [(24576, True), (4096, False), (1000, True), (37, False)])
+def test_fused_mlp_forward_is_bitwise_the_per_layer_gemms(M, rows):
+    """pmlp_mlp_forward (both nets' 4 layers in one launch, activations in LDS) == the
+    per-layer pmlp_gemm forward (af gather/convert, FWD_HIDDEN x3, FWD_OUT) bitwise: the
+    converted input rows, every hidden output and both outputs; ragged M included."""
+    torch.manual_seed(0)
+    N, T, O, A = 1024, 24, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), num_learning_epochs=1,
+              num_mini_batches=1, device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    f = alg._fused
+    assert f.fused_fwd
+    f.ensure_weights()
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = 2.0 * torch.randn(T * N, O, device="cuda", generator=g)
+    idx = torch.randperm(T * N, device="cuda", generator=g)[:M] if rows else None
+    outs = {}
+    for fused in (True, False):
+        y = [[torch.full((M, lin.out_features), float("nan"), dtype=torch.bfloat16, device="cuda") for lin in ls[:-1]]
+             for ls in f.lins]
+        out = [torch.full((M, ls[-1].out_features), float("nan"), device="cuda") for ls in f.lins]
+        xa = torch.full((M, f.k0p[0]), float("nan"), dtype=torch.bfloat16, device="cuda")
+        if fused:
+            mfma_mlp.mlp_forward([dict(x=x, kx=O, rows=idx, xa=xa if n == 0 else None, K0=f.k0p[n], W=f.wb[n],
+                                       b=[lin.bias.detach() for lin in f.lins[n]],
+                                       N=[lin.out_features for lin in f.lins[n]], y=y[n], out=out[n])
+                                  for n in range(2)], M)
+        else:
+            for l in range(4):
+                last = l == 3
+                gj = []
+                for n in range(2):
+                    lin = f.lins[n][l]
+                    a = dict(af=x, rows=idx, xa=xa if n == 0 else None) if l == 0 else dict(A=y[n][l - 1])
+                    o = dict(cf=out[n]) if last else dict(cb=y[n][l])
+                    gj.append(dict(B=f.wb[n][l], M=M, N=lin.out_features, K=f.k0p[n] if l == 0 else lin.in_features,
+                                   bias=lin.bias.detach(), **a, **o))
+                mfma_mlp._gemm(mfma_mlp.EPI_FWD_OUT if last else mfma_mlp.EPI_FWD_HIDDEN, gj)
+        torch.cuda.synchronize()
+        outs[fused] = (xa, y, out)
+    (xa1, y1, o1), (xa0, y0, o0) = outs[True], outs[False]
+    assert torch.equal(xa1, xa0)
+    for n in range(2):
+        for a, b in zip(y1[n], y0[n]):
+            assert torch.equal(a, b)
+        assert torch.equal(o1[n], o0[n])

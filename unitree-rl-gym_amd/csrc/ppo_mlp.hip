@@ -1425,6 +1425,164 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
     }
 }
 
+// ------------------------------------------------------------ fused MLP forward --
+// The whole forward of a 4-layer Linear/ELU MLP (rsl_rl's actor or critic: K0 -> H0 ->
+// H1 -> H2 -> N3) in ONE launch: a workgroup of 8 waves owns R mini-batch rows and keeps
+// their activations in LDS from layer to layer; only the weights stream (bf16 W[out,in],
+// L2-resident), straight into registers as MFMA B fragments.  The hidden outputs are still
+// stored (bf16, row-major) when the backward needs them, by 16-byte copies out of LDS.
+// Per output element the MFMA chain (v_mfma_f32_32x32x16_bf16, k ascending in steps of
+// 16), the bias + ELU epilogue and the bf16 roundings are those of the per-layer GEMMs
+// (k_gemm_nt): the result is bitwise the same.
+#define FMLP_MAX_H0 512
+#define FMLP_MAX_H1 256
+#define FMLP_THREADS 512
+
+struct FmlpJob {
+    const float* x;         // fp32 input rows: row m of the batch is x[rows ? rows[m] : m]
+    const int64_t* rows;
+    int ldx, kx;            // x row stride; real input width (columns >= kx read as 0)
+    bf16* xa;               // optional: the converted bf16 input rows [M, K0] (ldxa)
+    int ldxa;
+    const bf16* W[4];       // W[l] = [N[l], K_l] bf16, ld K_l (K_0 = K0, K_l = N[l-1])
+    const float* b[4];
+    int N[4];
+    int K0;                 // padded input width, a multiple of 16, <= 64
+    bf16* y[3];             // optional hidden outputs [M, N[l]] (ld ldy[l])
+    int ldy[3];
+    float* out;             // fp32 [M, N[3]] (ld ldo)
+    int ldo;
+};
+struct FmlpJobs {
+    FmlpJob j[2];
+    int njobs;
+};
+
+// One layer: D[R, N] = act(A[R, K] . W[N, K]^T + b), A in LDS (ld lda); wave w takes the
+// 32-column tiles w, w + 8, ...; every row tile of the workgroup per column tile, so a
+// B fragment (one 16-byte load per lane per k-step) feeds RT MFMAs.
+template <int R, bool LAST>
+__device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const bf16* __restrict__ W,
+                                           const float* __restrict__ bias, int N, bf16* D, int ldd,
+                                           float* __restrict__ out, int ldo, int r0, int M) {
+    constexpr int RT = R / 32;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nct = (N + 31) >> 5, ks = K >> 4;
+    for (int ct = wid; ct < nct; ct += FMLP_THREADS / 64) {
+        floatx16 acc[RT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) acc[i][t] = 0.f;
+        const int n = ct * 32 + (lane & 31);
+        const bool nv = n < N;
+        const bf16* wrow = W + (size_t)(nv ? n : 0) * K + 8 * (lane >> 5);
+        const bf16* arow = A + (lane & 31) * lda + 8 * (lane >> 5);
+        // B fragments in groups of FG k-steps, the next group's loads in flight while this
+        // group's MFMAs run (k ascending, as the per-layer GEMM)
+        constexpr int FG = 4;
+        bf16x8 bq[FG], bn[FG];
+        auto loadg = [&](int s0, bf16x8(&b)[FG]) {
+#pragma unroll
+            for (int u = 0; u < FG; ++u) {
+                if (nv && s0 + u < ks) {
+                    b[u] = *(const bf16x8*)(wrow + (s0 + u) * 16);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) b[u][e] = (bf16)0.f;
+                }
+            }
+        };
+        loadg(0, bq);
+        for (int s0 = 0; s0 < ks; s0 += FG) {
+            if (s0 + FG < ks) loadg(s0 + FG, bn);
+#pragma unroll
+            for (int u = 0; u < FG; ++u) {
+                if (s0 + u < ks) {
+#pragma unroll
+                    for (int i = 0; i < RT; ++i) {
+                        const bf16x8 af = *(const bf16x8*)(arow + i * 32 * lda + (s0 + u) * 16);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq[u], acc[i], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < FG; ++u) bq[u] = bn[u];
+        }
+        if (!nv) continue;
+        const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int r = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * (lane >> 5);
+                if constexpr (LAST) {
+                    if (r0 + r < M) out[(size_t)(r0 + r) * ldo + n] = acc[i][t] + bv;
+                } else {
+                    D[r * ldd + n] = (bf16)elu(acc[i][t] + bv);
+                }
+            }
+    }
+}
+
+// copy an LDS activation tile [R, N] (ld lds_ld) to the global rows r0.. of y (ld ldy)
+template <int R>
+__device__ __forceinline__ void fmlp_store(const bf16* D, int lds_ld, int N, bf16* y, int ldy, int r0, int M) {
+    if (!y) return;
+    const int cpr = N >> 3;
+    for (int i = threadIdx.x; i < R * cpr; i += FMLP_THREADS) {
+        const int r = i / cpr, c = (i - r * cpr) * 8;
+        if (r0 + r < M) *(uint4*)(y + (size_t)(r0 + r) * ldy + c) = *(const uint4*)(D + r * lds_ld + c);
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) {
+    // y0 (then y2) and x (then y1); row strides 8 elements past the width: ds_read_b128
+    // fragment reads of 32 consecutive rows hit 4-bank groups 4 apart (conflict-free)
+    constexpr int LD0 = FMLP_MAX_H0 + 8, LD1 = FMLP_MAX_H1 + 8;
+    __shared__ __attribute__((aligned(16))) bf16 Y0[R * LD0];
+    __shared__ __attribute__((aligned(16))) bf16 Y1[R * LD1];
+    const int r0 = blockIdx.x * R;
+    const int jb = gridDim.y > 1 ? blockIdx.y : 0, je = gridDim.y > 1 ? blockIdx.y + 1 : jobs.njobs;
+    for (int jj = jb; jj < je; ++jj) {
+        const FmlpJob& J = jobs.j[jj];
+        // input rows: gathered, fp32 -> bf16 (columns >= kx are 0), into LDS (+ the bf16 copy)
+        const int cpr = J.K0 >> 3;
+        for (int i = threadIdx.x; i < R * cpr; i += FMLP_THREADS) {
+            const int r = i / cpr, k = (i - r * cpr) * 8, m = r0 + r;
+            bf16x8 t;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = (bf16)0.f;
+            if (m < M) {
+                const float* src = J.x + (size_t)(J.rows ? J.rows[m] : (int64_t)m) * J.ldx + k;
+                if (k + 8 <= J.kx) {
+                    const float4 x0 = *(const float4*)src, x1 = *(const float4*)(src + 4);
+                    t[0] = (bf16)x0.x; t[1] = (bf16)x0.y; t[2] = (bf16)x0.z; t[3] = (bf16)x0.w;
+                    t[4] = (bf16)x1.x; t[5] = (bf16)x1.y; t[6] = (bf16)x1.z; t[7] = (bf16)x1.w;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = k + u < J.kx ? (bf16)src[u] : (bf16)0.f;
+                }
+                if (J.xa) *(bf16x8*)(J.xa + (size_t)m * J.ldxa + k) = t;
+            }
+            *(bf16x8*)(Y1 + r * LD1 + k) = t;
+        }
+        __syncthreads();
+        fmlp_layer<R, false>(Y1, LD1, J.K0, J.W[0], J.b[0], J.N[0], Y0, LD0, nullptr, 0, r0, M);
+        __syncthreads();
+        fmlp_store<R>(Y0, LD0, J.N[0], J.y[0], J.ldy[0], r0, M);
+        fmlp_layer<R, false>(Y0, LD0, J.N[0], J.W[1], J.b[1], J.N[1], Y1, LD1, nullptr, 0, r0, M);
+        __syncthreads();
+        fmlp_store<R>(Y1, LD1, J.N[1], J.y[1], J.ldy[1], r0, M);
+        fmlp_layer<R, false>(Y1, LD1, J.N[1], J.W[2], J.b[2], J.N[2], Y0, LD0, nullptr, 0, r0, M);
+        __syncthreads();
+        fmlp_store<R>(Y0, LD0, J.N[2], J.y[2], J.ldy[2], r0, M);
+        fmlp_layer<R, true>(Y0, LD0, J.N[2], J.W[3], J.b[3], J.N[3], nullptr, 0, J.out, J.ldo, r0, M);
+        __syncthreads();  // (the next job restages x over y1)
+    }
+}
+
 // ----------------------------------------------------------------- GAE --
 // RolloutStorage.compute_returns: one thread per env walks t backwards; the
 // advantage sums for the normalisation go to per-block fp64 partials.
@@ -2079,6 +2237,45 @@ PMLP_API int pmlp_adv_normalize(float* advantages, int64_t n, const double* mome
     hipLaunchKernelGGL(k_adv_norm, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, advantages, n,
                        (const double*)nullptr, 0, moments);
     PMLP_CHECK_LAUNCH("pmlp_adv_normalize");
+    return 0;
+}
+
+PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream) {
+    if (njobs <= 0 || njobs > 2 || !jobs || M <= 0) return fail(-1, "pmlp_mlp_forward: 1..2 jobs, M > 0");
+    FmlpJobs fj{};
+    fj.njobs = njobs;
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_mlp_fwd_job& J = jobs[i];
+        const std::string w = "pmlp_mlp_forward job " + std::to_string(i) + ": ";
+        if (!J.x || J.kx <= 0 || J.ldx < J.kx || J.ldx % 4 || ((uintptr_t)J.x & 15))
+            return fail(-1, w + "x: 0 < kx <= ldx, ldx a multiple of 4, 16-byte aligned");
+        if (J.K0 <= 0 || J.K0 % 16 || J.K0 > 64 || J.kx > J.K0)
+            return fail(-1, w + "K0 must be a multiple of 16, kx <= K0 <= 64");
+        if (J.xa && (J.ldxa < J.K0 || J.ldxa % 8 || !al16(J.xa))) return fail(-1, w + "xa: ldxa >= K0, a multiple of 8");
+        const int lim[3] = {FMLP_MAX_H0, FMLP_MAX_H1, FMLP_MAX_H0};
+        for (int l = 0; l < 4; ++l) {
+            if (!J.W[l] || !al16(J.W[l])) return fail(-1, w + "null or unaligned weight");
+            if (l < 3 && (J.N[l] <= 0 || J.N[l] % 32 || J.N[l] > lim[l]))
+                return fail(-1, w + "hidden widths: multiples of 32, <= 512 / 256 / 512");
+            if (l < 3 && J.y[l] && (J.ldy[l] < J.N[l] || J.ldy[l] % 8 || !al16(J.y[l])))
+                return fail(-1, w + "y: ld >= N, a multiple of 8, 16-byte aligned");
+        }
+        if (J.N[3] <= 0 || J.N[3] > 32 || !J.out || J.ldo < J.N[3]) return fail(-1, w + "output: 0 < N3 <= 32, ldo >= N3");
+        FmlpJob& f = fj.j[i];
+        f.x = J.x; f.rows = J.rows; f.ldx = J.ldx; f.kx = J.kx; f.xa = (bf16*)J.xa; f.ldxa = J.ldxa;
+        for (int l = 0; l < 4; ++l) { f.W[l] = (const bf16*)J.W[l]; f.b[l] = J.b[l]; f.N[l] = J.N[l]; }
+        f.K0 = J.K0;
+        for (int l = 0; l < 3; ++l) { f.y[l] = (bf16*)J.y[l]; f.ldy[l] = J.ldy[l]; }
+        f.out = J.out; f.ldo = J.ldo;
+    }
+    // rows per workgroup: 96 (one 150 KB workgroup per CU, every job in turn) for the update's
+    // mini-batches; 32 with one job per workgroup for the rollout's num_envs rows
+    hipStream_t st = (hipStream_t)stream;
+    if (M >= 96 * 192)
+        hipLaunchKernelGGL(k_mlp_fwd<96>, dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0, st, fj, M);
+    else
+        hipLaunchKernelGGL(k_mlp_fwd<32>, dim3((M + 31) / 32, njobs), dim3(FMLP_THREADS), 0, st, fj, M);
+    PMLP_CHECK_LAUNCH("pmlp_mlp_forward");
     return 0;
 }
 

@@ -96,6 +96,10 @@ class FusedPPOStep:
         self.tn = os.environ.get("PMLP_TN", "1") != "0"
         self.sync_optimizer_state(alg.optimizer)
         self._alloc()
+        # the whole forward of both nets in ONE launch (pmlp_mlp_forward: activations kept on
+        # chip between layers, bitwise the per-layer GEMMs); PMLP_FUSED_FWD=0: per-layer GEMMs
+        self.fused_fwd = os.environ.get("PMLP_FUSED_FWD", "1") != "0" and self.tn and \
+            all(mm.mlp_forward_supported(self.lins[n], self.k0p[n]) for n in range(2))
 
     # ------------------------------------------------------------ buffers --
     def _alloc(self):
@@ -217,7 +221,13 @@ class FusedPPOStep:
         xt = [self.xt[0], self.xt[0] if shared else self.xt[1]]
         fobs = [obs, cobs]
         # 2. forward
-        for l in range(L):
+        if self.fused_fwd:
+            mm.mlp_forward([dict(x=fobs[n], kx=self.lins[n][0].in_features, rows=rows,
+                                 xa=self.xb[n] if (n == 0 or not shared) else None, K0=self.k0p[n],
+                                 W=self.wb[n], b=[lin.bias.detach() for lin in self.lins[n]],
+                                 N=[lin.out_features for lin in self.lins[n]], y=self.y[n], out=self.out[n])
+                            for n in range(2)], M)
+        for l in range(L if not self.fused_fwd else 0):
             last = l == L - 1
             gj = []
             for n in range(2):
@@ -341,6 +351,11 @@ class FusedRollout:
         f, N = self.f, self.N
         f.ensure_weights()
         xs = [obs, cobs]
+        if f.fused_fwd:  # one launch for both nets (pmlp_mlp_forward)
+            mm.mlp_forward([dict(x=xs[n], kx=f.lins[n][0].in_features, K0=f.k0p[n], W=f.wb[n],
+                                 b=[lin.bias.detach() for lin in f.lins[n]],
+                                 N=[lin.out_features for lin in f.lins[n]], out=self.out[n]) for n in range(2)], N)
+            return self.out
         for l in range(f.L):
             last = l == f.L - 1
             gj = []

@@ -60,6 +60,13 @@ class RowsumJob(C.Structure):
                 ("ld", C.c_int32)]
 
 
+class MlpFwdJob(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("rows", C.c_void_p), ("ldx", C.c_int32), ("kx", C.c_int32), ("xa", C.c_void_p),
+                ("ldxa", C.c_int32), ("W", C.c_void_p * 4), ("b", C.c_void_p * 4), ("N", C.c_int32 * 4),
+                ("K0", C.c_int32), ("y", C.c_void_p * 3), ("ldy", C.c_int32 * 3), ("out", C.c_void_p),
+                ("ldo", C.c_int32)]
+
+
 MAX_JOBS, MAX_GEMM_JOBS = 16, 4
 PMLP_MAX_MIRROR = 8  # include/ppo_mlp.h: bf16 weight copies one Adam launch writes
 
@@ -100,6 +107,7 @@ def load():
                                                      i32, vp]
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
+        L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
         _lib = L
     return _lib
 
@@ -134,6 +142,33 @@ def supported(seq):
         elif not (isinstance(m, nn.ELU) and m.alpha == 1.0):
             return False
     return True
+
+
+def mlp_forward_supported(lins, k0p):
+    """pmlp_mlp_forward's shape limits (include/ppo_mlp.h): 4 Linear layers, K0 a multiple
+    of 16 (<= 64), hidden widths multiples of 32 (<= 512 / 256 / 512), output <= 32."""
+    if len(lins) != 4 or k0p % 16 or k0p > 64:
+        return False
+    lim = (512, 256, 512)
+    return all(lins[l].out_features % 32 == 0 and lins[l].out_features <= lim[l] for l in range(3)) and \
+        lins[3].out_features <= 32
+
+
+def mlp_forward(nets, M):
+    """One launch of the whole forward of up to two 4-layer MLPs (pmlp_mlp_forward).  nets:
+    dicts x (fp32 [*, ldx]), kx, rows (int64 [M] | None), xa (bf16 [M, K0] | None), K0,
+    W (4 bf16 [N, K] tensors), b (4 fp32 tensors), N (4 ints), y (3 bf16 [M, N] tensors or
+    None), out (fp32 [M, N3])."""
+    def mk(n):
+        y = n.get("y") or (None, None, None)
+        return MlpFwdJob(_p(n["x"]), _p(n.get("rows")), n["x"].stride(0), n["kx"], _p(n.get("xa")),
+                         0 if n.get("xa") is None else n["xa"].stride(0),
+                         (C.c_void_p * 4)(*[_p(w) for w in n["W"]]), (C.c_void_p * 4)(*[_p(b) for b in n["b"]]),
+                         (C.c_int32 * 4)(*n["N"]), n["K0"], (C.c_void_p * 3)(*[_p(t) for t in y]),
+                         (C.c_int32 * 3)(*[0 if t is None else t.stride(0) for t in y]), _p(n["out"]),
+                         n["out"].stride(0))
+    arr = (MlpFwdJob * len(nets))(*[mk(n) for n in nets])
+    _ok(load().pmlp_mlp_forward(len(nets), arr, int(M), _stream()), "pmlp_mlp_forward")
 
 
 def _convert(jobs):
