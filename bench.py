@@ -179,11 +179,14 @@ def _cpu_ppo_iter_s(num_envs, obs_dim, num_actions, threads, env_step_rate, samp
     at env_step_rate) + the update (5 epochs x 4 mini-batches; `sample_steps` optimizer steps
     timed and scaled to the 20).  Go2 MLP actor-critic 512-256-128, fp32 CPU torch."""
     import torch
+    from rsl_rl.algorithms import PPO
     from rsl_rl.modules import ActorCritic
     torch.set_num_threads(int(threads))
     T, epochs, mbs = 24, 5, 4
     ac = ActorCritic(obs_dim, obs_dim, num_actions, [512, 256, 128], [512, 256, 128], mixed_precision=False)
-    opt = torch.optim.Adam(ac.parameters(), lr=1e-3)
+    ppo = PPO(ac, num_learning_epochs=epochs, num_mini_batches=mbs, learning_rate=1e-3, schedule="adaptive",
+              desired_kl=0.01, entropy_coef=0.01, device="cpu", fused_loss=False)
+    opt = ppo.optimizer
     obs = torch.randn(num_envs, obs_dim)
     with torch.no_grad():
         ac.act_and_value(obs, obs)
@@ -192,12 +195,16 @@ def _cpu_ppo_iter_s(num_envs, obs_dim, num_actions, threads, env_step_rate, samp
             ac.act_and_value(obs, obs)
         infer = time.time() - t0
     rows = num_envs * T // mbs
-    xb = torch.randn(rows, obs_dim)
-    ab = torch.randn(rows, num_actions)
+    g = torch.Generator().manual_seed(0)
+    xb = torch.randn(rows, obs_dim, generator=g)
+    mu = 0.3 * torch.randn(rows, num_actions, generator=g)
+    sigma = torch.ones(rows, num_actions)
+    ab = mu + torch.randn(rows, num_actions, generator=g)
+    logp = torch.distributions.Normal(mu, sigma).log_prob(ab).sum(-1, keepdim=True)
+    val, adv, ret = (torch.randn(rows, 1, generator=g) for _ in range(3))
     t0 = time.time()
-    for _ in range(sample_steps):
-        ac.update_distribution(xb)
-        loss = -ac.get_actions_log_prob(ab).mean() + ac.evaluate(xb).pow(2).mean()
+    for _ in range(sample_steps):  # rsl_rl v1.0.2's PPO loss (the torch statement, PPO._reference_loss)
+        loss, _, _ = ppo._reference_loss(xb, xb, ab, val, adv, ret, logp, mu, sigma, (None, None), None)
         opt.zero_grad()
         loss.backward()
         torch.nn.utils.clip_grad_norm_(ac.parameters(), 1.0)
@@ -239,7 +246,8 @@ def cpu_baseline(env, seconds):
     return {"value": round(24 * n / it_all, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": (f"Go2 {n} envs: oracle fused step (PD + 4 substeps + post-physics) {st_all} steps in "
                        f"{el_all:.1f} s on {threads} threads; PPO iteration = 24 x (oracle step + CPU torch "
-                       f"MLP policy) + update (2 optimizer steps of 24,576 rows timed, scaled to 5 x 4)"),
+                       f"MLP policy) + update (2 optimizer steps of rsl_rl's PPO loss on 24,576 rows, clip_grad_norm_ and "
+                       f"Adam timed, scaled to 5 x 4)"),
             "ppo_iter_ms": round(it_all * 1e3, 1),
             "ppo_iter_breakdown_ms": {"env": round(24 * n / rate_all * 1e3, 1), "inference": round(inf_all * 1e3, 1),
                                       "update": round(upd_all * 1e3, 1)},

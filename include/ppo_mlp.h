@@ -291,5 +291,16 @@ PMLP_API int pmlp_lstm_step(int32_t B, int32_t H, const float* gx, const float* 
                             float* h_save, float* c_save, void* stream);
 PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0, const uint8_t* reset,
                            const float* c_out, const float* gact, const float* dh_out, float* dgx, void* stream);
+/* The update's dense sequences on the matrix cores (hidden 64, input <= 64): the forward of
+ * pmlp_lstm_fwd_x and the backward of pmlp_lstm_bwd with the per-step products
+ * [x_t | h_{t-1}] . [W_ih | W_hh]^T and dG . W_hh as bf16 MFMAs (fp32 accumulation, the cell
+ * state and every output fp32).  Same outputs and layouts as the fp32 kernels, to bf16 operand
+ * rounding; the rollout's step (pmlp_lstm_step) stays fp32. */
+PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* x, const float* wih,
+                                const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
+                                const uint8_t* reset, float* h_out, float* c_out, float* gact, float* xh, void* stream);
+PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0,
+                                const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
+                                float* dgx, void* stream);
 
 #endif

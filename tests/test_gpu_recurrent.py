@@ -29,7 +29,7 @@ def test_lstm_kernels_match_torch(H, I):
     c0 = 0.5 * torch.randn(1, B, H, device="cuda")
     reset = (torch.rand(T, B, device="cuda") < 0.1).to(torch.uint8)
     reset[0] = 0
-    y = lstm_seq.lstm_dense(rnn, x, h0, c0, reset)
+    y = lstm_seq.lstm_dense(rnn, x, h0, c0, reset, mfma=False)
     y_ref = lstm_seq.lstm_dense_reference(rnn, x, h0, c0, reset)
     torch.testing.assert_close(y, y_ref, rtol=1e-5, atol=2e-6)
     g = torch.randn_like(y)
@@ -40,8 +40,39 @@ def test_lstm_kernels_match_torch(H, I):
         rel = float((a - b).norm() / b.norm())
         assert rel < 1e-5, (name, rel)
     # without resets and from zeros, the reference statement is nn.LSTM itself
-    y0 = lstm_seq.lstm_dense(rnn, x, None, None, None)
+    y0 = lstm_seq.lstm_dense(rnn, x, None, None, None, mfma=False)
     torch.testing.assert_close(y0, rnn(x)[0], rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("I", [41, 47, 64, 17])
+def test_lstm_mfma_kernels_match_torch_to_bf16(I):
+    """The update's matrix-core LSTM (pmlp_lstm_fwd_mfma / _bwd_mfma: split-bf16 operands,
+    hi.hi + hi.lo + lo.hi products, fp32 accumulation and state) vs the same recurrence in
+    torch fp32 ops over 24 steps with resets inside and a carried initial state: h within
+    1e-4 absolute (h in [-1, 1]), the weight gradients within 1e-3 relative (norm); the
+    weight-gradient operand [x | h_prev | 1] is the fp32 state."""
+    torch.manual_seed(I)
+    T, B, H = 24, 1000, 64
+    rnn = torch.nn.LSTM(I, H).cuda()
+    x = torch.randn(T, B, I, device="cuda")
+    h0 = 0.5 * torch.randn(1, B, H, device="cuda")
+    c0 = 0.5 * torch.randn(1, B, H, device="cuda")
+    reset = (torch.rand(T, B, device="cuda") < 0.1).to(torch.uint8)
+    reset[0, :7] = 1
+    y = lstm_seq.lstm_dense(rnn, x, h0, c0, reset, mfma=True)
+    y_ref = lstm_seq.lstm_dense_reference(rnn, x, h0, c0, reset)
+    err = float((y - y_ref).abs().max())
+    print("mfma lstm max |dh|", err)
+    assert err < 1e-4
+    assert float((y - y_ref).norm() / y_ref.norm()) < 1e-4
+    g = torch.randn_like(y)
+    params = [rnn.weight_ih_l0, rnn.weight_hh_l0, rnn.bias_ih_l0, rnn.bias_hh_l0]
+    gk = torch.autograd.grad(y, params, g)
+    gr = torch.autograd.grad(y_ref, params, g)
+    for name, a, b in zip(("w_ih", "w_hh", "b_ih", "b_hh"), gk, gr):
+        rel = float((a - b).norm() / b.norm())
+        print("mfma lstm grad", name, rel)
+        assert rel < 1e-3, (name, rel)
 
 
 def test_lstm_fused_input_writes_the_weight_gradient_operand():
@@ -303,9 +334,12 @@ def test_hip_lstm_matches_pretrained_policy_golden(robot):
     assert lstm_seq.usable(ac.memory_a.rnn, seq[0])
     for r in rows:
         torch.testing.assert_close(got[:, r], want, rtol=1e-5, atol=1e-5)
-    # (b) the dense sequence kernel (the update's forward), zero state at t = 0
-    with torch.no_grad():
-        h = lstm_seq.lstm_dense(ac.memory_a.rnn, seq, None, None, reset)
-        mu = ac.actor(h.reshape(-1, 64)).view(steps + 5, B, n_act)
-    for r in rows:
-        torch.testing.assert_close(mu[:, r], want, rtol=1e-5, atol=1e-5)
+    # (b) the dense sequence kernels (the update's forward), zero state at t = 0: the fp32
+    # kernel at 1e-5, the matrix-core kernel (split-bf16 operands, ~2^-16 relative per
+    # product) at 2e-4 on the action means
+    for mfma, tol in ((False, 1e-5), (True, 2e-4)):
+        with torch.no_grad():
+            h = lstm_seq.lstm_dense(ac.memory_a.rnn, seq, None, None, reset, mfma=mfma)
+            mu = ac.actor(h.reshape(-1, 64)).view(steps + 5, B, n_act)
+        for r in rows:
+            torch.testing.assert_close(mu[:, r], want, rtol=tol, atol=tol)

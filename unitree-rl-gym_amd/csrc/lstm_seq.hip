@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ppo_mlp.h"
@@ -351,6 +352,316 @@ __global__ __launch_bounds__(4 * H) void k_lstm_bwd(int T, int B, const float* _
     }
 }
 
+
+// ---------------------------------------------------------------- MFMA form --
+// The update's dense sequences on the matrix cores (H = 64, I <= 64): a workgroup of 4
+// waves owns E = 16 envs for all T steps; per step the gate pre-activations of its 16
+// envs are ONE [16 x 128] . [128 x 256] product, [x_t | h_{t-1}] . [W_ih | W_hh]^T, on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation from the fp32 bias.  Precision: every
+// operand is split into bf16 hi + lo (v = hi + lo to ~2^-16 relative) and the product is
+// hi.hi + hi.lo + lo.hi (SPLIT = 3), near fp32; SPLIT = 1 is the plain bf16 product.
+// Gate columns are permuted so that wave w's four 16-column tiles are the i, f, g, o
+// gates of units 16w .. 16w+15: a lane (column j, rows 4(l>>4)..+3) then holds all four
+// gates of its 4 (env, unit) pairs, and the cell update, c and h stay in the lane (fp32).
+// The weight fragments are loaded once; h_{t-1} and x_t sit in a double-buffered LDS
+// operand, one barrier per step.  Outputs as k_lstm_fwd (fp32).
+// The backward runs the same way: the gate gradients (fp32, in the lane) go to dgx and, as
+// bf16 (hi, lo), to an LDS operand for dh_{t-1} = dG . W_hh, whose 16 x 16 result tile of
+// wave w is exactly the lane's own (env, unit) pairs.
+constexpr int ME = 16, MH = 64, MG = 256, MKX = 64;  // envs per workgroup, hidden, gates, x slots
+constexpr int MLDA = MKX + MH + 8;                   // LDS row stride of [x | h] (bf16): 272 B
+constexpr int MLDG = MG + 8;                         // LDS row stride of dG (bf16): 528 B
+
+typedef __bf16 mbf16;
+typedef mbf16 mbf16x8 __attribute__((ext_vector_type(8)));
+typedef float mfloatx4 __attribute__((ext_vector_type(4)));
+
+// activations of the MFMA kernels: v_exp_f32 + v_rcp_f32 (a few ulp; tanh to ~1e-7 absolute)
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; }
+
+__device__ __forceinline__ void split_bf16(float v, mbf16& hi, mbf16& lo) {
+    hi = (mbf16)v;
+    lo = (mbf16)(v - (float)hi);
+}
+
+struct MFwdArgs {
+    int T, B, I;
+    const float *x, *wih, *bih, *bhh, *whh, *h0, *c0;
+    const uint8_t* reset;
+    float *h_out, *c_out, *gact, *xh;
+};
+
+template <int SPLIT>
+__global__ __launch_bounds__(256) void k_lstm_fwd_mfma(MFwdArgs a) {
+    constexpr int NP = SPLIT == 3 ? 2 : 1;  // operand parts (hi, lo)
+    __shared__ __attribute__((aligned(16))) mbf16 A[NP][2][ME * MLDA];
+    const int T = a.T, B = a.B, I = a.I, RL = I + MH + 1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int e0 = blockIdx.x * ME;
+    const int j = lane & 15, rg = lane >> 4;  // column in the tile; row group (envs 4 rg .. 4 rg + 3)
+    const int u = 16 * w + j;                // this lane's unit
+    // weight fragments: tile q (gate q of units 16w..), k-step s: B[k][col] = [W_ih | W_hh][q*H + u][k]
+    mbf16x8 wf[NP][4][4];
+    float bias[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = q * MH + u;
+        bias[q] = a.bih[r] + a.bhh[r];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = s * 32 + 8 * rg + e;
+                const float v = k < MKX ? (k < I ? a.wih[(size_t)r * I + k] : 0.f) : a.whh[(size_t)r * MH + (k - MKX)];
+                mbf16 hi, lo;
+                split_bf16(v, hi, lo);
+                wf[0][q][s][e] = hi;
+                if constexpr (NP == 2) wf[NP - 1][q][s][e] = lo;
+            }
+    }
+    auto put = [&](int buf, int idx, float v) {  // operand element (hi, lo)
+        mbf16 hi, lo;
+        split_bf16(v, hi, lo);
+        A[0][buf][idx] = hi;
+        if constexpr (NP == 2) A[NP - 1][buf][idx] = lo;
+    };
+    // x staging: 4 floats per thread per step (16 envs x 64 slots)
+    const int xe = tid >> 4, xk = (tid & 15) * 4;  // env row, first x slot
+    float xr[4];
+    // loads are unconditional at clamped addresses, the value selected after: a load under a
+    // lane-divergent branch gets a vmcnt(0) at the branch's end and loses its step of slack
+    auto xload = [&](int t) {  // raw values; masked in xstore (no use of a load here)
+        const int gc = min(e0 + xe, B - 1);
+        const size_t tc = (size_t)min(t, T - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = a.x[(tc * B + gc) * I + min(xk + i, I - 1)];
+    };
+    auto xstore = [&](int buf, int t) {  // the operand; the fp32 x into xh
+        const int ge = e0 + xe;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = (ge < B && xk + i < I) ? xr[i] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) put(buf, xe * MLDA + xk + i, xr[i]);
+        if (a.xh && ge < B) {
+            float* row = a.xh + ((size_t)t * B + ge) * RL;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (xk + i < I) row[xk + i] = xr[i];
+            if (xk == 0) row[I + MH] = 1.f;
+        }
+    };
+    // state of the lane's 4 (env, unit) pairs
+    float c[4], hp[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int ge = e0 + 4 * rg + p;
+        const bool rs = a.reset && ge < B && a.reset[ge];
+        const float h0 = (ge < B && a.h0) ? a.h0[(size_t)ge * MH + u] : 0.f;
+        const float c0 = (ge < B && a.c0) ? a.c0[(size_t)ge * MH + u] : 0.f;
+        hp[p] = rs ? 0.f : h0;
+        c[p] = rs ? 0.f : c0;
+        put(0, (4 * rg + p) * MLDA + MKX + u, hp[p]);
+    }
+    // next step's reset flags of the lane's 4 envs, loaded a step ahead
+    const bool has_reset = a.reset != nullptr;
+    const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
+    auto rload = [&](int t, uint8_t* r) {
+        const size_t tc = (size_t)min(t, T - 1) * B;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) r[p] = rbase[tc + min(e0 + 4 * rg + p, B - 1)];
+    };
+    uint8_t rnx[4];
+    rload(1, rnx);
+    xload(0);
+    xstore(0, 0);
+    if (T > 1) xload(1);
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        const int cur = t & 1;
+        bool rn[4];  // a reset at t + 1 (rows past B never matter)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) rn[p] = has_reset && t + 1 < T && rnx[p] != 0;
+        rload(t + 2, rnx);
+        mfloatx4 acc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[q][p] = bias[q];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {  // four independent accumulator chains per product
+            const int o = j * MLDA + s * 32 + 8 * rg;
+            const mbf16x8 ah = *(const mbf16x8*)(&A[0][cur][o]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[0][q][s], acc[q], 0, 0, 0);
+            if constexpr (NP == 2) {
+                const mbf16x8 al = *(const mbf16x8*)(&A[NP - 1][cur][o]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[NP - 1][q][s], acc[q], 0, 0, 0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[0][q][s], acc[q], 0, 0, 0);
+            }
+        }
+        const int nxt = cur ^ 1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int ge = e0 + 4 * rg + p;
+            const float ig = fsig(acc[0][p]), fg = fsig(acc[1][p]), gg = ftanh(acc[2][p]), og = fsig(acc[3][p]);
+            const float cn = fg * c[p] + ig * gg;
+            const float hn = og * ftanh(cn);
+            if (ge < B) {
+                const size_t row = (size_t)t * B + ge;
+                if (a.gact) {
+                    float* gr = a.gact + row * MG;
+                    gr[u] = ig; gr[MH + u] = fg; gr[2 * MH + u] = gg; gr[3 * MH + u] = og;
+                }
+                if (a.c_out) a.c_out[row * MH + u] = cn;
+                if (a.h_out) a.h_out[row * MH + u] = hn;
+                if (a.xh) a.xh[row * RL + I + u] = hp[p];  // the state this step started from
+            }
+            c[p] = rn[p] ? 0.f : cn;  // a reset at t + 1 starts that step from zero
+            hp[p] = rn[p] ? 0.f : hn;
+            if (t + 1 < T) put(nxt, (4 * rg + p) * MLDA + MKX + u, hp[p]);
+        }
+        if (t + 1 < T) xstore(nxt, t + 1);
+        xload(t + 2);  // clamped to T - 1 past the end
+        __syncthreads();
+    }
+}
+
+struct MBwdArgs {
+    int T, B;
+    const float *whh, *c0;
+    const uint8_t* reset;
+    const float *c_out, *gact, *dh_out;
+    float* dgx;
+};
+
+template <int SPLIT>
+__global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
+    constexpr int NP = SPLIT == 3 ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) mbf16 G[NP][2][ME * MLDG];
+    const int T = a.T, B = a.B;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int e0 = blockIdx.x * ME;
+    const int j = lane & 15, rg = lane >> 4, u = 16 * w + j;
+    // B[k = permuted gate column][n = unit 16w + j] = W_hh[torch row of k][u], 8 k-steps of 32
+    mbf16x8 wf[NP][8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = s * 32 + 8 * rg + e;  // permuted column: wave kw, gate kq, unit kj
+            const int kw = k >> 6, kq = (k >> 4) & 3, kj = k & 15;
+            mbf16 hi, lo;
+            split_bf16(a.whh[(size_t)(kq * MH + 16 * kw + kj) * MH + u], hi, lo);
+            wf[0][s][e] = hi;
+            if constexpr (NP == 2) wf[NP - 1][s][e] = lo;
+        }
+    // the step's global inputs for the lane's 4 (env, unit) pairs, loaded one step ahead
+    struct In {
+        float g[4][4], cv[4], cp[4], dh[4];
+        uint8_t rs[4];
+        bool cz;
+    };
+    // unconditional loads at clamped addresses (see the forward); rows past B are computed
+    // and never stored, t < 0 is never used
+    // (absent reset / c0 read valid memory and are masked where used; nothing here consumes
+    // a loaded value, so the loads stay in flight across the step)
+    const bool has_reset = a.reset != nullptr, has_c0 = a.c0 != nullptr;
+    const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.c_out;
+    auto load = [&](int t, In& v) {
+        const int tt = max(t, 0);
+        const float* cpb = tt > 0 ? a.c_out + (size_t)(tt - 1) * B * MH : (has_c0 ? a.c0 : a.c_out);
+        v.cz = tt == 0 && !has_c0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int gc = min(e0 + 4 * rg + p, B - 1);
+            const size_t row = (size_t)tt * B + gc;
+            v.rs[p] = rbase[row];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v.g[p][q] = a.gact[row * MG + q * MH + u];
+            v.cv[p] = a.c_out[row * MH + u];
+            v.cp[p] = cpb[(size_t)gc * MH + u];
+            v.dh[p] = a.dh_out[row * MH + u];
+        }
+    };
+    float dhn[4] = {0.f, 0.f, 0.f, 0.f}, dcn[4] = {0.f, 0.f, 0.f, 0.f};
+    In nx;
+    load(T - 1, nx);
+    for (int t = T - 1; t >= 0; --t) {
+        const int buf = t & 1;
+        const In v = nx;
+        load(t - 1, nx);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int ge = e0 + 4 * rg + p;
+            const bool rs = has_reset && v.rs[p] != 0;
+            const float cp = (rs || v.cz) ? 0.f : v.cp[p];
+            const float ig = v.g[p][0], fg = v.g[p][1], gg = v.g[p][2], og = v.g[p][3];
+            const float dh = v.dh[p] + dhn[p];
+            const float tc = ftanh(v.cv[p]);
+            const float dc = dcn[p] + dh * og * (1.f - tc * tc);
+            float dg[4];
+            dg[0] = dc * gg * ig * (1.f - ig);
+            dg[1] = dc * cp * fg * (1.f - fg);
+            dg[2] = dc * ig * (1.f - gg * gg);
+            dg[3] = dh * tc * og * (1.f - og);
+            dcn[p] = rs ? 0.f : dc * fg;  // into c_{t-1} (none across a reset)
+            if (ge < B) {
+                float* o = a.dgx + ((size_t)t * B + ge) * MG;
+                o[u] = dg[0]; o[MH + u] = dg[1]; o[2 * MH + u] = dg[2]; o[3 * MH + u] = dg[3];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dg[q] = 0.f;  // rows past B feed nothing
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                mbf16 hi, lo;
+                split_bf16(dg[q], hi, lo);
+                const int o = (4 * rg + p) * MLDG + 64 * w + 16 * q + j;
+                G[0][buf][o] = hi;
+                if constexpr (NP == 2) G[NP - 1][buf][o] = lo;
+            }
+        }
+        __syncthreads();
+        // dh_{t-1} = dG . W_hh for units 16w + j, envs 4 rg .. 4 rg + 3: this lane's own pairs;
+        // six independent accumulator chains (k-step parity x product), summed at the end
+        mfloatx4 acc[2][3];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) acc[m][k][p] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int o = j * MLDG + s * 32 + 8 * rg;
+            const mbf16x8 ah = *(const mbf16x8*)(&G[0][buf][o]);
+            acc[s & 1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[0][s], acc[s & 1][0], 0, 0, 0);
+            if constexpr (NP == 2) {
+                const mbf16x8 al = *(const mbf16x8*)(&G[NP - 1][buf][o]);
+                acc[s & 1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[NP - 1][s], acc[s & 1][1], 0, 0, 0);
+                acc[s & 1][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[0][s], acc[s & 1][2], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const float d = (acc[0][0][p] + acc[1][0][p]) + ((acc[0][1][p] + acc[1][1][p]) + (acc[0][2][p] + acc[1][2][p]));
+            dhn[p] = (has_reset && v.rs[p]) ? 0.f : d;
+        }
+    }
+}
+
+// operand precision of the MFMA sequence kernels: 3 = split bf16 (default), 1 = plain bf16
+static int mfma_split() {
+    static const int v = [] {
+        const char* e = getenv("LSTM_MFMA_SPLIT");
+        return (e && atoi(e) == 1) ? 1 : 3;
+    }();
+    return v;
+}
+
 thread_local std::string g_err;
 
 int fail(const std::string& m) {
@@ -446,4 +757,28 @@ PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, co
     case 128: return bwd_h<128>(T, B, whh, c0, reset, c_out, gact, dh_out, dgx, s);
     default: return fail("pmlp_lstm_bwd: hidden size must be 32, 64 or 128");
     }
+}
+
+PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* x, const float* wih,
+                                const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
+                                const uint8_t* reset, float* h_out, float* c_out, float* gact, float* xh, void* stream) {
+    if (T <= 0 || B <= 0 || !x || !wih || !bih || !bhh || !whh) return fail("pmlp_lstm_fwd_mfma: empty sequence or null input");
+    if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
+    MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh};
+    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma<1>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(k_lstm_fwd_mfma<3>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma: ") + hipGetErrorString(e));
+}
+
+PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0,
+                                const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
+                                float* dgx, void* stream) {
+    if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !dgx) return fail("pmlp_lstm_bwd_mfma: null buffer");
+    if (H != MH) return fail("pmlp_lstm_bwd_mfma: hidden 64");
+    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, dgx};
+    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_bwd_mfma<1>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(k_lstm_bwd_mfma<3>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_mfma: ") + hipGetErrorString(e));
 }

@@ -34,6 +34,8 @@ def _lib():
         L.pmlp_lstm_bwd.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
         L.pmlp_lstm_fwd_x.argtypes = [i32, i32, i32, i32] + [vp] * 14 + [vp]
         L.pmlp_lstm_step.argtypes = [i32, i32] + [vp] * 6 + [vp]
+        L.pmlp_lstm_fwd_mfma.argtypes = [i32, i32, i32, i32] + [vp] * 12 + [vp]
+        L.pmlp_lstm_bwd_mfma.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
         _bound = True
     return L
 
@@ -41,6 +43,16 @@ def _lib():
 def _ok(status, what):
     if status != 0:
         raise RuntimeError(f"{what} failed: {_lib().pmlp_lstm_last_error().decode(errors='replace')}")
+
+
+# The update's dense sequences on the matrix cores (pmlp_lstm_fwd_mfma / _bwd_mfma: bf16
+# products, fp32 state) for hidden 64 and inputs <= 64; LSTM_MFMA=0 keeps the fp32 kernels.
+# The rollout's step (lstm_step_) is always the fp32 kernel.
+MFMA = os.environ.get("LSTM_MFMA", "1") != "0"
+
+
+def mfma_usable(rnn, x):
+    return MFMA and rnn.hidden_size == 64 and x.shape[-1] <= 64
 
 
 def usable(rnn, x):
@@ -73,7 +85,7 @@ def _rows_tn(g, x, chunk=None):
 
 class _LSTMDense(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, h0, c0, reset, w_ih, w_hh, b_ih, b_hh):
+    def forward(ctx, x, h0, c0, reset, w_ih, w_hh, b_ih, b_hh, mfma=False):
         T, B, I = x.shape
         H = w_hh.shape[1]
         whh = w_hh.detach().contiguous()
@@ -83,7 +95,12 @@ class _LSTMDense(torch.autograd.Function):
         # [x | h_prev | 1] per row: the operand of all three weight gradients
         xh = torch.empty(T, B, I + H + 1, device=x.device)
         p = mm._p
-        if I <= 64:  # the input projection inside the sequence kernel, which also writes xh
+        ctx.mfma = mfma
+        if mfma:  # the per-step products on the matrix cores (bf16 operands, fp32 state)
+            _ok(_lib().pmlp_lstm_fwd_mfma(T, B, H, I, p(x), p(w_ih.detach().contiguous()), p(b_ih.detach()),
+                                          p(b_hh.detach()), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out),
+                                          p(gact), p(xh), mm._stream()), "pmlp_lstm_fwd_mfma")
+        elif I <= 64:  # the input projection inside the sequence kernel, which also writes xh
             _ok(_lib().pmlp_lstm_fwd_x(T, B, H, I, p(x), p(w_ih.detach().contiguous()), p(b_ih.detach()),
                                        p(b_hh.detach()), p(whh), p(h0), p(c0), p(reset), p(h_out), p(c_out), p(gact),
                                        None, None, p(xh), mm._stream()), "pmlp_lstm_fwd_x")
@@ -112,19 +129,21 @@ class _LSTMDense(torch.autograd.Function):
         H = whh.shape[1]
         dgx = torch.empty(T, B, 4 * H, device=xh.device)
         p = mm._p
-        _ok(_lib().pmlp_lstm_bwd(T, B, H, p(whh), p(c0), p(reset), p(c_out), p(gact), p(dh_out.contiguous()), p(dgx),
-                                 mm._stream()), "pmlp_lstm_bwd")
+        bwd = _lib().pmlp_lstm_bwd_mfma if ctx.mfma else _lib().pmlp_lstm_bwd
+        _ok(bwd(T, B, H, p(whh), p(c0), p(reset), p(c_out), p(gact), p(dh_out.contiguous()), p(dgx), mm._stream()),
+            "pmlp_lstm_bwd_mfma" if ctx.mfma else "pmlp_lstm_bwd")
         # all three weight gradients from ONE product dgx^T [x | h_prev | 1] over the T*B
         # rows, split over the rows (a library GEMM puts a 49k-long reduction on a few
         # output tiles: 170 us per call at H1 scale)
         dw = _rows_tn(dgx.view(T * B, 4 * H), xh.view(T * B, I + H + 1))
         dw_ih, dw_hh, db = dw[:, :I].contiguous(), dw[:, I:I + H].contiguous(), dw[:, I + H].contiguous()
-        return None, None, None, None, dw_ih, dw_hh, db, db
+        return None, None, None, None, dw_ih, dw_hh, db, db, None
 
 
-def lstm_dense(rnn, x, h0, c0, reset):
+def lstm_dense(rnn, x, h0, c0, reset, mfma=None):
     """[T,B,I] -> [T,B,H] through rnn (nn.LSTM, one layer) with resets before step t where
-    reset[t] != 0; h0/c0 [B,H] (detached: the saved rollout state) or None."""
+    reset[t] != 0; h0/c0 [B,H] (detached: the saved rollout state) or None.  mfma: the
+    matrix-core kernels (default: where mfma_usable)."""
     def state(s):
         if s is None:
             return None
@@ -133,8 +152,9 @@ def lstm_dense(rnn, x, h0, c0, reset):
 
     h0, c0 = state(h0), state(c0)
     reset = None if reset is None else reset.to(torch.uint8).contiguous()
+    mfma = mfma_usable(rnn, x) if mfma is None else bool(mfma)
     return _LSTMDense.apply(x.contiguous(), h0, c0, reset, rnn.weight_ih_l0, rnn.weight_hh_l0, rnn.bias_ih_l0,
-                            rnn.bias_hh_l0)
+                            rnn.bias_hh_l0, mfma)
 
 
 def lstm_dense_reference(rnn, x, h0, c0, reset):
