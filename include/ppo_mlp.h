@@ -245,6 +245,28 @@ typedef struct {
 } pmlp_mlp_fwd_job;
 PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream);
 
+/* ---- recurrent heads (the fused recurrent optimizer step, rsl_rl/algorithms/fused_recurrent.py):
+ * the MLP heads of ActorCriticRecurrent on the LSTM output h [M, H] (rsl_rl
+ * actor_critic_recurrent.py: the actor / critic Sequential(Linear(H, N0), ELU, Linear(N0, N1))),
+ * fp32, up to two nets per launch.  H in {32, 64, 128}; N0 <= 32 a multiple of 4; N1 <= 16.
+ * pmlp_heads_forward:  y0 = elu(W0 h + b0) [M, N0], out = W1 y0 + b1 [M, N1]
+ * pmlp_heads_backward: from dout [M, N1] (the loss gradient): dh = W0^T ((W1^T dout) * elu'(y0))
+ *   [M, H] (the LSTM's output gradient, elu' from the output as torch), and the partial
+ *   weight gradients of every block of 128 rows, slab[b] = [dW0 | db0 | dW1 | db1]
+ *   (N0 H + N0 + N1 N0 + N1 floats per row of the slab, pmlp_heads_blocks(M) rows): summed
+ *   by pmlp_reduce_slabs into the flat gradient (the Sequential's parameter order).
+ * Weights row-major as nn.Linear ([out, in]); h, W0, dh and slab 16-byte aligned.        */
+typedef struct {
+    const float *h, *W0, *b0, *W1, *b1;
+    float *y0, *out;
+    const float* dout;
+    float *dh, *slab;
+    int32_t N0, N1;
+} pmlp_head_job;
+PMLP_API int32_t pmlp_heads_blocks(int32_t M);
+PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream);
+PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream);
+
 /* The same loss for the fused optimizer step (gradient of the loss itself):
  * one pass writes the output gradients straight into the MLP backward's bf16
  * operands, dmu[M,Ap] + dmu_t[Ap,M] and dvalue[M,Vp] + dvalue_t[Vp,M]
@@ -258,6 +280,14 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
                                 float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
                                 float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
                                 pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
+/* The same step with fp32 output gradients dmu [M, A] (16-byte aligned when A % 4 == 0) and
+ * dvalue [M] (the recurrent heads' fp32 backward, pmlp_heads_backward).                */
+PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const float* value, const float* actions,
+                                    const float* old_logp, const float* old_mu, const float* old_sigma,
+                                    const float* adv, const float* ret, const float* target, const int64_t* rows,
+                                    int32_t M, int32_t A, float clip, int32_t clipped_value, float vcoef, float ecoef,
+                                    float* partial, float* stats, float* dstd, float* dmu, float* dvalue,
+                                    void* stream);
 
 /* ---- recurrent memory: rsl_rl v1.0.2 Memory (one-layer LSTM, gate order i, f, g, o)
  * for ActorCriticRecurrent (the G1 / H1 / H1_2 policies: g1_config.py:92-108,

@@ -197,7 +197,8 @@ def test_recurrent_update_graph_matches_eager():
     last = _synthetic_storage(alg, T, N, O, P, A, H, seed=2).cuda()
     alg.compute_returns(last)
     alg.update()  # eager warm-up
-    assert alg._graph is None
+    graph_of = lambda a: a._graph if a._rfused is None else a._rgraph  # noqa: E731
+    assert graph_of(alg) is None
     saved = {k: v.clone() for k, v in alg.storage.__dict__.items() if torch.is_tensor(v) and not k.startswith("_")}
     params = list(ac.parameters())
     p0 = [p.detach().clone() for p in params]
@@ -205,7 +206,7 @@ def test_recurrent_update_graph_matches_eager():
            for p in params}
     alg.storage.step = T
     g_loss = alg.update()  # captured + replayed
-    assert alg._graph is not None
+    assert graph_of(alg) is not None
     p_graph = [p.detach().clone() for p in params]
     with torch.no_grad():
         for p, v in zip(params, p0):
@@ -343,3 +344,45 @@ def test_hip_lstm_matches_pretrained_policy_golden(robot):
             mu = ac.actor(h.reshape(-1, 64)).view(steps + 5, B, n_act)
         for r in rows:
             torch.testing.assert_close(mu[:, r], want, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("H", [32, 64, 128])
+def test_fused_recurrent_heads_match_torch(H):
+    """pmlp_heads_forward / pmlp_heads_backward (the fused recurrent step's MLP heads, fp32) vs
+    torch autograd of Sequential(Linear(H, 32), ELU, Linear(32, N1)) for the actor (N1 = 12)
+    and the critic (N1 = 1) in one launch each, on a row count that is not a multiple of the
+    128-row blocks; the per-block weight-gradient partials summed by pmlp_reduce_slabs."""
+    from rsl_rl.modules import mfma_mlp as mm
+    torch.manual_seed(H)
+    M, N0 = 1000, 32
+    nets = [torch.nn.Sequential(torch.nn.Linear(H, N0), torch.nn.ELU(), torch.nn.Linear(N0, n1)).cuda()
+            for n1 in (12, 1)]
+    hs = [torch.randn(M, H, device="cuda") for _ in range(2)]
+    douts = [torch.randn(M, n.__getitem__(2).out_features, device="cuda") for n in nets]
+    lib = mm.load()
+    nblk = lib.pmlp_heads_blocks(M)
+    bufs = []
+    for n, net in enumerate(nets):
+        n1 = net[2].out_features
+        nh = N0 * H + N0 + n1 * N0 + n1
+        bufs.append(dict(y0=torch.empty(M, N0, device="cuda"), out=torch.empty(M, n1, device="cuda"),
+                         dh=torch.empty(M, H, device="cuda"), slab=torch.empty(nblk, nh, device="cuda"),
+                         grad=torch.empty(nh, device="cuda"), nh=nh))
+    P = mm._p
+    jobs = (mm.HeadJob * 2)(*[mm.HeadJob(P(hs[n]), P(net[0].weight), P(net[0].bias), P(net[2].weight), P(net[2].bias),
+                                         P(bufs[n]["y0"]), P(bufs[n]["out"]), P(douts[n]), P(bufs[n]["dh"]),
+                                         P(bufs[n]["slab"]), N0, net[2].out_features) for n, net in enumerate(nets)])
+    mm._ok(lib.pmlp_heads_forward(2, jobs, M, H, mm._stream()), "pmlp_heads_forward")
+    mm._ok(lib.pmlp_heads_backward(2, jobs, M, H, mm._stream()), "pmlp_heads_backward")
+    mm._reduce([(b["slab"], b["grad"], b["nh"], nblk) for b in bufs])
+    for n, net in enumerate(nets):
+        h = hs[n].clone().requires_grad_(True)
+        y0 = torch.nn.functional.elu(net[0](h))
+        out = net[2](y0)
+        torch.testing.assert_close(bufs[n]["y0"], y0.detach(), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(bufs[n]["out"], out.detach(), rtol=1e-5, atol=1e-5)
+        params = [net[0].weight, net[0].bias, net[2].weight, net[2].bias]
+        g = torch.autograd.grad(out, [h] + params, douts[n])
+        torch.testing.assert_close(bufs[n]["dh"], g[0], rtol=1e-5, atol=1e-5)
+        want = torch.cat([t.reshape(-1) for t in g[1:]])
+        torch.testing.assert_close(bufs[n]["grad"], want, rtol=1e-4, atol=1e-4)

@@ -55,6 +55,7 @@ mm._gemm = wrap("gemm", mm._gemm, lambda epi, jobs, ksplit=0: f"gemm {EPI.get(ep
                 f"N={jobs[0]['N']:4d} K={jobs[0]['K']:6d} x{len(jobs)}")
 mm._convert = wrap("convert", mm._convert, lambda jobs: "convert")
 mm._reduce = wrap("reduce", mm._reduce, lambda jobs: "reduce slabs")
+mm.mlp_forward = wrap("mlp_forward", mm.mlp_forward, lambda nets, M: f"mlp_forward (fused, both nets) M={M}")
 
 for i in range(3):
     f.run(perm[(i % 4) * mb:((i % 4) + 1) * mb], src, acc)

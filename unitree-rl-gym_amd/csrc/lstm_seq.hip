@@ -653,6 +653,195 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     }
 }
 
+// ------------------------------------------------------------ recurrent heads --
+// The MLP heads of ActorCriticRecurrent on the LSTM output (rsl_rl actor / critic:
+// Linear(H, N0) -> ELU -> Linear(N0, N1)), fp32, for the fused recurrent optimizer step:
+// one row per thread, HR rows per workgroup, the weights in LDS (every lane reads the same
+// entry: broadcasts), row tiles staged through LDS so every global access is coalesced.
+//   forward:  y0 = elu(W0 h + b0) [M, N0], out = W1 y0 + b1 [M, N1]
+//   backward: from dout [M, N1]: dz0 = (W1^T dout) * elu'(y0) (torch's form from the output:
+//             1 for y0 > 0, else y0 + 1), dh = W0^T dz0 [M, H] (the LSTM's output gradient),
+//             and per workgroup the partial sums of [dW0 | db0 | dW1 | db1] (the parameter
+//             order of the Sequential's two Linears) into slab row blockIdx.x.
+constexpr int HR = 128, HN0 = 32, HN1 = 16;  // rows per workgroup; max N0, N1 (rsl_rl configs: [32])
+
+struct HeadJob {
+    const float *h, *W0, *b0, *W1, *b1;
+    float *y0, *out;        // forward outputs
+    const float* dout;      // backward input
+    float *dh, *slab;       // backward outputs
+    int N0, N1;
+};
+struct HeadJobs {
+    HeadJob j[2];
+};
+
+template <int H>
+__global__ __launch_bounds__(HR) void k_heads_fwd(HeadJobs jobs, int M) {
+    const HeadJob& J = jobs.j[blockIdx.y];
+    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
+    constexpr int LH = H + 4, LY = HN0 + 1, LO = HN1 + 1;
+    constexpr int HS = HR * LH > HR * (LY + LO) ? HR * LH : HR * (LY + LO);  // h tile, then y0 + out
+    __shared__ __attribute__((aligned(16))) float hs[HS];
+    __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
+    __shared__ float bb0[HN0], w1[HN1 * HN0], bb1[HN1];
+    for (int i = tid; i < N0 * H; i += HR) w0[i] = J.W0[i];
+    for (int i = tid; i < N1 * N0; i += HR) w1[i] = J.W1[i];
+    if (tid < N0) bb0[tid] = J.b0[tid];
+    if (tid < N1) bb1[tid] = J.b1[tid];
+    for (int i = tid; i < HR * (H / 4); i += HR) {  // the h rows, coalesced
+        const int r = i / (H / 4), c = (i % (H / 4)) * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r0 + r < M) v = *(const float4*)(J.h + (size_t)(r0 + r) * H + c);
+        *(float4*)(hs + r * LH + c) = v;
+    }
+    __syncthreads();
+    float hr[H];
+#pragma unroll
+    for (int k = 0; k < H; k += 4) {
+        const float4 v = *(const float4*)(hs + tid * LH + k);
+        hr[k] = v.x; hr[k + 1] = v.y; hr[k + 2] = v.z; hr[k + 3] = v.w;
+    }
+    float o[HN1];
+#pragma unroll
+    for (int i = 0; i < HN1; ++i) o[i] = 0.f;
+    __syncthreads();  // (hs is reused for the y0 tile below)
+    for (int j = 0; j < N0; ++j) {
+        float z = bb0[j];
+#pragma unroll
+        for (int k = 0; k < H; k += 4) {
+            const float4 w = *(const float4*)(w0 + j * H + k);
+            z = fmaf(w.x, hr[k], z); z = fmaf(w.y, hr[k + 1], z); z = fmaf(w.z, hr[k + 2], z); z = fmaf(w.w, hr[k + 3], z);
+        }
+        const float y = z > 0.f ? z : expm1f(z);
+        hs[tid * LY + j] = y;
+#pragma unroll
+        for (int i = 0; i < HN1; ++i)
+            if (i < N1) o[i] = fmaf(w1[i * N0 + j], y, o[i]);
+    }
+    float* os = hs + HR * LY;  // [HR][LO]
+#pragma unroll
+    for (int i = 0; i < HN1; ++i)
+        if (i < N1) os[tid * LO + i] = o[i] + bb1[i];
+    __syncthreads();
+    for (int i = tid; i < HR * N0; i += HR) {  // coalesced row-major stores
+        const int r = i / N0, c = i - r * N0;
+        if (r0 + r < M) J.y0[(size_t)(r0 + r) * N0 + c] = hs[r * LY + c];
+    }
+    for (int i = tid; i < HR * N1; i += HR) {
+        const int r = i / N1, c = i - r * N1;
+        if (r0 + r < M) J.out[(size_t)(r0 + r) * N1 + c] = os[r * LO + c];
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(HR) void k_heads_bwd(HeadJobs jobs, int M) {
+    const HeadJob& J = jobs.j[blockIdx.y];
+    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
+    constexpr int LH = H + 4, LZ = HN0 + 4, LY = HN0 + 1, LO = HN1 + 1;
+    __shared__ __attribute__((aligned(16))) float hs[HR * LH];   // h, then dh
+    __shared__ __attribute__((aligned(16))) float zs[HR * LZ];   // dz0
+    __shared__ float ys[HR * LY], ds[HR * LO];                    // y0, dout
+    __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
+    __shared__ float w1[HN1 * HN0];
+    for (int i = tid; i < N0 * H; i += HR) w0[i] = J.W0[i];
+    for (int i = tid; i < N1 * N0; i += HR) w1[i] = J.W1[i];
+    for (int i = tid; i < HR * (H / 4); i += HR) {
+        const int r = i / (H / 4), c = (i % (H / 4)) * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r0 + r < M) v = *(const float4*)(J.h + (size_t)(r0 + r) * H + c);
+        *(float4*)(hs + r * LH + c) = v;
+    }
+    for (int i = tid; i < HR * N0; i += HR) {
+        const int r = i / N0, c = i - r * N0;
+        ys[r * LY + c] = r0 + r < M ? J.y0[(size_t)(r0 + r) * N0 + c] : 0.f;
+    }
+    for (int i = tid; i < HR * N1; i += HR) {
+        const int r = i / N1, c = i - r * N1;
+        ds[r * LO + c] = r0 + r < M ? J.dout[(size_t)(r0 + r) * N1 + c] : 0.f;
+    }
+    __syncthreads();
+    // the row's dz0 (registers and the LDS tile)
+    float dz[HN0];
+    {
+        float d[HN1];
+#pragma unroll
+        for (int i = 0; i < HN1; ++i) d[i] = i < N1 ? ds[tid * LO + i] : 0.f;
+#pragma unroll
+        for (int j = 0; j < HN0; ++j) {
+            float g = 0.f;
+            if (j < N0) {
+#pragma unroll
+                for (int i = 0; i < HN1; ++i)
+                    if (i < N1) g = fmaf(w1[i * N0 + j], d[i], g);
+                const float y = ys[tid * LY + j];
+                g = y > 0.f ? g : g * (y + 1.f);
+            }
+            dz[j] = g;
+            zs[tid * LZ + j] = g;
+        }
+    }
+    __syncthreads();
+    // partial weight gradients of this workgroup's rows (fixed order: deterministic)
+    float* sl = J.slab + (size_t)blockIdx.x * (N0 * H + N0 + N1 * N0 + N1);
+    for (int t = tid; t < (N0 / 4) * (H / 4); t += HR) {  // dW0, 4 x 4 per thread
+        const int j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
+        float a[4][4] = {};
+        for (int r = 0; r < HR; ++r) {
+            const float4 z4 = *(const float4*)(zs + r * LZ + j0);
+            const float4 h4 = *(const float4*)(hs + r * LH + k0);
+            const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) a[u][v] = fmaf(zz[u], hh[v], a[u][v]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            *(float4*)(sl + (size_t)(j0 + u) * H + k0) = make_float4(a[u][0], a[u][1], a[u][2], a[u][3]);
+    }
+    for (int j = tid; j < N0; j += HR) {  // db0
+        float a = 0.f;
+        for (int r = 0; r < HR; ++r) a += zs[r * LZ + j];
+        sl[N0 * H + j] = a;
+    }
+    for (int t = tid; t < N1 * N0; t += HR) {  // dW1
+        const int i = t / N0, j = t - i * N0;
+        float a = 0.f;
+        for (int r = 0; r < HR; ++r) a = fmaf(ds[r * LO + i], ys[r * LY + j], a);
+        sl[N0 * H + N0 + t] = a;
+    }
+    for (int i = tid; i < N1; i += HR) {  // db1
+        float a = 0.f;
+        for (int r = 0; r < HR; ++r) a += ds[r * LO + i];
+        sl[N0 * H + N0 + N1 * N0 + i] = a;
+    }
+    __syncthreads();  // every read of the h tile is done: it takes dh
+    {
+        float dh[H];
+#pragma unroll
+        for (int k = 0; k < H; ++k) dh[k] = 0.f;
+#pragma unroll
+        for (int j = 0; j < HN0; ++j) {
+            if (j < N0) {
+#pragma unroll
+                for (int k = 0; k < H; k += 4) {
+                    const float4 w = *(const float4*)(w0 + j * H + k);
+                    dh[k] = fmaf(w.x, dz[j], dh[k]); dh[k + 1] = fmaf(w.y, dz[j], dh[k + 1]);
+                    dh[k + 2] = fmaf(w.z, dz[j], dh[k + 2]); dh[k + 3] = fmaf(w.w, dz[j], dh[k + 3]);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < H; k += 4) *(float4*)(hs + tid * LH + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
+    }
+    __syncthreads();
+    for (int i = tid; i < HR * (H / 4); i += HR) {
+        const int r = i / (H / 4), c = (i % (H / 4)) * 4;
+        if (r0 + r < M) *(float4*)(J.dh + (size_t)(r0 + r) * H + c) = *(const float4*)(hs + r * LH + c);
+    }
+}
+
 // operand precision of the MFMA sequence kernels: 3 = split bf16 (default), 1 = plain bf16
 static int mfma_split() {
     static const int v = [] {
@@ -781,4 +970,56 @@ PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* wh
     else hipLaunchKernelGGL(k_lstm_bwd_mfma<3>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_mfma: ") + hipGetErrorString(e));
+}
+
+/* The recurrent policy's MLP heads (include/ppo_mlp.h, "recurrent heads"). */
+static int heads_check(const char* w, int njobs, const pmlp_head_job* jobs, int M, int H, bool bwd) {
+    if (njobs < 1 || njobs > 2 || !jobs || M <= 0) return fail(std::string(w) + ": 1..2 jobs, M > 0");
+    if (H != 32 && H != 64 && H != 128) return fail(std::string(w) + ": H must be 32, 64 or 128");
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_head_job& J = jobs[i];
+        if (J.N0 <= 0 || J.N0 > HN0 || J.N0 % 4 || J.N1 <= 0 || J.N1 > HN1)
+            return fail(std::string(w) + ": 0 < N0 <= 32 (a multiple of 4), 0 < N1 <= 16");
+        if (!J.h || !J.W0 || !J.W1 || ((uintptr_t)J.h & 15u) || ((uintptr_t)J.W0 & 15u))
+            return fail(std::string(w) + ": null or unaligned h / W0 / W1");
+        if (!bwd && (!J.b0 || !J.b1 || !J.y0 || !J.out)) return fail(std::string(w) + ": null b0 / b1 / y0 / out");
+        if (bwd && (!J.y0 || !J.dout || !J.dh || !J.slab || ((uintptr_t)J.dh & 15u) || ((uintptr_t)J.slab & 15u)))
+            return fail(std::string(w) + ": null or unaligned y0 / dout / dh / slab");
+    }
+    return 0;
+}
+
+static HeadJobs heads_pack(int njobs, const pmlp_head_job* jobs) {
+    HeadJobs hj{};
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_head_job& J = jobs[i];
+        hj.j[i] = HeadJob{J.h, J.W0, J.b0, J.W1, J.b1, J.y0, J.out, J.dout, J.dh, J.slab, J.N0, J.N1};
+    }
+    return hj;
+}
+
+PMLP_API int32_t pmlp_heads_blocks(int32_t M) { return (M + HR - 1) / HR; }
+
+PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
+    if (int e = heads_check("pmlp_heads_forward", njobs, jobs, M, H, false)) return e;
+    const HeadJobs hj = heads_pack(njobs, jobs);
+    const dim3 g((M + HR - 1) / HR, njobs);
+    hipStream_t s = (hipStream_t)stream;
+    if (H == 32) hipLaunchKernelGGL(k_heads_fwd<32>, g, dim3(HR), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL(k_heads_fwd<64>, g, dim3(HR), 0, s, hj, M);
+    else hipLaunchKernelGGL(k_heads_fwd<128>, g, dim3(HR), 0, s, hj, M);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward: ") + hipGetErrorString(e));
+}
+
+PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
+    if (int e = heads_check("pmlp_heads_backward", njobs, jobs, M, H, true)) return e;
+    const HeadJobs hj = heads_pack(njobs, jobs);
+    const dim3 g((M + HR - 1) / HR, njobs);
+    hipStream_t s = (hipStream_t)stream;
+    if (H == 32) hipLaunchKernelGGL(k_heads_bwd<32>, g, dim3(HR), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL(k_heads_bwd<64>, g, dim3(HR), 0, s, hj, M);
+    else hipLaunchKernelGGL(k_heads_bwd<128>, g, dim3(HR), 0, s, hj, M);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_backward: ") + hipGetErrorString(e));
 }

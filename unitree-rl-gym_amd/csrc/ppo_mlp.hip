@@ -961,7 +961,8 @@ __global__ __launch_bounds__(PMLP_LOSS_THREADS) void k_ppo_loss_std(LossArgs a, 
 struct LossStepOut {
     float* partial;
     bf16 *dmu_b, *dmu_t, *dv_b, *dv_t;
-    int Ap, Vp;  // padded widths of the actor / critic output gradients
+    int Ap, Vp;  // padded widths of the actor / critic output gradients (0: no bf16 output)
+    float *dmu_f, *dv_f;  // optional fp32 output gradients [M, A] and [M] (the recurrent heads)
 };
 __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o) {
     const int i = blockIdx.x * 64 + threadIdx.x;
@@ -998,6 +999,12 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
             o.dmu_b[(size_t)i * o.Ap + k] = (bf16)g;
             if (o.dmu_t) o.dmu_t[(size_t)k * a.M + i] = (bf16)g;
         }
+        if (o.dmu_f)
+            for (int k = 0; k < a.A; ++k) {
+                const float sg = a.stdv[k];
+                const float d = a.actions[si * a.A + k] - a.mu[(size_t)i * a.A + k];
+                o.dmu_f[(size_t)i * a.A + k] = dlogp * d / (sg * sg);
+            }
         const float v = a.value[i], r = a.ret[si];
         float dv;
         if (a.clipped_value) {
@@ -1016,6 +1023,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step(LossArgs a, LossStepOut o)
             o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
             if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
         }
+        if (o.dv_f) o.dv_f[i] = dv;
     }
     auto wsum = [](float x) {
 #pragma unroll
@@ -1128,6 +1136,11 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
             }
             *(bf16x8*)(o.dmu_b + (size_t)i * o.Ap + k) = g;
         }
+        if (o.dmu_f) {
+#pragma unroll
+            for (int kk = 0; kk < AM; ++kk)
+                if (kk < A) o.dmu_f[(size_t)i * A + kk] = dlogp * d[kk] * c_i2[kk];
+        }
         const float v = a.value[i], r = a.ret[si];
         float dv;
         const float gvc = a.vcoef / (float)a.M;
@@ -1147,6 +1160,7 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
             o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
             if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
         }
+        if (o.dv_f) o.dv_f[i] = dv;
     } else {
 #pragma unroll
         for (int k = 0; k < AM; ++k) d[k] = 0.f;
@@ -1260,6 +1274,11 @@ __global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut
         for (int k = q; k < o.Vp; k += 4) {
             o.dv_b[(size_t)i * o.Vp + k] = (bf16)(k == 0 ? dv : 0.f);
             if (o.dv_t) o.dv_t[(size_t)k * a.M + i] = (bf16)(k == 0 ? dv : 0.f);
+        }
+        if (o.dv_f && q == 0) o.dv_f[i] = dv;
+        if (o.dmu_f && own) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o.dmu_f[(size_t)i * A + k0 + u] = dlogp * d[u] * c_i2[k0 + u];
         }
         if (q == 0) {  // the row's scalars counted once
             surr = fmaxf(s1, s2);
@@ -2315,19 +2334,8 @@ PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const u
 
 PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A) { return ((M + 63) / 64) * (3 + A); }
 
-PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float* value, const float* actions,
-                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
-                                const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
-                                float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
-                                float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
-                                pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream) {
-    LossArgs a;
-    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
-                          clipped_value, vcoef, ecoef))
-        return e;
-    if (!partial || !stats || !dstd || !dmu || !dvalue || Ap < A || Vp < 1)
-        return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
-    LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp};
+static int loss_step_launch(const LossArgs& a, const LossStepOut& o, int M, int A, int Ap, float* partial,
+                            float* stats, float* dstd, void* stream) {
     const int nb = (M + 63) / 64;
     if (A % 4 == 0 && A <= 16 && Ap <= 16 && Ap % 4 == 0)
         hipLaunchKernelGGL(k_ppo_loss_step_q, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, o);
@@ -2340,5 +2348,39 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
     PMLP_CHECK_LAUNCH("pmlp_ppo_loss_step");
     return 0;
 }
+
+PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float* value, const float* actions,
+                                const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,
+                                const float* ret, const float* target, const int64_t* rows, int32_t M, int32_t A,
+                                float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
+                                float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
+                                pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream) {
+    LossArgs a;
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
+                          clipped_value, vcoef, ecoef))
+        return e;
+    if (!partial || !stats || !dstd || !dmu || !dvalue || Ap < A || Vp < 1)
+        return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
+    LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp, nullptr, nullptr};
+    return loss_step_launch(a, o, M, A, Ap, partial, stats, dstd, stream);
+}
+
+PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const float* value, const float* actions,
+                                    const float* old_logp, const float* old_mu, const float* old_sigma,
+                                    const float* adv, const float* ret, const float* target, const int64_t* rows,
+                                    int32_t M, int32_t A, float clip, int32_t clipped_value, float vcoef, float ecoef,
+                                    float* partial, float* stats, float* dstd, float* dmu, float* dvalue,
+                                    void* stream) {
+    LossArgs a;
+    if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
+                          clipped_value, vcoef, ecoef))
+        return e;
+    if (!partial || !stats || !dstd || !dmu || !dvalue) return fail(-1, "pmlp_ppo_loss_step_f32: null output");
+    if (A % 4 == 0 && ((uintptr_t)dmu & 15)) return fail(-1, "pmlp_ppo_loss_step_f32: dmu 16-byte aligned");
+    LossStepOut o{partial, nullptr, nullptr, nullptr, nullptr, 0, 0, dmu, dvalue};
+    return loss_step_launch(a, o, M, A, 0, partial, stats, dstd, stream);
+}
+
+
 
 }  // extern "C"

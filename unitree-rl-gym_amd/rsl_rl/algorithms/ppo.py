@@ -19,7 +19,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.optim as optim
 
-from rsl_rl.algorithms import fused_step
+from rsl_rl.algorithms import fused_recurrent, fused_step
 from rsl_rl.modules import ActorCritic
 from rsl_rl.modules import mfma_mlp
 from rsl_rl.storage import RolloutStorage
@@ -89,6 +89,8 @@ class PPO:
         # the torch statement of the loss, _reference_loss)
         self._fused_loss = bool(fused_loss) and on_gpu and hasattr(self.actor_critic, "mean_and_value")
         self._fused = None  # FusedPPOStep, built with the storage (init_storage)
+        self._rfused = None  # FusedRecurrentStep (recurrent policies), likewise
+        self._rgraph = None
         self._rollout = None  # FusedRollout: act/process_env_step of the same policy
         self._stored_t = None  # storage row the fused act() filled, awaiting process_env_step
         self._fgraph = None
@@ -123,6 +125,10 @@ class PPO:
                 self._rollout = fused_step.FusedRollout(self._fused, num_envs) if num_envs % 8 == 0 else None
             except ValueError:
                 self._fused = self._rollout = None
+        if self._fused_loss and self._dense_recurrent and self._rfused is None and \
+                fused_recurrent.supported(self.actor_critic, num_envs, self.num_mini_batches):
+            # the recurrent optimizer step without autograd (algorithms/fused_recurrent.py)
+            self._rfused = fused_recurrent.FusedRecurrentStep(self, num_envs, num_transitions_per_env)
         if self.actor_critic.is_recurrent and self._rollout is None and str(self.device).startswith("cuda") and \
                 hasattr(self.actor_critic, "rollout_capturable"):
             self._rollout = fused_step.RecurrentRollout(self, num_envs)
@@ -387,6 +393,8 @@ class PPO:
         self._graph_calls += 1
         if self._fused is not None:
             acc = self._update_fused()
+        elif self._rfused is not None:
+            acc = self._update_rfused()
         elif self.use_graph and self._graph_calls >= 2:  # first call runs eagerly (warm-up)
             acc = self._update_graphed()
         else:
@@ -447,6 +455,39 @@ class PPO:
             self._fgraph = graph
         self._fgraph.replay()
         return self._facc
+
+    def _update_rfused(self):
+        """The recurrent update as num_epochs x num_mini_batches FusedRecurrentStep.run calls
+        over the dense mini-batches (contiguous env slices, as rsl_rl's recurrent generator),
+        replayed as one HIP graph from the second call on."""
+        rf, st = self._rfused, self.storage
+        rf.sync_optimizer_state(self.optimizer)
+        if not hasattr(self, "_racc"):
+            self._racc = torch.zeros(2, device=self.device)
+            self._radv = st.advantages
+        if st.advantages.data_ptr() != self._radv.data_ptr():  # the captured graph reads this buffer
+            self._radv.copy_(st.advantages)
+            st.advantages = self._radv
+
+        def body():
+            self._racc.zero_()
+            for batch in st.recurrent_dense_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs):
+                rf.run(batch, self._racc)
+
+        if not (self.use_graph and self._graph_calls >= 2):
+            body()
+            return self._racc
+        if self._rgraph is None:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            graph = torch.cuda.CUDAGraph()
+            if not self._capture(graph, side, body):
+                body()
+                return self._racc
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            self._rgraph = graph
+        self._rgraph.replay()
+        return self._racc
 
     def _capture(self, graph, stream, body):
         """Record body() into graph on stream.  A capture that fails (e.g. a collective

@@ -67,6 +67,12 @@ class MlpFwdJob(C.Structure):
                 ("ldo", C.c_int32)]
 
 
+class HeadJob(C.Structure):
+    _fields_ = [("h", C.c_void_p), ("W0", C.c_void_p), ("b0", C.c_void_p), ("W1", C.c_void_p), ("b1", C.c_void_p),
+                ("y0", C.c_void_p), ("out", C.c_void_p), ("dout", C.c_void_p), ("dh", C.c_void_p),
+                ("slab", C.c_void_p), ("N0", C.c_int32), ("N1", C.c_int32)]
+
+
 MAX_JOBS, MAX_GEMM_JOBS = 16, 4
 PMLP_MAX_MIRROR = 8  # include/ppo_mlp.h: bf16 weight copies one Adam launch writes
 
@@ -108,6 +114,11 @@ def load():
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
+        L.pmlp_ppo_loss_step_f32.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
+        L.pmlp_heads_blocks.argtypes = [i32]
+        L.pmlp_heads_blocks.restype = i32
+        L.pmlp_heads_forward.argtypes = [i32, C.POINTER(HeadJob), i32, i32, vp]
+        L.pmlp_heads_backward.argtypes = [i32, C.POINTER(HeadJob), i32, i32, vp]
         _lib = L
     return _lib
 
