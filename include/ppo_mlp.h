@@ -332,5 +332,15 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
 PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* whh, const float* c0,
                                 const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
                                 float* dgx, void* stream);
+/* pmlp_lstm_bwd_mfma plus the three weight gradients (the fused recurrent step): per
+ * workgroup of 16 envs (pmlp_lstm_bwd_dw_blocks(B) of them) the partial sums over its envs
+ * and the T steps of dG^T [x | h_prev | 1] (xh: the rows pmlp_lstm_fwd_mfma wrote), as one
+ * slab row [dW_ih (4H x I) | dW_hh (4H x H) | db (4H)] of 4H (I + H + 1) floats in torch's
+ * row order (summed over the rows by pmlp_reduce_slabs; db is the gradient of b_ih and b_hh).
+ * The gate gradients themselves are not written.  H = 64, I + H + 1 <= 128.            */
+PMLP_API int32_t pmlp_lstm_bwd_dw_blocks(int32_t B);
+PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* whh, const float* c0,
+                                   const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
+                                   const float* xh, float* slab, void* stream);
 
 #endif

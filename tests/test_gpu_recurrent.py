@@ -179,8 +179,9 @@ def test_recurrent_ppo_update_matches_fp32_cpu_update():
         da, db = a.detach() - c, b.detach().cpu() - c
         assert da.abs().max() > 0, name
         # Adam turns a sign flip of a ~0 gradient into a ~lr move: a few entries may differ
-        bad = ((da - db).abs() > 0.1 * lr).float().mean().item()
-        assert bad < 0.02, (name, bad)
+        # (at most 2 %, or one entry of a small tensor such as the critic's 32 output weights)
+        nbad = int(((da - db).abs() > 0.1 * lr).sum())
+        assert nbad <= max(1, 0.02 * da.numel()), (name, nbad, da.numel())
         assert (da - db).abs().max() <= 2 * 20 * 1.5 * lr, name
 
 
@@ -386,3 +387,37 @@ def test_fused_recurrent_heads_match_torch(H):
         torch.testing.assert_close(bufs[n]["dh"], g[0], rtol=1e-5, atol=1e-5)
         want = torch.cat([t.reshape(-1) for t in g[1:]])
         torch.testing.assert_close(bufs[n]["grad"], want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("I", [41, 47, 17, 63])
+def test_lstm_bwd_accumulates_the_weight_gradients(I):
+    """pmlp_lstm_bwd_dw_mfma (the fused recurrent step's memory backward): the per-workgroup
+    partials of dG^T [x | h_prev | 1], summed over the slab rows, are the weight gradients of
+    torch autograd through the same recurrence (resets inside, a carried initial state; env
+    count not a multiple of the 16-env workgroups), within 1e-4 relative (norm)."""
+    from rsl_rl.modules import mfma_mlp as mm
+    torch.manual_seed(I)
+    T, B, H = 24, 1000, 64
+    rnn = torch.nn.LSTM(I, H).cuda()
+    x = torch.randn(T, B, I, device="cuda")
+    h0 = 0.5 * torch.randn(B, H, device="cuda")
+    c0 = 0.5 * torch.randn(B, H, device="cuda")
+    reset = (torch.rand(T, B, device="cuda") < 0.1).to(torch.uint8)
+    g = torch.randn(T, B, H, device="cuda")
+    L, P, st = lstm_seq._lib(), mm._p, mm._stream()
+    h_out, c_out = torch.empty(T, B, H, device="cuda"), torch.empty(T, B, H, device="cuda")
+    gact, xh = torch.empty(T, B, 4 * H, device="cuda"), torch.empty(T, B, I + H + 1, device="cuda")
+    w = [t.detach().contiguous() for t in (rnn.weight_ih_l0, rnn.bias_ih_l0, rnn.bias_hh_l0, rnn.weight_hh_l0)]
+    lstm_seq._ok(L.pmlp_lstm_fwd_mfma(T, B, H, I, P(x), P(w[0]), P(w[1]), P(w[2]), P(w[3]), P(h0), P(c0), P(reset),
+                                      P(h_out), P(c_out), P(gact), P(xh), st), "fwd")
+    nblk = L.pmlp_lstm_bwd_dw_blocks(B)
+    slab = torch.empty(nblk, 4 * H * (I + H + 1), device="cuda")
+    lstm_seq._ok(L.pmlp_lstm_bwd_dw_mfma(T, B, H, I, P(w[3]), P(c0), P(reset), P(c_out), P(gact), P(g), P(xh),
+                                         P(slab), st), "bwd_dw")
+    tot = slab.sum(0)
+    got = [tot[:4 * H * I].view(4 * H, I), tot[4 * H * I:4 * H * (I + H)].view(4 * H, H), tot[4 * H * (I + H):]]
+    y_ref = lstm_seq.lstm_dense_reference(rnn, x, h0, c0, reset)
+    want = torch.autograd.grad(y_ref, [rnn.weight_ih_l0, rnn.weight_hh_l0, rnn.bias_ih_l0], g)
+    for name, a, b in zip(("w_ih", "w_hh", "b"), got, want):
+        rel = float((a - b).norm() / b.norm())
+        assert rel < 1e-4, (name, rel)

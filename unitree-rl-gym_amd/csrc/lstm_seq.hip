@@ -534,13 +534,29 @@ struct MBwdArgs {
     const float *whh, *c0;
     const uint8_t* reset;
     const float *c_out, *gact, *dh_out;
-    float* dgx;
+    float* dgx;        // optional: the gate gradients [T, B, 4H]
+    const float* xh;   // DW: the forward's [x | h_prev | 1] rows [T, B, I + H + 1]
+    int I;
+    float* slab;       // DW: per workgroup [dW_ih (4H x I) | dW_hh (4H x H) | db (4H)], torch row order
 };
 
-template <int SPLIT>
+// DW: the three weight gradients dG^T [x | h_prev | 1] accumulate inside the backward as well:
+// per step the workgroup's 16 envs are the K of a [256 gates x 16] . [16 x (I + H + 1)]
+// product on v_mfma_f32_32x32x16_bf16 (split-bf16 operands, fp32 accumulators held over all T
+// steps; wave w owns gate-row tiles 2w, 2w + 1), written once per workgroup into its slab row
+// (summed over workgroups by pmlp_reduce_slabs): no [T, B, 4H] dgx round trip and no
+// separate 49k-row reduction GEMM.
+constexpr int MXC = 128;  // xh columns covered (I + H + 1 <= 128)
+typedef float mfloatx16 __attribute__((ext_vector_type(16)));
+
+template <int SPLIT, bool DW>
 __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     constexpr int NP = SPLIT == 3 ? 2 : 1;
     __shared__ __attribute__((aligned(16))) mbf16 G[NP][2][ME * MLDG];
+    // DW operands, transposed so a fragment is 8 consecutive envs (one 16-byte read):
+    // GT[perm gate col][env], XT[xh col][env]
+    __shared__ __attribute__((aligned(16))) mbf16 GT[DW ? NP : 1][2][DW ? MG * ME : 8];
+    __shared__ __attribute__((aligned(16))) mbf16 XT[DW ? NP : 1][2][DW ? MXC * ME : 8];
     const int T = a.T, B = a.B;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int e0 = blockIdx.x * ME;
@@ -589,10 +605,45 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     float dhn[4] = {0.f, 0.f, 0.f, 0.f}, dcn[4] = {0.f, 0.f, 0.f, 0.f};
     In nx;
     load(T - 1, nx);
+    // DW: the step's xh rows (16 envs x RL contiguous floats), loaded a step ahead
+    const int RL = a.I + MH + 1, nxe = min(ME, B - e0) * RL, nct = (RL + 31) / 32;
+    constexpr int XU = (ME * MXC + 255) / 256;
+    float xr[DW ? XU : 1];
+    auto xload = [&](int t) {
+        if constexpr (DW) {
+            const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL;
+#pragma unroll
+            for (int k = 0; k < XU; ++k) xr[k] = src[min(tid + 256 * k, nxe - 1)];
+        }
+    };
+    mfloatx16 dacc[DW ? 8 : 1];
+    if constexpr (DW) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dacc[i][r] = 0.f;
+        for (int i = tid; i < NP * 2 * MXC * ME; i += 256) (&XT[0][0][0])[i] = (mbf16)0.f;  // columns >= RL stay 0
+        __syncthreads();
+    }
+    xload(T - 1);
     for (int t = T - 1; t >= 0; --t) {
         const int buf = t & 1;
         const In v = nx;
         load(t - 1, nx);
+        if constexpr (DW) {  // this step's xh rows, transposed, split; then the next step's loads
+#pragma unroll
+            for (int k = 0; k < XU; ++k) {
+                const int i = tid + 256 * k;
+                if (i < ME * RL) {
+                    const int env = i / RL, col = i - env * RL;
+                    mbf16 hi, lo;
+                    split_bf16(i < nxe ? xr[k] : 0.f, hi, lo);
+                    XT[0][buf][col * ME + env] = hi;
+                    if constexpr (NP == 2) XT[NP - 1][buf][col * ME + env] = lo;
+                }
+            }
+            xload(t - 1);
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int ge = e0 + 4 * rg + p;
@@ -609,8 +660,10 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
             dg[3] = dh * tc * og * (1.f - og);
             dcn[p] = rs ? 0.f : dc * fg;  // into c_{t-1} (none across a reset)
             if (ge < B) {
-                float* o = a.dgx + ((size_t)t * B + ge) * MG;
-                o[u] = dg[0]; o[MH + u] = dg[1]; o[2 * MH + u] = dg[2]; o[3 * MH + u] = dg[3];
+                if (a.dgx) {
+                    float* o = a.dgx + ((size_t)t * B + ge) * MG;
+                    o[u] = dg[0]; o[MH + u] = dg[1]; o[2 * MH + u] = dg[2]; o[3 * MH + u] = dg[3];
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) dg[q] = 0.f;  // rows past B feed nothing
@@ -622,6 +675,11 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
                 const int o = (4 * rg + p) * MLDG + 64 * w + 16 * q + j;
                 G[0][buf][o] = hi;
                 if constexpr (NP == 2) G[NP - 1][buf][o] = lo;
+                if constexpr (DW) {
+                    const int ot = (64 * w + 16 * q + j) * ME + 4 * rg + p;
+                    GT[0][buf][ot] = hi;
+                    if constexpr (NP == 2) GT[NP - 1][buf][ot] = lo;
+                }
             }
         }
         __syncthreads();
@@ -650,20 +708,65 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
             const float d = (acc[0][0][p] + acc[1][0][p]) + ((acc[0][1][p] + acc[1][1][p]) + (acc[0][2][p] + acc[1][2][p]));
             dhn[p] = (has_reset && v.rs[p]) ? 0.f : d;
         }
+        if constexpr (DW) {  // dW += dG^T [x | h_prev | 1] over this step's 16 envs
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int ao = ((2 * w + mt) * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
+                const mbf16x8 ah = *(const mbf16x8*)(&GT[0][buf][ao]);
+                mbf16x8 al;
+                if constexpr (NP == 2) al = *(const mbf16x8*)(&GT[NP - 1][buf][ao]);
+#pragma unroll
+                for (int nt = 0; nt < MXC / 32; ++nt) {
+                    if (nt < nct) {
+                        const int bo = (nt * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
+                        const mbf16x8 bh = *(const mbf16x8*)(&XT[0][buf][bo]);
+                        mfloatx16& c = dacc[mt * 4 + nt];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+                        if constexpr (NP == 2) {
+                            const mbf16x8 bl = *(const mbf16x8*)(&XT[NP - 1][buf][bo]);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (DW) {  // this workgroup's partial weight gradients, torch row order
+        const int I = a.I;
+        float* sl = a.slab + (size_t)blockIdx.x * (size_t)MG * RL;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < MXC / 32; ++nt) {
+                const int n = nt * 32 + (lane & 31);
+                if (nt >= nct || n >= RL) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int gp = (2 * w + mt) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);  // permuted
+                    const int tr = ((gp >> 4) & 3) * MH + 16 * (gp >> 6) + (gp & 15);         // torch row
+                    const float x = dacc[mt * 4 + nt][r];
+                    if (n < I) sl[(size_t)tr * I + n] = x;
+                    else if (n < I + MH) sl[(size_t)MG * I + (size_t)tr * MH + (n - I)] = x;
+                    else sl[(size_t)MG * (I + MH) + tr] = x;
+                }
+            }
     }
 }
 
 // ------------------------------------------------------------ recurrent heads --
 // The MLP heads of ActorCriticRecurrent on the LSTM output (rsl_rl actor / critic:
-// Linear(H, N0) -> ELU -> Linear(N0, N1)), fp32, for the fused recurrent optimizer step:
-// one row per thread, HR rows per workgroup, the weights in LDS (every lane reads the same
-// entry: broadcasts), row tiles staged through LDS so every global access is coalesced.
+// Linear(H, N0) -> ELU -> Linear(N0, N1)), fp32, for the fused recurrent optimizer step.
+// A workgroup of 256 threads owns HR = 128 rows, two threads per row (each half of the row's
+// units); the weights sit in LDS (every lane reads the same entry: broadcasts) and the row
+// tiles are staged through LDS so every global access is coalesced.
 //   forward:  y0 = elu(W0 h + b0) [M, N0], out = W1 y0 + b1 [M, N1]
 //   backward: from dout [M, N1]: dz0 = (W1^T dout) * elu'(y0) (torch's form from the output:
 //             1 for y0 > 0, else y0 + 1), dh = W0^T dz0 [M, H] (the LSTM's output gradient),
 //             and per workgroup the partial sums of [dW0 | db0 | dW1 | db1] (the parameter
 //             order of the Sequential's two Linears) into slab row blockIdx.x.
-constexpr int HR = 128, HN0 = 32, HN1 = 16;  // rows per workgroup; max N0, N1 (rsl_rl configs: [32])
+// LDS stays under 80 KB at H = 64 (two workgroups, 8 waves per CU).
+constexpr int HR = 128, HT = 256, HN0 = 32, HN1 = 16;  // rows, threads per workgroup; max N0, N1
 
 struct HeadJob {
     const float *h, *W0, *b0, *W1, *b1;
@@ -676,167 +779,235 @@ struct HeadJobs {
     HeadJob j[2];
 };
 
+// Stage n consecutive floats (src[0..n), 0 < n <= U * HT) into LDS through put(i, v): every
+// thread's loads are issued before any is stored (unrolled to U), unconditionally at clamped
+// addresses (a load under a divergent branch gets a vmcnt(0) at the branch's end), so the
+// round trips overlap instead of a load -> wait -> load chain per element.
+template <int U, typename F>
+__device__ __forceinline__ void stage(const float* __restrict__ src, int n, F&& put) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min((int)threadIdx.x + u * HT, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * HT;
+        if (i < n) put(i, v[u]);
+    }
+}
+// the h rows r0 .. r0 + HR of [M, H] into an LDS tile of row stride LH (rows >= M zero)
+template <int H, int LH>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ h, int r0, int M, float* hs) {
+    constexpr int U = HR * H / 4 / HT;
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * HT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        v[u] = *(const float4*)(h + (size_t)min(r0 + r, M - 1) * H + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * HT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        *(float4*)(hs + r * LH + c) = r0 + r < M ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+// a [rows, N] row-major span (N <= 32 runtime) into an LDS tile of row stride L, zero past M
+template <int UMAX, int L>
+__device__ __forceinline__ void stage_span(const float* __restrict__ src, int N, int r0, int M, float* t) {
+    const int nr = min(HR, M - r0);
+    for (int i = threadIdx.x; i < HR * N; i += HT) t[(i / N) * L + i % N] = 0.f;
+    stage<UMAX>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
+}
+
 template <int H>
-__global__ __launch_bounds__(HR) void k_heads_fwd(HeadJobs jobs, int M) {
+__global__ __launch_bounds__(HT) void k_heads_fwd(HeadJobs jobs, int M) {
     const HeadJob& J = jobs.j[blockIdx.y];
     const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
+    const int row = tid & (HR - 1), half = tid / HR;
     constexpr int LH = H + 4, LY = HN0 + 1, LO = HN1 + 1;
     constexpr int HS = HR * LH > HR * (LY + LO) ? HR * LH : HR * (LY + LO);  // h tile, then y0 + out
     __shared__ __attribute__((aligned(16))) float hs[HS];
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float bb0[HN0], w1[HN1 * HN0], bb1[HN1];
-    for (int i = tid; i < N0 * H; i += HR) w0[i] = J.W0[i];
-    for (int i = tid; i < N1 * N0; i += HR) w1[i] = J.W1[i];
+    stage<HN0 * H / HT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
+    stage<(HN1 * HN0 + HT - 1) / HT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
     if (tid < N0) bb0[tid] = J.b0[tid];
     if (tid < N1) bb1[tid] = J.b1[tid];
-    for (int i = tid; i < HR * (H / 4); i += HR) {  // the h rows, coalesced
-        const int r = i / (H / 4), c = (i % (H / 4)) * 4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r0 + r < M) v = *(const float4*)(J.h + (size_t)(r0 + r) * H + c);
-        *(float4*)(hs + r * LH + c) = v;
-    }
+    stage_rows<H, LH>(J.h, r0, M, hs);
     __syncthreads();
     float hr[H];
 #pragma unroll
     for (int k = 0; k < H; k += 4) {
-        const float4 v = *(const float4*)(hs + tid * LH + k);
+        const float4 v = *(const float4*)(hs + row * LH + k);
         hr[k] = v.x; hr[k + 1] = v.y; hr[k + 2] = v.z; hr[k + 3] = v.w;
     }
-    float o[HN1];
-#pragma unroll
-    for (int i = 0; i < HN1; ++i) o[i] = 0.f;
     __syncthreads();  // (hs is reused for the y0 tile below)
-    for (int j = 0; j < N0; ++j) {
-        float z = bb0[j];
+    // y0: this thread's half of the units, one at a time (four FMA chains over k mod 4)
+    const int nh = N0 / 2, jb = half * nh;
+#pragma unroll 1
+    for (int j = jb; j < jb + nh; ++j) {
+        float z[4] = {bb0[j], 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < H; k += 4) {
             const float4 w = *(const float4*)(w0 + j * H + k);
-            z = fmaf(w.x, hr[k], z); z = fmaf(w.y, hr[k + 1], z); z = fmaf(w.z, hr[k + 2], z); z = fmaf(w.w, hr[k + 3], z);
+            z[0] = fmaf(w.x, hr[k], z[0]); z[1] = fmaf(w.y, hr[k + 1], z[1]);
+            z[2] = fmaf(w.z, hr[k + 2], z[2]); z[3] = fmaf(w.w, hr[k + 3], z[3]);
         }
-        const float y = z > 0.f ? z : expm1f(z);
-        hs[tid * LY + j] = y;
-#pragma unroll
-        for (int i = 0; i < HN1; ++i)
-            if (i < N1) o[i] = fmaf(w1[i * N0 + j], y, o[i]);
+        const float zz = (z[0] + z[1]) + (z[2] + z[3]);
+        hs[row * LY + j] = zz > 0.f ? zz : expm1f(zz);
     }
-    float* os = hs + HR * LY;  // [HR][LO]
-#pragma unroll
-    for (int i = 0; i < HN1; ++i)
-        if (i < N1) os[tid * LO + i] = o[i] + bb1[i];
     __syncthreads();
-    for (int i = tid; i < HR * N0; i += HR) {  // coalesced row-major stores
+    // out: this thread's outputs i = half, half + 2, ... over the row's y0 (LDS)
+    float* os = hs + HR * LY;  // [HR][LO]
+#pragma unroll 1
+    for (int i = half; i < N1; i += 2) {
+        float a[4] = {bb1[i], 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int j = 0; j < N0; j += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = fmaf(w1[i * N0 + j + u], hs[row * LY + j + u], a[u]);
+        }
+        os[row * LO + i] = (a[0] + a[1]) + (a[2] + a[3]);
+    }
+    __syncthreads();
+    for (int i = tid; i < HR * N0; i += HT) {  // coalesced row-major stores
         const int r = i / N0, c = i - r * N0;
         if (r0 + r < M) J.y0[(size_t)(r0 + r) * N0 + c] = hs[r * LY + c];
     }
-    for (int i = tid; i < HR * N1; i += HR) {
+    for (int i = tid; i < HR * N1; i += HT) {
         const int r = i / N1, c = i - r * N1;
         if (r0 + r < M) J.out[(size_t)(r0 + r) * N1 + c] = os[r * LO + c];
     }
 }
 
 template <int H>
-__global__ __launch_bounds__(HR) void k_heads_bwd(HeadJobs jobs, int M) {
+__global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
     const HeadJob& J = jobs.j[blockIdx.y];
     const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
-    constexpr int LH = H + 4, LZ = HN0 + 4, LY = HN0 + 1, LO = HN1 + 1;
-    __shared__ __attribute__((aligned(16))) float hs[HR * LH];   // h, then dh
-    __shared__ __attribute__((aligned(16))) float zs[HR * LZ];   // dz0
-    __shared__ float ys[HR * LY], ds[HR * LO];                    // y0, dout
+    const int row = tid & (HR - 1), half = tid / HR;
+    constexpr int LH = H + 4, LZ = HN0 + 4, LO = HN1 + 1;
+    __shared__ __attribute__((aligned(16))) float hs[HR * LH];   // h, then dW0 halves, then dh
+    __shared__ __attribute__((aligned(16))) float zs[HR * LZ];   // y0, then dz0
+    __shared__ float ds[HR * LO];                                 // dout
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float w1[HN1 * HN0];
-    for (int i = tid; i < N0 * H; i += HR) w0[i] = J.W0[i];
-    for (int i = tid; i < N1 * N0; i += HR) w1[i] = J.W1[i];
-    for (int i = tid; i < HR * (H / 4); i += HR) {
-        const int r = i / (H / 4), c = (i % (H / 4)) * 4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r0 + r < M) v = *(const float4*)(J.h + (size_t)(r0 + r) * H + c);
-        *(float4*)(hs + r * LH + c) = v;
-    }
-    for (int i = tid; i < HR * N0; i += HR) {
-        const int r = i / N0, c = i - r * N0;
-        ys[r * LY + c] = r0 + r < M ? J.y0[(size_t)(r0 + r) * N0 + c] : 0.f;
-    }
-    for (int i = tid; i < HR * N1; i += HR) {
-        const int r = i / N1, c = i - r * N1;
-        ds[r * LO + c] = r0 + r < M ? J.dout[(size_t)(r0 + r) * N1 + c] : 0.f;
-    }
+    stage<HN0 * H / HT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
+    stage<(HN1 * HN0 + HT - 1) / HT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
+    stage_rows<H, LH>(J.h, r0, M, hs);
+    stage_span<HR * HN0 / HT, LZ>(J.y0, N0, r0, M, zs);
+    stage_span<HR * HN1 / HT, LO>(J.dout, N1, r0, M, ds);
     __syncthreads();
-    // the row's dz0 (registers and the LDS tile)
-    float dz[HN0];
-    {
-        float d[HN1];
-#pragma unroll
-        for (int i = 0; i < HN1; ++i) d[i] = i < N1 ? ds[tid * LO + i] : 0.f;
-#pragma unroll
-        for (int j = 0; j < HN0; ++j) {
-            float g = 0.f;
-            if (j < N0) {
-#pragma unroll
-                for (int i = 0; i < HN1; ++i)
-                    if (i < N1) g = fmaf(w1[i * N0 + j], d[i], g);
-                const float y = ys[tid * LY + j];
-                g = y > 0.f ? g : g * (y + 1.f);
-            }
-            dz[j] = g;
-            zs[tid * LZ + j] = g;
-        }
-    }
-    __syncthreads();
-    // partial weight gradients of this workgroup's rows (fixed order: deterministic)
     float* sl = J.slab + (size_t)blockIdx.x * (N0 * H + N0 + N1 * N0 + N1);
-    for (int t = tid; t < (N0 / 4) * (H / 4); t += HR) {  // dW0, 4 x 4 per thread
-        const int j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
-        float a[4][4] = {};
-        for (int r = 0; r < HR; ++r) {
-            const float4 z4 = *(const float4*)(zs + r * LZ + j0);
-            const float4 h4 = *(const float4*)(hs + r * LH + k0);
-            const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) a[u][v] = fmaf(zz[u], hh[v], a[u][v]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            *(float4*)(sl + (size_t)(j0 + u) * H + k0) = make_float4(a[u][0], a[u][1], a[u][2], a[u][3]);
-    }
-    for (int j = tid; j < N0; j += HR) {  // db0
-        float a = 0.f;
-        for (int r = 0; r < HR; ++r) a += zs[r * LZ + j];
-        sl[N0 * H + j] = a;
-    }
-    for (int t = tid; t < N1 * N0; t += HR) {  // dW1
+    // dW1 (+ db1 on j = 0) from the y0 and dout tiles, before y0 is overwritten
+    for (int t = tid; t < N1 * N0; t += HT) {
         const int i = t / N0, j = t - i * N0;
-        float a = 0.f;
-        for (int r = 0; r < HR; ++r) a = fmaf(ds[r * LO + i], ys[r * LY + j], a);
+        float a = 0.f, b = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < HR; ++r) {
+            const float d = ds[r * LO + i];
+            a = fmaf(d, zs[r * LZ + j], a);
+            b += d;
+        }
         sl[N0 * H + N0 + t] = a;
+        if (j == 0) sl[N0 * H + N0 + N1 * N0 + i] = b;
     }
-    for (int i = tid; i < N1; i += HR) {  // db1
-        float a = 0.f;
-        for (int r = 0; r < HR; ++r) a += ds[r * LO + i];
-        sl[N0 * H + N0 + N1 * N0 + i] = a;
+    // dz0 of this thread's half of the row's units (registers), W1^T dout over the rows of W1
+    const int nh = N0 / 2, jb = half * nh;
+    float dz[HN0 / 2];
+#pragma unroll
+    for (int u = 0; u < HN0 / 2; ++u) dz[u] = 0.f;
+    for (int i = 0; i < N1; ++i) {
+        const float di = ds[row * LO + i];
+#pragma unroll
+        for (int u = 0; u < HN0 / 2; ++u)
+            if (u < nh) dz[u] = fmaf(w1[i * N0 + jb + u], di, dz[u]);
     }
-    __syncthreads();  // every read of the h tile is done: it takes dh
-    {
-        float dh[H];
 #pragma unroll
-        for (int k = 0; k < H; ++k) dh[k] = 0.f;
+    for (int u = 0; u < HN0 / 2; ++u) {
+        if (u < nh) {
+            const float y = zs[row * LZ + jb + u];
+            dz[u] = y > 0.f ? dz[u] : dz[u] * (y + 1.f);
+        }
+    }
+    __syncthreads();  // every read of the y0 tile is done
 #pragma unroll
-        for (int j = 0; j < HN0; ++j) {
-            if (j < N0) {
+    for (int u = 0; u < HN0 / 2; ++u)
+        if (u < nh) zs[row * LZ + jb + u] = dz[u];
+    __syncthreads();
+    // dW0 (+ db0 on k0 = 0): 4 x 4 tiles, each over one half of the rows; the second half's
+    // partial goes through LDS (over the h tile) and the first adds it (fixed order)
+    const int ntile = (N0 / 4) * (H / 4);  // one tile per thread pair and pass
+    float* part = hs;  // [HR][20]: the h tile, after its last read (dh overwrites it later)
+    static_assert(HR * 20 <= HR * LH, "dW0 partials fit the h tile");
+    for (int tb = 0; tb < ntile; tb += HR) {
+        float a[4][4] = {}, bs[4] = {};
+        const int t = tb + row, j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
+        if (t < ntile) {
+            const int rb = half * (HR / 2);
+#pragma unroll 4
+            for (int r = rb; r < rb + HR / 2; ++r) {
+                const float4 z4 = *(const float4*)(zs + r * LZ + j0);
+                const float4 h4 = *(const float4*)(hs + r * LH + k0);
+                const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
-                for (int k = 0; k < H; k += 4) {
-                    const float4 w = *(const float4*)(w0 + j * H + k);
-                    dh[k] = fmaf(w.x, dz[j], dh[k]); dh[k + 1] = fmaf(w.y, dz[j], dh[k + 1]);
-                    dh[k + 2] = fmaf(w.z, dz[j], dh[k + 2]); dh[k + 3] = fmaf(w.w, dz[j], dh[k + 3]);
+                for (int u = 0; u < 4; ++u) {
+                    bs[u] += zz[u];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) a[u][v] = fmaf(zz[u], hh[v], a[u][v]);
                 }
             }
         }
+        __syncthreads();  // every read of the h tile in this pass is done
+        if (half == 1 && t < ntile) {
 #pragma unroll
-        for (int k = 0; k < H; k += 4) *(float4*)(hs + tid * LH + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) part[row * 20 + 4 * u + v] = a[u][v];
+                part[row * 20 + 16 + u] = bs[u];
+            }
+        }
+        __syncthreads();
+        if (half == 0 && t < ntile) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) a[u][v] += part[row * 20 + 4 * u + v];
+                bs[u] += part[row * 20 + 16 + u];
+                *(float4*)(sl + (size_t)(j0 + u) * H + k0) = make_float4(a[u][0], a[u][1], a[u][2], a[u][3]);
+            }
+            if (k0 == 0)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sl[N0 * H + j0 + u] = bs[u];
+        }
+        if (tb + HR < ntile) {  // the next pass reads the h tile again: restage it
+            __syncthreads();
+            stage_rows<H, LH>(J.h, r0, M, hs);
+            __syncthreads();
+        }
+    }
+    // dh: this thread's half of the row's H entries, over all N0 units (dz0 from the tile)
+    {
+        constexpr int HH = H / 2;
+        const int kb = half * HH;
+        float dh[HH];
+#pragma unroll
+        for (int k = 0; k < HH; ++k) dh[k] = 0.f;
+#pragma unroll 1
+        for (int j = 0; j < N0; ++j) {
+            const float zj = zs[row * LZ + j];
+#pragma unroll
+            for (int k = 0; k < HH; k += 4) {
+                const float4 w = *(const float4*)(w0 + j * H + kb + k);
+                dh[k] = fmaf(w.x, zj, dh[k]); dh[k + 1] = fmaf(w.y, zj, dh[k + 1]);
+                dh[k + 2] = fmaf(w.z, zj, dh[k + 2]); dh[k + 3] = fmaf(w.w, zj, dh[k + 3]);
+            }
+        }
+        __syncthreads();  // every read of the h tile is done: it takes dh
+#pragma unroll
+        for (int k = 0; k < HH; k += 4)
+            *(float4*)(hs + row * LH + kb + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
     }
     __syncthreads();
-    for (int i = tid; i < HR * (H / 4); i += HR) {
+    for (int i = tid; i < HR * (H / 4); i += HT) {
         const int r = i / (H / 4), c = (i % (H / 4)) * 4;
         if (r0 + r < M) *(float4*)(J.dh + (size_t)(r0 + r) * H + c) = *(const float4*)(hs + r * LH + c);
     }
@@ -965,11 +1136,26 @@ PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* wh
                                 float* dgx, void* stream) {
     if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !dgx) return fail("pmlp_lstm_bwd_mfma: null buffer");
     if (H != MH) return fail("pmlp_lstm_bwd_mfma: hidden 64");
-    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, dgx};
-    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_bwd_mfma<1>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(k_lstm_bwd_mfma<3>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, dgx, nullptr, 0, nullptr};
+    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_mfma: ") + hipGetErrorString(e));
+}
+
+PMLP_API int32_t pmlp_lstm_bwd_dw_blocks(int32_t B) { return (B + ME - 1) / ME; }
+
+PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* whh, const float* c0,
+                                   const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
+                                   const float* xh, float* slab, void* stream) {
+    if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !xh || !slab)
+        return fail("pmlp_lstm_bwd_dw_mfma: null buffer");
+    if (H != MH || I <= 0 || I + MH + 1 > MXC) return fail("pmlp_lstm_bwd_dw_mfma: hidden 64, I + 65 <= 128");
+    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, nullptr, xh, I, slab};
+    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, true>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma: ") + hipGetErrorString(e));
 }
 
 /* The recurrent policy's MLP heads (include/ppo_mlp.h, "recurrent heads"). */
@@ -978,8 +1164,8 @@ static int heads_check(const char* w, int njobs, const pmlp_head_job* jobs, int 
     if (H != 32 && H != 64 && H != 128) return fail(std::string(w) + ": H must be 32, 64 or 128");
     for (int i = 0; i < njobs; ++i) {
         const pmlp_head_job& J = jobs[i];
-        if (J.N0 <= 0 || J.N0 > HN0 || J.N0 % 4 || J.N1 <= 0 || J.N1 > HN1)
-            return fail(std::string(w) + ": 0 < N0 <= 32 (a multiple of 4), 0 < N1 <= 16");
+        if (J.N0 <= 0 || J.N0 > HN0 || J.N0 % 8 || J.N1 <= 0 || J.N1 > HN1)
+            return fail(std::string(w) + ": 0 < N0 <= 32 (a multiple of 8), 0 < N1 <= 16");
         if (!J.h || !J.W0 || !J.W1 || ((uintptr_t)J.h & 15u) || ((uintptr_t)J.W0 & 15u))
             return fail(std::string(w) + ": null or unaligned h / W0 / W1");
         if (!bwd && (!J.b0 || !J.b1 || !J.y0 || !J.out)) return fail(std::string(w) + ": null b0 / b1 / y0 / out");
@@ -1005,9 +1191,9 @@ PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_
     const HeadJobs hj = heads_pack(njobs, jobs);
     const dim3 g((M + HR - 1) / HR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL(k_heads_fwd<32>, g, dim3(HR), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL(k_heads_fwd<64>, g, dim3(HR), 0, s, hj, M);
-    else hipLaunchKernelGGL(k_heads_fwd<128>, g, dim3(HR), 0, s, hj, M);
+    if (H == 32) hipLaunchKernelGGL(k_heads_fwd<32>, g, dim3(HT), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL(k_heads_fwd<64>, g, dim3(HT), 0, s, hj, M);
+    else hipLaunchKernelGGL(k_heads_fwd<128>, g, dim3(HT), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward: ") + hipGetErrorString(e));
 }
@@ -1017,9 +1203,9 @@ PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32
     const HeadJobs hj = heads_pack(njobs, jobs);
     const dim3 g((M + HR - 1) / HR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL(k_heads_bwd<32>, g, dim3(HR), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL(k_heads_bwd<64>, g, dim3(HR), 0, s, hj, M);
-    else hipLaunchKernelGGL(k_heads_bwd<128>, g, dim3(HR), 0, s, hj, M);
+    if (H == 32) hipLaunchKernelGGL(k_heads_bwd<32>, g, dim3(HT), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL(k_heads_bwd<64>, g, dim3(HT), 0, s, hj, M);
+    else hipLaunchKernelGGL(k_heads_bwd<128>, g, dim3(HT), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_backward: ") + hipGetErrorString(e));
 }

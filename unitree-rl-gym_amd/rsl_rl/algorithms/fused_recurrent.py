@@ -11,9 +11,9 @@ LSTM weight-gradient product, clip_grad_norm_'s per-tensor norms and torch's Ada
     1   both heads forward, fp32 (pmlp_heads_forward)
     2   the PPO loss and its fp32 output gradients (pmlp_ppo_loss_step_f32)
     1   both heads backward: the LSTM output gradients and per-block weight-gradient partials
-    1   the partials summed into the flat gradient (pmlp_reduce_slabs)
-    2   LSTM backward
-    2x  LSTM weight gradients dgx^T [x | h_prev | 1] (row-chunked product + chunk sum)
+    2   LSTM backward, each accumulating its weight gradients dG^T [x | h_prev | 1] on the
+        matrix cores into per-workgroup partials (pmlp_lstm_bwd_dw_mfma)
+    1   every partial (heads, memories) summed into the flat gradient (pmlp_reduce_slabs)
     2   grad-norm partials (+ step / adaptive LR / loss bookkeeping) and Adam
 Every parameter is a view of ONE flat fp32 buffer (each tensor starting on 16 bytes), the
 gradient a view of another (its 4-float tail: the loss statistics, all-reduced with it at
@@ -73,9 +73,10 @@ class FusedRecurrentStep:
         self.dev = dev
         # flat parameter layout: each head's [W0 | b0 | W1 | b1] contiguous (the slab order of
         # pmlp_heads_backward), every block / LSTM tensor starting on 16 bytes
+        # and each memory's [w_ih | w_hh | b_ih | b_hh] contiguous (the slab order of
+        # pmlp_lstm_bwd_dw_mfma, b_ih first)
         groups = [[s[0].weight, s[0].bias, s[2].weight, s[2].bias] for s in self.heads] + [[ac.std]] + \
-            [[r.weight_ih_l0] for r in self.rnns] + [[r.weight_hh_l0] for r in self.rnns] + \
-            [[r.bias_ih_l0] for r in self.rnns] + [[r.bias_hh_l0] for r in self.rnns]
+            [[r.weight_ih_l0, r.weight_hh_l0, r.bias_ih_l0, r.bias_hh_l0] for r in self.rnns]
         params = [p for g in groups for p in g]
         if sorted(map(id, params)) != sorted(map(id, ac.parameters())):
             raise ValueError("fused recurrent step: unexpected parameter set")
@@ -116,7 +117,7 @@ class FusedRecurrentStep:
         self.c_out = [f(T, mb, H) for _ in range(2)]
         self.gact = [f(T, mb, 4 * H) for _ in range(2)]
         self.xh = [f(T, mb, self.I[n] + H + 1) for n in range(2)]
-        self.dgx = [f(T, mb, 4 * H) for _ in range(2)]
+        self.dgx = [None if self.mfma_of(n) else f(T, mb, 4 * H) for n in range(2)]
         self.dh = [f(T, mb, H) for _ in range(2)]
         self.y0 = [f(M, self.N0[n]) for n in range(2)]
         self.out = [f(M, self.N1[n]) for n in range(2)]
@@ -127,10 +128,29 @@ class FusedRecurrentStep:
         self.slab = [f(self.nblk, self.nh[n]) for n in range(2)]
         self.loss_partial = f(lib.pmlp_ppo_loss_step_parts(M, self.N1[0]))
         self.opt_partial = f(lib.pmlp_opt_parts())
-        self.mfma = [lstm_seq.mfma_usable(self.rnns[n], torch.empty(1, self.I[n])) for n in range(2)]
+        self.mfma = [self.mfma_of(n) for n in range(2)]
         self._head_jobs = (mm.HeadJob * 2)(*[self._head_job(n) for n in range(2)])
-        self._red_jobs = [(self.slab[n], self.grad[self._offset[id(self.heads[n][0].weight)]:], self.nh[n], self.nblk)
-                          for n in range(2)]
+        # the memories' weight gradients: accumulated inside the matrix-core backward (one slab
+        # row per 16 envs); else the gate gradients and a row-chunked product (lstm_seq._rows_tn)
+        L = lstm_seq._lib()
+        self.lblk = L.pmlp_lstm_bwd_dw_blocks(mb)
+        self.lrow = [4 * H * (self.I[n] + H + 1) for n in range(2)]
+        self.lslab = [f(self.lblk, self.lrow[n]) if self.mfma[n] else None for n in range(2)]
+        red = [mm.ReduceJob(mm._p(self.slab[n]), mm._p(self.grad) + 4 * self._offset[id(self.heads[n][0].weight)],
+                            None, self.nh[n], self.nh[n], self.nblk, 0, 0) for n in range(2)]
+        for n in range(2):
+            if self.mfma[n]:
+                r = self.rnns[n]
+                red.append(mm.ReduceJob(mm._p(self.lslab[n]), mm._p(self.grad) + 4 * self._offset[id(r.weight_ih_l0)],
+                                        None, self.lrow[n], self.lrow[n], self.lblk, 0, 0))
+                red.append(mm.ReduceJob(mm._p(self.lslab[n]) + 4 * 4 * H * (self.I[n] + H),
+                                        mm._p(self.grad) + 4 * self._offset[id(r.bias_hh_l0)], None, self.lrow[n],
+                                        4 * H, self.lblk, 0, 0))
+        self._red_jobs = (mm.ReduceJob * len(red))(*red)
+
+    def mfma_of(self, n):
+        return lstm_seq.mfma_usable(self.rnns[n], torch.empty(1, self.rnns[n].input_size)) and \
+            self.rnns[n].input_size + self.H + 1 <= 128
 
     def _head_job(self, n):
         s, p = self.heads[n], mm._p
@@ -190,20 +210,24 @@ class FusedRecurrentStep:
                                           P(self.dout[1]), st), "pmlp_ppo_loss_step_f32")
         # 4. both heads backward: the memories' output gradients + weight-gradient partials
         mm._ok(lib.pmlp_heads_backward(2, self._head_jobs, M, H, st), "pmlp_heads_backward")
-        mm._reduce(self._red_jobs)
-        # 5. the memories backward; the three LSTM weight gradients from one product each
+        # 5. the memories backward, with their weight gradients (slab partials) on the matrix cores
         for n in range(2):
-            r = self.rnns[n]
+            r, I = self.rnns[n], self.I[n]
             c0 = hids[n][1].reshape(mb, H)
-            bwd = L.pmlp_lstm_bwd_mfma if self.mfma[n] else L.pmlp_lstm_bwd
-            lstm_seq._ok(bwd(T, mb, H, P(r.weight_hh_l0), P(c0), P(reset), P(self.c_out[n]), P(self.gact[n]),
-                             P(self.dh[n]), P(self.dgx[n]), st), "pmlp_lstm_bwd")
-            I = self.I[n]
+            if self.mfma[n]:
+                lstm_seq._ok(L.pmlp_lstm_bwd_dw_mfma(T, mb, H, I, P(r.weight_hh_l0), P(c0), P(reset),
+                                                     P(self.c_out[n]), P(self.gact[n]), P(self.dh[n]), P(self.xh[n]),
+                                                     P(self.lslab[n]), st), "pmlp_lstm_bwd_dw_mfma")
+                continue
+            lstm_seq._ok(L.pmlp_lstm_bwd(T, mb, H, P(r.weight_hh_l0), P(c0), P(reset), P(self.c_out[n]),
+                                         P(self.gact[n]), P(self.dh[n]), P(self.dgx[n]), st), "pmlp_lstm_bwd")
             dw = lstm_seq._rows_tn(self.dgx[n].view(M, 4 * H), self.xh[n].view(M, I + H + 1))
             self._gview[id(r.weight_ih_l0)].copy_(dw[:, :I])
             self._gview[id(r.weight_hh_l0)].copy_(dw[:, I:I + H])
             self._gview[id(r.bias_ih_l0)].copy_(dw[:, I + H])
             self._gview[id(r.bias_hh_l0)].copy_(dw[:, I + H])
+        # every slab (heads, memories) summed into the flat gradient in one launch
+        mm._ok(lib.pmlp_reduce_slabs(len(self._red_jobs), self._red_jobs, st), "pmlp_reduce_slabs")
         # 6. data-parallel: one bucket (gradient + loss statistics)
         scale = 1.0
         if alg.world_size > 1:

@@ -36,6 +36,9 @@ def _lib():
         L.pmlp_lstm_step.argtypes = [i32, i32] + [vp] * 6 + [vp]
         L.pmlp_lstm_fwd_mfma.argtypes = [i32, i32, i32, i32] + [vp] * 12 + [vp]
         L.pmlp_lstm_bwd_mfma.argtypes = [i32, i32, i32] + [vp] * 7 + [vp]
+        L.pmlp_lstm_bwd_dw_blocks.argtypes = [i32]
+        L.pmlp_lstm_bwd_dw_blocks.restype = i32
+        L.pmlp_lstm_bwd_dw_mfma.argtypes = [i32, i32, i32, i32] + [vp] * 8 + [vp]
         _bound = True
     return L
 
