@@ -374,6 +374,7 @@ constexpr int MLDG = MG + 8;                         // LDS row stride of dG (bf
 
 typedef __bf16 mbf16;
 typedef mbf16 mbf16x8 __attribute__((ext_vector_type(8)));
+typedef mbf16 mbf16x4 __attribute__((ext_vector_type(4)));
 typedef float mfloatx4 __attribute__((ext_vector_type(4)));
 
 // activations of the MFMA kernels: v_exp_f32 + v_rcp_f32 (a few ulp; tanh to ~1e-7 absolute)
@@ -605,15 +606,17 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     float dhn[4] = {0.f, 0.f, 0.f, 0.f}, dcn[4] = {0.f, 0.f, 0.f, 0.f};
     In nx;
     load(T - 1, nx);
-    // DW: the step's xh rows (16 envs x RL contiguous floats), loaded a step ahead
-    const int RL = a.I + MH + 1, nxe = min(ME, B - e0) * RL, nct = (RL + 31) / 32;
-    constexpr int XU = (ME * MXC + 255) / 256;
-    float xr[DW ? XU : 1];
+    // DW: the step's xh rows, loaded a step ahead: thread (column xc = tid % 128, env group
+    // xg = tid / 128) holds column xc of envs 8 xg .. 8 xg + 7 (each load instruction reads 64
+    // consecutive columns of one row: coalesced), stored transposed as one 16-byte run per part
+    const int RL = a.I + MH + 1, nenv = min(ME, B - e0), nct = (RL + 31) / 32;
+    const int xc = tid & (MXC - 1), xg = tid >> 7;
+    float xr[DW ? 8 : 1];
     auto xload = [&](int t) {
         if constexpr (DW) {
-            const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL;
+            const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL + min(xc, RL - 1);
 #pragma unroll
-            for (int k = 0; k < XU; ++k) xr[k] = src[min(tid + 256 * k, nxe - 1)];
+            for (int k = 0; k < 8; ++k) xr[k] = src[(size_t)min(8 * xg + k, nenv - 1) * RL];
         }
     };
     mfloatx16 dacc[DW ? 8 : 1];
@@ -630,17 +633,19 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
         const int buf = t & 1;
         const In v = nx;
         load(t - 1, nx);
+        mbf16x4 gth[4], gtl[4];
         if constexpr (DW) {  // this step's xh rows, transposed, split; then the next step's loads
+            if (xc < RL) {  // (columns >= RL stay zero)
+                mbf16x8 hi8, lo8;
 #pragma unroll
-            for (int k = 0; k < XU; ++k) {
-                const int i = tid + 256 * k;
-                if (i < ME * RL) {
-                    const int env = i / RL, col = i - env * RL;
+                for (int k = 0; k < 8; ++k) {
                     mbf16 hi, lo;
-                    split_bf16(i < nxe ? xr[k] : 0.f, hi, lo);
-                    XT[0][buf][col * ME + env] = hi;
-                    if constexpr (NP == 2) XT[NP - 1][buf][col * ME + env] = lo;
+                    split_bf16(8 * xg + k < nenv ? xr[k] : 0.f, hi, lo);
+                    hi8[k] = hi;
+                    lo8[k] = lo;
                 }
+                *(mbf16x8*)(&XT[0][buf][xc * ME + 8 * xg]) = hi8;
+                if constexpr (NP == 2) *(mbf16x8*)(&XT[NP - 1][buf][xc * ME + 8 * xg]) = lo8;
             }
             xload(t - 1);
         }
@@ -676,10 +681,17 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
                 G[0][buf][o] = hi;
                 if constexpr (NP == 2) G[NP - 1][buf][o] = lo;
                 if constexpr (DW) {
-                    const int ot = (64 * w + 16 * q + j) * ME + 4 * rg + p;
-                    GT[0][buf][ot] = hi;
-                    if constexpr (NP == 2) GT[NP - 1][buf][ot] = lo;
+                    gth[q][p] = hi;
+                    gtl[q][p] = lo;
                 }
+            }
+        }
+        if constexpr (DW) {  // dG^T: the lane's 4 envs of each gate column, one 8-byte run per part
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ot = (64 * w + 16 * q + j) * ME + 4 * rg;
+                *(mbf16x4*)(&GT[0][buf][ot]) = gth[q];
+                if constexpr (NP == 2) *(mbf16x4*)(&GT[NP - 1][buf][ot]) = gtl[q];
             }
         }
         __syncthreads();
@@ -709,27 +721,32 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
             dhn[p] = (has_reset && v.rs[p]) ? 0.f : d;
         }
         if constexpr (DW) {  // dW += dG^T [x | h_prev | 1] over this step's 16 envs
+            // operands of the wave's 2 x 4 tiles, then the products pass by pass (consecutive
+            // MFMAs on different accumulators)
+            mbf16x8 ah[2], al[2], bh[4], bl[4];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 const int ao = ((2 * w + mt) * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
-                const mbf16x8 ah = *(const mbf16x8*)(&GT[0][buf][ao]);
-                mbf16x8 al;
-                if constexpr (NP == 2) al = *(const mbf16x8*)(&GT[NP - 1][buf][ao]);
-#pragma unroll
-                for (int nt = 0; nt < MXC / 32; ++nt) {
-                    if (nt < nct) {
-                        const int bo = (nt * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
-                        const mbf16x8 bh = *(const mbf16x8*)(&XT[0][buf][bo]);
-                        mfloatx16& c = dacc[mt * 4 + nt];
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-                        if constexpr (NP == 2) {
-                            const mbf16x8 bl = *(const mbf16x8*)(&XT[NP - 1][buf][bo]);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-                        }
-                    }
-                }
+                ah[mt] = *(const mbf16x8*)(&GT[0][buf][ao]);
+                if constexpr (NP == 2) al[mt] = *(const mbf16x8*)(&GT[NP - 1][buf][ao]);
             }
+#pragma unroll
+            for (int nt = 0; nt < MXC / 32; ++nt) {
+                const int bo = (nt * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
+                bh[nt] = *(const mbf16x8*)(&XT[0][buf][bo]);
+                if constexpr (NP == 2) bl[nt] = *(const mbf16x8*)(&XT[NP - 1][buf][bo]);
+            }
+#pragma unroll
+            for (int pass = 0; pass < (NP == 2 ? 3 : 1); ++pass)
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < MXC / 32; ++nt)
+                        if (nt < nct) {
+                            const mbf16x8& A = pass == 2 ? al[mt] : ah[mt];
+                            const mbf16x8& Bv = pass == 1 ? bl[nt] : bh[nt];
+                            dacc[mt * 4 + nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bv, dacc[mt * 4 + nt], 0, 0, 0);
+                        }
         }
     }
     if constexpr (DW) {  // this workgroup's partial weight gradients, torch row order
