@@ -183,7 +183,8 @@ def _cpu_ppo_iter_s(num_envs, obs_dim, num_actions, threads, env_step_rate, samp
     from rsl_rl.modules import ActorCritic
     torch.set_num_threads(int(threads))
     T, epochs, mbs = 24, 5, 4
-    ac = ActorCritic(obs_dim, obs_dim, num_actions, [512, 256, 128], [512, 256, 128], mixed_precision=False)
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+        ac = ActorCritic(obs_dim, obs_dim, num_actions, [512, 256, 128], [512, 256, 128], mixed_precision=False)
     ppo = PPO(ac, num_learning_epochs=epochs, num_mini_batches=mbs, learning_rate=1e-3, schedule="adaptive",
               desired_kl=0.01, entropy_coef=0.01, device="cpu", fused_loss=False)
     opt = ppo.optimizer
