@@ -421,3 +421,22 @@ def test_lstm_bwd_accumulates_the_weight_gradients(I):
     for name, a, b in zip(("w_ih", "w_hh", "b"), got, want):
         rel = float((a - b).norm() / b.norm())
         assert rel < 1e-4, (name, rel)
+
+
+def test_recurrent_rollout_heads_kernel_matches_torch_heads():
+    """RecurrentRollout runs both MLP heads in one pmlp_heads_forward launch: the stored action
+    means and values equal the torch heads on the memories' new state within 1e-5."""
+    torch.manual_seed(3)
+    N, T, O, P, A, H = 1000, 4, 41, 44, 10, 64
+    ac = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                              rnn_hidden_size=H, rnn_num_layers=1, init_noise_std=0.8).cuda()
+    alg = PPO(ac, device="cuda", num_learning_epochs=1, num_mini_batches=1)
+    alg.init_storage(N, T, [O], [P], [A])
+    assert alg._rollout is not None and alg._rollout.heads is not None
+    obs, cobs = torch.randn(N, O, device="cuda"), torch.randn(N, P, device="cuda")
+    with torch.inference_mode():
+        alg.act(obs, cobs)
+        ha, hc = ac.memory_a.hidden_states[0][0], ac.memory_c.hidden_states[0][0]
+        mu, value = ac.actor(ha), ac.critic(hc)
+    torch.testing.assert_close(alg.storage.mu[0], mu, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(alg.storage.values[0], value, rtol=1e-5, atol=1e-5)

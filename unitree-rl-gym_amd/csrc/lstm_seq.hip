@@ -530,6 +530,168 @@ __global__ __launch_bounds__(256) void k_lstm_fwd_mfma(MFwdArgs a) {
     }
 }
 
+// The same forward on 8 waves (512 threads, two waves per SIMD): wave w owns units
+// 8w .. 8w + 7 as two 16-column tiles, [i | f] and [g | o] (8 units each), so a step is 24
+// MFMAs per wave instead of 48.  A lane (column j) then holds i, g (j < 8) or f, o (j >= 8)
+// of unit 8w + (j & 7) for its 4 rows; the partner lane j ^ 8 (DPP row_ror:8, one VALU move
+// per value) supplies the other two gates, and each lane updates 2 of the 4 (env, unit) pairs
+// (j < 8: rows 0, 1; j >= 8: rows 2, 3).  Same products and operation order per element as
+// the 4-wave kernel.
+__device__ __forceinline__ float ror8(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+}
+
+template <int SPLIT>
+__global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdArgs a) {
+    constexpr int NP = SPLIT == 3 ? 2 : 1;  // operand parts (hi, lo)
+    __shared__ __attribute__((aligned(16))) mbf16 A[NP][2][ME * MLDA];
+    const int T = a.T, B = a.B, I = a.I, RL = I + MH + 1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int e0 = blockIdx.x * ME;
+    const int j = lane & 15, rg = lane >> 4;  // column in the tile; row group (envs 4 rg .. 4 rg + 3)
+    const int hj = j >> 3;                    // 0: this column holds i / g, 1: f / o
+    const int uu = 8 * w + (j & 7);           // this lane's unit
+    // weight fragments: tile t (0: [i | f], 1: [g | o]), k-step s
+    mbf16x8 wf[NP][2][4];
+    float bias[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const int r = (2 * tt + hj) * MH + uu;
+        bias[tt] = a.bih[r] + a.bhh[r];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = s * 32 + 8 * rg + e;
+                const float v = k < MKX ? (k < I ? a.wih[(size_t)r * I + k] : 0.f) : a.whh[(size_t)r * MH + (k - MKX)];
+                mbf16 hi, lo;
+                split_bf16(v, hi, lo);
+                wf[0][tt][s][e] = hi;
+                if constexpr (NP == 2) wf[NP - 1][tt][s][e] = lo;
+            }
+    }
+    auto put = [&](int buf, int idx, float v) {  // operand element (hi, lo)
+        mbf16 hi, lo;
+        split_bf16(v, hi, lo);
+        A[0][buf][idx] = hi;
+        if constexpr (NP == 2) A[NP - 1][buf][idx] = lo;
+    };
+    // x staging by the first 256 threads: 4 floats each per step (16 envs x 64 slots)
+    const bool xs = tid < 256;
+    const int xe = (tid & 255) >> 4, xk = (tid & 15) * 4;
+    float xr[4];
+    auto xload = [&](int t) {
+        const int gc = min(e0 + xe, B - 1);
+        const size_t tc = (size_t)min(t, T - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = a.x[(tc * B + gc) * I + min(xk + i, I - 1)];
+    };
+    auto xstore = [&](int buf, int t) {
+        const int ge = e0 + xe;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = (ge < B && xk + i < I) ? xr[i] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) put(buf, xe * MLDA + xk + i, xr[i]);
+        if (a.xh && ge < B) {
+            float* row = a.xh + ((size_t)t * B + ge) * RL;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (xk + i < I) row[xk + i] = xr[i];
+            if (xk == 0) row[I + MH] = 1.f;
+        }
+    };
+    // state of the lane's 2 (env, unit) pairs: rows 2 hj, 2 hj + 1 of its row group
+    float c[2], hp[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        const int p = 2 * hj + pp, ge = e0 + 4 * rg + p;
+        const bool rs = a.reset && ge < B && a.reset[ge];
+        const float h0 = (ge < B && a.h0) ? a.h0[(size_t)ge * MH + uu] : 0.f;
+        const float c0 = (ge < B && a.c0) ? a.c0[(size_t)ge * MH + uu] : 0.f;
+        hp[pp] = rs ? 0.f : h0;
+        c[pp] = rs ? 0.f : c0;
+        put(0, (4 * rg + p) * MLDA + MKX + uu, hp[pp]);
+    }
+    const bool has_reset = a.reset != nullptr;
+    const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
+    auto rload = [&](int t, uint8_t* r) {
+        const size_t tc = (size_t)min(t, T - 1) * B;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) r[pp] = rbase[tc + min(e0 + 4 * rg + 2 * hj + pp, B - 1)];
+    };
+    uint8_t rnx[2];
+    rload(1, rnx);
+    if (xs) {
+        xload(0);
+        xstore(0, 0);
+        if (T > 1) xload(1);
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        const int cur = t & 1;
+        bool rn[2];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) rn[pp] = has_reset && t + 1 < T && rnx[pp] != 0;
+        rload(t + 2, rnx);
+        mfloatx4 acc[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[tt][p] = bias[tt];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int o = j * MLDA + s * 32 + 8 * rg;
+            const mbf16x8 ah = *(const mbf16x8*)(&A[0][cur][o]);
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[0][tt][s], acc[tt], 0, 0, 0);
+            if constexpr (NP == 2) {
+                const mbf16x8 al = *(const mbf16x8*)(&A[NP - 1][cur][o]);
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[NP - 1][tt][s], acc[tt], 0, 0, 0);
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[0][tt][s], acc[tt], 0, 0, 0);
+            }
+        }
+        // own rows and the partner's: own = rows 2 hj + pp, sent = the partner's own rows
+        float ownA[2], ownB[2], rcvA[2], rcvB[2];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            ownA[pp] = hj ? acc[0][2 + pp] : acc[0][pp];
+            ownB[pp] = hj ? acc[1][2 + pp] : acc[1][pp];
+            rcvA[pp] = ror8(hj ? acc[0][pp] : acc[0][2 + pp]);
+            rcvB[pp] = ror8(hj ? acc[1][pp] : acc[1][2 + pp]);
+        }
+        const int nxt = cur ^ 1;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            const int p = 2 * hj + pp, ge = e0 + 4 * rg + p;
+            const float zi = hj ? rcvA[pp] : ownA[pp], zf = hj ? ownA[pp] : rcvA[pp];
+            const float zg = hj ? rcvB[pp] : ownB[pp], zo = hj ? ownB[pp] : rcvB[pp];
+            const float ig = fsig(zi), fg = fsig(zf), gg = ftanh(zg), og = fsig(zo);
+            const float cn = fg * c[pp] + ig * gg;
+            const float hn = og * ftanh(cn);
+            if (ge < B) {
+                const size_t row = (size_t)t * B + ge;
+                if (a.gact) {
+                    float* gr = a.gact + row * MG;
+                    gr[uu] = ig; gr[MH + uu] = fg; gr[2 * MH + uu] = gg; gr[3 * MH + uu] = og;
+                }
+                if (a.c_out) a.c_out[row * MH + uu] = cn;
+                if (a.h_out) a.h_out[row * MH + uu] = hn;
+                if (a.xh) a.xh[row * RL + I + uu] = hp[pp];  // the state this step started from
+            }
+            c[pp] = rn[pp] ? 0.f : cn;  // a reset at t + 1 starts that step from zero
+            hp[pp] = rn[pp] ? 0.f : hn;
+            if (t + 1 < T) put(nxt, (4 * rg + p) * MLDA + MKX + uu, hp[pp]);
+        }
+        if (xs) {
+            if (t + 1 < T) xstore(nxt, t + 1);
+            xload(t + 2);  // clamped to T - 1 past the end
+        }
+        __syncthreads();
+    }
+}
+
 struct MBwdArgs {
     int T, B;
     const float *whh, *c0;
@@ -541,17 +703,18 @@ struct MBwdArgs {
     float* slab;       // DW: per workgroup [dW_ih (4H x I) | dW_hh (4H x H) | db (4H)], torch row order
 };
 
-// DW: the three weight gradients dG^T [x | h_prev | 1] accumulate inside the backward as well:
-// per step the workgroup's 16 envs are the K of a [256 gates x 16] . [16 x (I + H + 1)]
-// product on v_mfma_f32_32x32x16_bf16 (split-bf16 operands, fp32 accumulators held over all T
-// steps; wave w owns gate-row tiles 2w, 2w + 1), written once per workgroup into its slab row
+// DW: the three weight gradients dG^T [x | h_prev | 1] accumulate inside the backward as well,
+// on four more waves of the workgroup (512 threads): per step the workgroup's 16 envs are the
+// K of a [256 gates x 16] . [16 x (I + H + 1)] product on v_mfma_f32_32x32x16_bf16 (split-bf16
+// operands, fp32 accumulators held over all T steps; weight-gradient wave w owns gate-row tiles
+// 2w, 2w + 1) beside the recurrence, written once per workgroup into its slab row
 // (summed over workgroups by pmlp_reduce_slabs): no [T, B, 4H] dgx round trip and no
 // separate 49k-row reduction GEMM.
 constexpr int MXC = 128;  // xh columns covered (I + H + 1 <= 128)
 typedef float mfloatx16 __attribute__((ext_vector_type(16)));
 
 template <int SPLIT, bool DW>
-__global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
+__global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdArgs a) {
     constexpr int NP = SPLIT == 3 ? 2 : 1;
     __shared__ __attribute__((aligned(16))) mbf16 G[NP][2][ME * MLDG];
     // DW operands, transposed so a fragment is 8 consecutive envs (one 16-byte read):
@@ -559,8 +722,98 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     __shared__ __attribute__((aligned(16))) mbf16 GT[DW ? NP : 1][2][DW ? MG * ME : 8];
     __shared__ __attribute__((aligned(16))) mbf16 XT[DW ? NP : 1][2][DW ? MXC * ME : 8];
     const int T = a.T, B = a.B;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int e0 = blockIdx.x * ME;
+    if (DW && threadIdx.x >= 256) {
+        // ---- DW: the weight-gradient waves (4..7), off the recurrence's critical path: per
+        // step they stage that step's xh rows (transposed, split) and, after the step's
+        // barrier, accumulate dG^T [x | h_prev | 1] from the gate gradients the recurrence
+        // waves wrote.  Same number of barriers per step as the recurrence loop below.
+        if constexpr (DW) {
+            const int wt = threadIdx.x - 256, lane = wt & 63, ww = wt >> 6;
+            // thread (column xc, env group xg) holds column xc of envs 8 xg .. 8 xg + 7: each
+            // load instruction reads 64 consecutive columns of one row (coalesced)
+            const int RL = a.I + MH + 1, nenv = min(ME, B - e0), nct = (RL + 31) / 32;
+            const int xc = wt & (MXC - 1), xg = wt >> 7;
+            float xr[8];
+            auto xload = [&](int t) {
+                const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL + min(xc, RL - 1);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xr[k] = src[(size_t)min(8 * xg + k, nenv - 1) * RL];
+            };
+            mfloatx16 dacc[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dacc[i][r] = 0.f;
+            for (int i = wt; i < NP * 2 * MXC * ME; i += 256) (&XT[0][0][0])[i] = (mbf16)0.f;  // columns >= RL stay 0
+            xload(T - 1);
+            for (int t = T - 1; t >= 0; --t) {
+                const int buf = t & 1;
+                if (xc < RL) {
+                    mbf16x8 hi8, lo8;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        mbf16 hi, lo;
+                        split_bf16(8 * xg + k < nenv ? xr[k] : 0.f, hi, lo);
+                        hi8[k] = hi;
+                        lo8[k] = lo;
+                    }
+                    *(mbf16x8*)(&XT[0][buf][xc * ME + 8 * xg]) = hi8;
+                    if constexpr (NP == 2) *(mbf16x8*)(&XT[NP - 1][buf][xc * ME + 8 * xg]) = lo8;
+                }
+                xload(t - 1);
+                __syncthreads();
+                // operands of the wave's 2 x 4 tiles, then the products pass by pass
+                // (consecutive MFMAs on different accumulators)
+                mbf16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int ao = ((2 * ww + mt) * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
+                    ah[mt] = *(const mbf16x8*)(&GT[0][buf][ao]);
+                    if constexpr (NP == 2) al[mt] = *(const mbf16x8*)(&GT[NP - 1][buf][ao]);
+                }
+#pragma unroll
+                for (int nt = 0; nt < MXC / 32; ++nt) {
+                    const int bo = (nt * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
+                    bh[nt] = *(const mbf16x8*)(&XT[0][buf][bo]);
+                    if constexpr (NP == 2) bl[nt] = *(const mbf16x8*)(&XT[NP - 1][buf][bo]);
+                }
+#pragma unroll
+                for (int pass = 0; pass < (NP == 2 ? 3 : 1); ++pass)
+#pragma unroll
+                    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < MXC / 32; ++nt)
+                            if (nt < nct) {
+                                const mbf16x8& A = pass == 2 ? al[mt] : ah[mt];
+                                const mbf16x8& Bv = pass == 1 ? bl[nt] : bh[nt];
+                                dacc[mt * 4 + nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bv, dacc[mt * 4 + nt], 0, 0, 0);
+                            }
+            }
+            // this workgroup's partial weight gradients, torch row order
+            const int I = a.I;
+            float* sl = a.slab + (size_t)blockIdx.x * (size_t)MG * RL;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < MXC / 32; ++nt) {
+                    const int n = nt * 32 + (lane & 31);
+                    if (nt >= nct || n >= RL) continue;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int gp = (2 * ww + mt) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);  // permuted
+                        const int tr = ((gp >> 4) & 3) * MH + 16 * (gp >> 6) + (gp & 15);          // torch row
+                        const float x = dacc[mt * 4 + nt][r];
+                        if (n < I) sl[(size_t)tr * I + n] = x;
+                        else if (n < I + MH) sl[(size_t)MG * I + (size_t)tr * MH + (n - I)] = x;
+                        else sl[(size_t)MG * (I + MH) + tr] = x;
+                    }
+                }
+        }
+        return;
+    }
+    // ---- the recurrence waves (0..3)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int j = lane & 15, rg = lane >> 4, u = 16 * w + j;
     // B[k = permuted gate column][n = unit 16w + j] = W_hh[torch row of k][u], 8 k-steps of 32
     mbf16x8 wf[NP][8];
@@ -606,49 +859,11 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
     float dhn[4] = {0.f, 0.f, 0.f, 0.f}, dcn[4] = {0.f, 0.f, 0.f, 0.f};
     In nx;
     load(T - 1, nx);
-    // DW: the step's xh rows, loaded a step ahead: thread (column xc = tid % 128, env group
-    // xg = tid / 128) holds column xc of envs 8 xg .. 8 xg + 7 (each load instruction reads 64
-    // consecutive columns of one row: coalesced), stored transposed as one 16-byte run per part
-    const int RL = a.I + MH + 1, nenv = min(ME, B - e0), nct = (RL + 31) / 32;
-    const int xc = tid & (MXC - 1), xg = tid >> 7;
-    float xr[DW ? 8 : 1];
-    auto xload = [&](int t) {
-        if constexpr (DW) {
-            const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL + min(xc, RL - 1);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) xr[k] = src[(size_t)min(8 * xg + k, nenv - 1) * RL];
-        }
-    };
-    mfloatx16 dacc[DW ? 8 : 1];
-    if constexpr (DW) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) dacc[i][r] = 0.f;
-        for (int i = tid; i < NP * 2 * MXC * ME; i += 256) (&XT[0][0][0])[i] = (mbf16)0.f;  // columns >= RL stay 0
-        __syncthreads();
-    }
-    xload(T - 1);
     for (int t = T - 1; t >= 0; --t) {
         const int buf = t & 1;
         const In v = nx;
         load(t - 1, nx);
         mbf16x4 gth[4], gtl[4];
-        if constexpr (DW) {  // this step's xh rows, transposed, split; then the next step's loads
-            if (xc < RL) {  // (columns >= RL stay zero)
-                mbf16x8 hi8, lo8;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    mbf16 hi, lo;
-                    split_bf16(8 * xg + k < nenv ? xr[k] : 0.f, hi, lo);
-                    hi8[k] = hi;
-                    lo8[k] = lo;
-                }
-                *(mbf16x8*)(&XT[0][buf][xc * ME + 8 * xg]) = hi8;
-                if constexpr (NP == 2) *(mbf16x8*)(&XT[NP - 1][buf][xc * ME + 8 * xg]) = lo8;
-            }
-            xload(t - 1);
-        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int ge = e0 + 4 * rg + p;
@@ -720,54 +935,6 @@ __global__ __launch_bounds__(256) void k_lstm_bwd_mfma(MBwdArgs a) {
             const float d = (acc[0][0][p] + acc[1][0][p]) + ((acc[0][1][p] + acc[1][1][p]) + (acc[0][2][p] + acc[1][2][p]));
             dhn[p] = (has_reset && v.rs[p]) ? 0.f : d;
         }
-        if constexpr (DW) {  // dW += dG^T [x | h_prev | 1] over this step's 16 envs
-            // operands of the wave's 2 x 4 tiles, then the products pass by pass (consecutive
-            // MFMAs on different accumulators)
-            mbf16x8 ah[2], al[2], bh[4], bl[4];
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                const int ao = ((2 * w + mt) * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
-                ah[mt] = *(const mbf16x8*)(&GT[0][buf][ao]);
-                if constexpr (NP == 2) al[mt] = *(const mbf16x8*)(&GT[NP - 1][buf][ao]);
-            }
-#pragma unroll
-            for (int nt = 0; nt < MXC / 32; ++nt) {
-                const int bo = (nt * 32 + (lane & 31)) * ME + 8 * (lane >> 5);
-                bh[nt] = *(const mbf16x8*)(&XT[0][buf][bo]);
-                if constexpr (NP == 2) bl[nt] = *(const mbf16x8*)(&XT[NP - 1][buf][bo]);
-            }
-#pragma unroll
-            for (int pass = 0; pass < (NP == 2 ? 3 : 1); ++pass)
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < MXC / 32; ++nt)
-                        if (nt < nct) {
-                            const mbf16x8& A = pass == 2 ? al[mt] : ah[mt];
-                            const mbf16x8& Bv = pass == 1 ? bl[nt] : bh[nt];
-                            dacc[mt * 4 + nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bv, dacc[mt * 4 + nt], 0, 0, 0);
-                        }
-        }
-    }
-    if constexpr (DW) {  // this workgroup's partial weight gradients, torch row order
-        const int I = a.I;
-        float* sl = a.slab + (size_t)blockIdx.x * (size_t)MG * RL;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < MXC / 32; ++nt) {
-                const int n = nt * 32 + (lane & 31);
-                if (nt >= nct || n >= RL) continue;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int gp = (2 * w + mt) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);  // permuted
-                    const int tr = ((gp >> 4) & 3) * MH + 16 * (gp >> 6) + (gp & 15);         // torch row
-                    const float x = dacc[mt * 4 + nt][r];
-                    if (n < I) sl[(size_t)tr * I + n] = x;
-                    else if (n < I + MH) sl[(size_t)MG * I + (size_t)tr * MH + (n - I)] = x;
-                    else sl[(size_t)MG * (I + MH) + tr] = x;
-                }
-            }
     }
 }
 
@@ -1142,8 +1309,16 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
     if (T <= 0 || B <= 0 || !x || !wih || !bih || !bhh || !whh) return fail("pmlp_lstm_fwd_mfma: empty sequence or null input");
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
     MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh};
-    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma<1>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(k_lstm_fwd_mfma<3>, dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    static const bool w8 = [] { const char* e = getenv("LSTM_FWD8"); return !(e && e[0] == '0'); }();
+    const dim3 g((B + ME - 1) / ME);
+    hipStream_t st = (hipStream_t)stream;
+    if (w8) {
+        if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma8<1>, g, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, g, dim3(512), 0, st, a);
+    } else {
+        if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma<1>, g, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_lstm_fwd_mfma<3>, g, dim3(256), 0, st, a);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma: ") + hipGetErrorString(e));
 }
@@ -1169,8 +1344,8 @@ PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, c
         return fail("pmlp_lstm_bwd_dw_mfma: null buffer");
     if (H != MH || I <= 0 || I + MH + 1 > MXC) return fail("pmlp_lstm_bwd_dw_mfma: hidden 64, I + 65 <= 128");
     MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, nullptr, xh, I, slab};
-    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, true>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma: ") + hipGetErrorString(e));
 }

@@ -415,6 +415,15 @@ class RecurrentRollout:
         self.actions = torch.empty(self.N, ac.std.shape[0], device=ac.std.device)
         self.draw = torch.zeros((), dtype=torch.int64, device=ac.std.device)
         self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        # both Linear/ELU/Linear heads in one launch (pmlp_heads_forward, fp32) where the
+        # fused recurrent step covers the policy; else the torch modules
+        from rsl_rl.algorithms import fused_recurrent
+        self.heads = None
+        if fused_recurrent.supported(ac, self.N, 1) and ac.memory_a.rnn.hidden_size == ac.memory_c.rnn.hidden_size:
+            dev = ac.std.device
+            self.heads = [ac.actor, ac.critic]
+            self.y0 = [torch.empty(self.N, s[0].out_features, device=dev) for s in self.heads]
+            self.out = [torch.empty(self.N, s[2].out_features, device=dev) for s in self.heads]
 
     def usable(self, obs, cobs, storage):
         ok = lambda t: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
@@ -438,8 +447,17 @@ class RecurrentRollout:
         else:
             storage._save_hidden_states(ac.get_hidden_states())
             ha, hc = ma(obs), mc(cobs)
-        mu = ac.actor(ha.squeeze(0)).contiguous()
-        value = ac.critic(hc.squeeze(0)).contiguous()
+        if self.heads is not None and ha.is_contiguous() and hc.is_contiguous():
+            P = mm._p
+            jobs = (mm.HeadJob * 2)(*[mm.HeadJob(P(h), P(s[0].weight), P(s[0].bias), P(s[2].weight), P(s[2].bias),
+                                                 P(self.y0[n]), P(self.out[n]), None, None, None, s[0].out_features,
+                                                 s[2].out_features)
+                                      for n, (h, s) in enumerate(zip((ha, hc), self.heads))])
+            mm._ok(mm.load().pmlp_heads_forward(2, jobs, self.N, H, mm._stream()), "pmlp_heads_forward")
+            mu, value = self.out
+        else:
+            mu = ac.actor(ha.squeeze(0)).contiguous()
+            value = ac.critic(hc.squeeze(0)).contiguous()
         A = self.actions.shape[1]
         priv = storage.privileged_observations
         P = mm._p
