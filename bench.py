@@ -283,7 +283,9 @@ def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
     out = {"num_envs": n, "policy": runner.cfg["policy_class_name"], "decimation": env_cfg.control.decimation,
            "ppo_iter_ms": round(el / iters * 1e3, 3), "env_steps_per_s": round(n * T * iters / el, 1),
            "rollout_graph": runner._rollout_graph is not None,
-           "update_graph": (getattr(runner.alg, "_graph", None) or getattr(runner.alg, "_fgraph", None)) is not None,
+           "update_graph": any(getattr(runner.alg, g, None) is not None for g in ("_graph", "_fgraph", "_rgraph")),
+           "update_path": "fused recurrent step" if getattr(runner.alg, "_rfused", None) is not None else
+           ("fused MLP step" if getattr(runner.alg, "_fused", None) is not None else "autograd"),
            "domain_rand": bool(env_cfg.domain_rand.randomize_friction or env_cfg.domain_rand.randomize_base_mass),
            "terrain": env_cfg.terrain.mesh_type, "iters_timed": iters}
     env.close()

@@ -338,6 +338,13 @@ PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* wh
  * slab row [dW_ih (4H x I) | dW_hh (4H x H) | db (4H)] of 4H (I + H + 1) floats in torch's
  * row order (summed over the rows by pmlp_reduce_slabs; db is the gradient of b_ih and b_hh).
  * The gate gradients themselves are not written.  H = 64, I + H + 1 <= 128.            */
+/* One rollout step of a hidden-64 memory on the matrix cores: the arithmetic of
+ * pmlp_lstm_fwd_mfma at T = 1 (so the rollout's log-probabilities come from the same
+ * numbers the update recomputes), input projection inside, h / c [B, 64] updated in place;
+ * h_save / c_save (both or neither) receive the state the step starts from.   I <= 64.  */
+PMLP_API int pmlp_lstm_step_mfma(int32_t B, int32_t H, int32_t I, const float* x, const float* wih, const float* bih,
+                                 const float* bhh, const float* whh, float* h, float* c, float* h_save, float* c_save,
+                                 void* stream);
 PMLP_API int32_t pmlp_lstm_bwd_dw_blocks(int32_t B);
 PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* whh, const float* c0,
                                    const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,

@@ -440,3 +440,25 @@ def test_recurrent_rollout_heads_kernel_matches_torch_heads():
         mu, value = ac.actor(ha), ac.critic(hc)
     torch.testing.assert_close(alg.storage.mu[0], mu, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(alg.storage.values[0], value, rtol=1e-5, atol=1e-5)
+
+
+def test_lstm_rollout_step_mfma_in_place_matches_nn_lstm():
+    """pmlp_lstm_step_mfma (the recurrent rollout's memory step: the update's matrix-core
+    arithmetic at T = 1): h, c updated in place and the pre-step state saved, vs one nn.LSTM
+    step within the split-bf16 tolerance (2e-5), over three steps."""
+    torch.manual_seed(5)
+    B, I, H = 1000, 44, 64
+    rnn = torch.nn.LSTM(I, H).cuda()
+    h = 0.5 * torch.randn(1, B, H, device="cuda")
+    c = 0.5 * torch.randn(1, B, H, device="cuda")
+    hs, cs = torch.empty_like(h), torch.empty_like(c)
+    for _ in range(3):
+        x = torch.randn(B, I, device="cuda")
+        h_ref, c_ref = h.clone(), c.clone()
+        with torch.no_grad():
+            y, (h_new, c_new) = rnn(x.unsqueeze(0), (h_ref, c_ref))
+        out = lstm_seq.lstm_step_mfma_(rnn, x, h, c, save=(hs, cs))
+        assert out.data_ptr() == h.data_ptr()
+        assert torch.equal(hs, h_ref) and torch.equal(cs, c_ref)
+        torch.testing.assert_close(h, h_new, rtol=2e-5, atol=2e-5)
+        torch.testing.assert_close(c, c_new, rtol=2e-5, atol=2e-5)

@@ -391,6 +391,7 @@ struct MFwdArgs {
     const float *x, *wih, *bih, *bhh, *whh, *h0, *c0;
     const uint8_t* reset;
     float *h_out, *c_out, *gact, *xh;
+    float *h_save, *c_save;  // optional: the state the sequence starts from (the rollout's storage slot)
 };
 
 template <int SPLIT>
@@ -611,6 +612,10 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdArgs a) {
         hp[pp] = rs ? 0.f : h0;
         c[pp] = rs ? 0.f : c0;
         put(0, (4 * rg + p) * MLDA + MKX + uu, hp[pp]);
+        if (a.h_save && ge < B) {
+            a.h_save[(size_t)ge * MH + uu] = hp[pp];
+            a.c_save[(size_t)ge * MH + uu] = c[pp];
+        }
     }
     const bool has_reset = a.reset != nullptr;
     const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
@@ -1308,7 +1313,7 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
                                 const uint8_t* reset, float* h_out, float* c_out, float* gact, float* xh, void* stream) {
     if (T <= 0 || B <= 0 || !x || !wih || !bih || !bhh || !whh) return fail("pmlp_lstm_fwd_mfma: empty sequence or null input");
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
-    MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh};
+    MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh, nullptr, nullptr};
     static const bool w8 = [] { const char* e = getenv("LSTM_FWD8"); return !(e && e[0] == '0'); }();
     const dim3 g((B + ME - 1) / ME);
     hipStream_t st = (hipStream_t)stream;
@@ -1400,4 +1405,22 @@ PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32
     else hipLaunchKernelGGL(k_heads_bwd<128>, g, dim3(HT), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_backward: ") + hipGetErrorString(e));
+}
+
+/* One rollout step of a hidden-64 memory on the matrix cores (the 8-wave sequence kernel at
+ * T = 1, the arithmetic of the update's pmlp_lstm_fwd_mfma): h, c [B, 64] are read and
+ * overwritten in place (each (env, unit) by the lane that reads it), the input projection
+ * is inside, and the state the step starts from goes to h_save / c_save when given. */
+PMLP_API int pmlp_lstm_step_mfma(int32_t B, int32_t H, int32_t I, const float* x, const float* wih, const float* bih,
+                                 const float* bhh, const float* whh, float* h, float* c, float* h_save, float* c_save,
+                                 void* stream) {
+    if (B <= 0 || !x || !wih || !bih || !bhh || !whh || !h || !c) return fail("pmlp_lstm_step_mfma: null input");
+    if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_step_mfma: hidden 64, input 1..64");
+    if ((h_save == nullptr) != (c_save == nullptr)) return fail("pmlp_lstm_step_mfma: h_save and c_save together");
+    MFwdArgs a{1, B, I, x, wih, bih, bhh, whh, h, c, nullptr, h, c, nullptr, nullptr, h_save, c_save};
+    const dim3 g((B + ME - 1) / ME);
+    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma8<1>, g, dim3(512), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, g, dim3(512), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma: ") + hipGetErrorString(e));
 }

@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from rsl_rl.modules import lstm_seq
 from rsl_rl.modules import mfma_mlp as mm
 
 
@@ -418,12 +419,27 @@ class RecurrentRollout:
         # both Linear/ELU/Linear heads in one launch (pmlp_heads_forward, fp32) where the
         # fused recurrent step covers the policy; else the torch modules
         from rsl_rl.algorithms import fused_recurrent
+        # the memories' rollout step on the update's matrix-core kernel (pmlp_lstm_step_mfma)
+        # when the update runs the fused recurrent step with it: the stored log-probabilities
+        # then come from the numbers the update recomputes (LSTM_MFMA_STEP=0: fp32 step kernel)
+        rnns = [getattr(getattr(ac, m, None), "rnn", None) for m in ("memory_a", "memory_c")]
+        self.mfma_step = os.environ.get("LSTM_MFMA_STEP", "1") != "0" and alg._rfused is not None and \
+            all(r is not None and lstm_seq.mfma_usable(r, torch.empty(1, r.input_size)) for r in rnns)
         self.heads = None
         if fused_recurrent.supported(ac, self.N, 1) and ac.memory_a.rnn.hidden_size == ac.memory_c.rnn.hidden_size:
             dev = ac.std.device
             self.heads = [ac.actor, ac.critic]
             self.y0 = [torch.empty(self.N, s[0].out_features, device=dev) for s in self.heads]
             self.out = [torch.empty(self.N, s[2].out_features, device=dev) for s in self.heads]
+
+    def _mstep(self, mem, x, save):
+        """Memory.step_ on pmlp_lstm_step_mfma (state buffers created as step_ creates them)."""
+        B, H = x.shape[0], mem.rnn.hidden_size
+        hs = mem.hidden_states
+        if hs is None or not isinstance(hs, tuple) or hs[0].shape != (1, B, H) or hs[0].device != x.device:
+            with torch.inference_mode(False):
+                mem.hidden_states = (torch.zeros(1, B, H, device=x.device), torch.zeros(1, B, H, device=x.device))
+        return lstm_seq.lstm_step_mfma_(mem.rnn, x, mem.hidden_states[0], mem.hidden_states[1], save=save)
 
     def usable(self, obs, cobs, storage):
         ok = lambda t: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
@@ -442,8 +458,12 @@ class RecurrentRollout:
             # the state BEFORE this step goes to the storage slot from inside the step kernel
             shape = (1, self.N, H)
             sa, sc = storage.hidden_state_slots(t, [shape, shape], [(1, self.N, mc.rnn.hidden_size)] * 2)
-            ha = ma.step_(obs, save=(sa[0], sa[1]))
-            hc = mc.step_(cobs, save=(sc[0], sc[1]))
+            if self.mfma_step:  # the update's matrix-core arithmetic, one launch per memory
+                ha = self._mstep(ma, obs, (sa[0], sa[1]))
+                hc = self._mstep(mc, cobs, (sc[0], sc[1]))
+            else:
+                ha = ma.step_(obs, save=(sa[0], sa[1]))
+                hc = mc.step_(cobs, save=(sc[0], sc[1]))
         else:
             storage._save_hidden_states(ac.get_hidden_states())
             ha, hc = ma(obs), mc(cobs)

@@ -39,6 +39,7 @@ def _lib():
         L.pmlp_lstm_bwd_dw_blocks.argtypes = [i32]
         L.pmlp_lstm_bwd_dw_blocks.restype = i32
         L.pmlp_lstm_bwd_dw_mfma.argtypes = [i32, i32, i32, i32] + [vp] * 8 + [vp]
+        L.pmlp_lstm_step_mfma.argtypes = [i32, i32, i32] + [vp] * 9 + [vp]
         _bound = True
     return L
 
@@ -195,4 +196,19 @@ def lstm_step_(rnn, x, h, c, save=None):
         hs, cs = (None, None) if save is None else save
         _ok(_lib().pmlp_lstm_step(B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), p(hs), p(cs),
                                   mm._stream()), "pmlp_lstm_step")
+    return h
+
+
+def lstm_step_mfma_(rnn, x, h, c, save=None):
+    """One rollout step in place on the matrix-core kernel (pmlp_lstm_step_mfma: the update's
+    arithmetic at T = 1, hidden 64): h, c [1,B,H] static buffers; save = (h_dst, c_dst)
+    receives the state the step starts from.  Returns h."""
+    B, I = x.shape
+    H = rnn.hidden_size
+    p = mm._p
+    hs, cs = (None, None) if save is None else save
+    with torch.no_grad():
+        _ok(_lib().pmlp_lstm_step_mfma(B, H, I, p(x), p(rnn.weight_ih_l0), p(rnn.bias_ih_l0), p(rnn.bias_hh_l0),
+                                       p(rnn.weight_hh_l0), p(h), p(c), p(hs), p(cs), mm._stream()),
+            "pmlp_lstm_step_mfma")
     return h
