@@ -1,6 +1,6 @@
-"""A/B of the recurrent PPO iteration (H1 / H1_2 / G1, LSTM 64) across the dense LSTM
-kernels of the update: LSTM_MFMA=0 (fp32 VALU sequence kernels), LSTM_MFMA=1 with
-LSTM_MFMA_SPLIT=3 (split-bf16, the default) and LSTM_MFMA_SPLIT=1 (plain bf16).
+"""A/B of the recurrent PPO iteration (H1 / H1_2 / G1, LSTM 64): LSTM_MFMA=0 (fp32 VALU
+sequence kernels and the autograd update) against the default matrix-core kernels with the
+fused recurrent step.
 Each variant runs in its own process (the switches are read once per process).
 
 usage: python tools/probes/recurrent_iter_ab.py [task] [num_envs] [iters]
@@ -37,8 +37,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     code = CHILD.format(root=ROOT, pkg=os.path.join(ROOT, "unitree-rl-gym_amd"), task=task, n=n, iters=iters)
-    for name, env in (("fp32", {"LSTM_MFMA": "0"}), ("mfma_split3", {"LSTM_MFMA": "1", "LSTM_MFMA_SPLIT": "3"}),
-                      ("mfma_bf16", {"LSTM_MFMA": "1", "LSTM_MFMA_SPLIT": "1"})):
+    for name, env in (("fp32", {"LSTM_MFMA": "0"}), ("mfma_split_bf16", {"LSTM_MFMA": "1"})):
         r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
                            timeout=300)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]

@@ -359,12 +359,11 @@ __global__ __launch_bounds__(4 * H) void k_lstm_bwd(int T, int B, const float* _
 // envs are ONE [16 x 128] . [128 x 256] product, [x_t | h_{t-1}] . [W_ih | W_hh]^T, on
 // v_mfma_f32_16x16x32_bf16 with fp32 accumulation from the fp32 bias.  Precision: every
 // operand is split into bf16 hi + lo (v = hi + lo to ~2^-16 relative) and the product is
-// hi.hi + hi.lo + lo.hi (SPLIT = 3), near fp32; SPLIT = 1 is the plain bf16 product.
-// Gate columns are permuted so that wave w's four 16-column tiles are the i, f, g, o
-// gates of units 16w .. 16w+15: a lane (column j, rows 4(l>>4)..+3) then holds all four
-// gates of its 4 (env, unit) pairs, and the cell update, c and h stay in the lane (fp32).
-// The weight fragments are loaded once; h_{t-1} and x_t sit in a double-buffered LDS
-// operand, one barrier per step.  Outputs as k_lstm_fwd (fp32).
+// hi.hi + hi.lo + lo.hi (SPLIT = 3), near fp32 (SPLIT = 1, the plain bf16 product, was 5e-2
+// off on the pretrained policies' action means: not shipped).
+// The cell update, c and h stay in the lanes (fp32); the weight fragments are loaded once;
+// h_{t-1} and x_t sit in a double-buffered LDS operand, one barrier per step.  Outputs as
+// k_lstm_fwd (fp32).
 // The backward runs the same way: the gate gradients (fp32, in the lane) go to dgx and, as
 // bf16 (hi, lo), to an LDS operand for dh_{t-1} = dG . W_hh, whose 16 x 16 result tile of
 // wave w is exactly the lane's own (env, unit) pairs.
@@ -394,150 +393,12 @@ struct MFwdArgs {
     float *h_save, *c_save;  // optional: the state the sequence starts from (the rollout's storage slot)
 };
 
-template <int SPLIT>
-__global__ __launch_bounds__(256) void k_lstm_fwd_mfma(MFwdArgs a) {
-    constexpr int NP = SPLIT == 3 ? 2 : 1;  // operand parts (hi, lo)
-    __shared__ __attribute__((aligned(16))) mbf16 A[NP][2][ME * MLDA];
-    const int T = a.T, B = a.B, I = a.I, RL = I + MH + 1;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int e0 = blockIdx.x * ME;
-    const int j = lane & 15, rg = lane >> 4;  // column in the tile; row group (envs 4 rg .. 4 rg + 3)
-    const int u = 16 * w + j;                // this lane's unit
-    // weight fragments: tile q (gate q of units 16w..), k-step s: B[k][col] = [W_ih | W_hh][q*H + u][k]
-    mbf16x8 wf[NP][4][4];
-    float bias[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = q * MH + u;
-        bias[q] = a.bih[r] + a.bhh[r];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = s * 32 + 8 * rg + e;
-                const float v = k < MKX ? (k < I ? a.wih[(size_t)r * I + k] : 0.f) : a.whh[(size_t)r * MH + (k - MKX)];
-                mbf16 hi, lo;
-                split_bf16(v, hi, lo);
-                wf[0][q][s][e] = hi;
-                if constexpr (NP == 2) wf[NP - 1][q][s][e] = lo;
-            }
-    }
-    auto put = [&](int buf, int idx, float v) {  // operand element (hi, lo)
-        mbf16 hi, lo;
-        split_bf16(v, hi, lo);
-        A[0][buf][idx] = hi;
-        if constexpr (NP == 2) A[NP - 1][buf][idx] = lo;
-    };
-    // x staging: 4 floats per thread per step (16 envs x 64 slots)
-    const int xe = tid >> 4, xk = (tid & 15) * 4;  // env row, first x slot
-    float xr[4];
-    // loads are unconditional at clamped addresses, the value selected after: a load under a
-    // lane-divergent branch gets a vmcnt(0) at the branch's end and loses its step of slack
-    auto xload = [&](int t) {  // raw values; masked in xstore (no use of a load here)
-        const int gc = min(e0 + xe, B - 1);
-        const size_t tc = (size_t)min(t, T - 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = a.x[(tc * B + gc) * I + min(xk + i, I - 1)];
-    };
-    auto xstore = [&](int buf, int t) {  // the operand; the fp32 x into xh
-        const int ge = e0 + xe;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = (ge < B && xk + i < I) ? xr[i] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) put(buf, xe * MLDA + xk + i, xr[i]);
-        if (a.xh && ge < B) {
-            float* row = a.xh + ((size_t)t * B + ge) * RL;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (xk + i < I) row[xk + i] = xr[i];
-            if (xk == 0) row[I + MH] = 1.f;
-        }
-    };
-    // state of the lane's 4 (env, unit) pairs
-    float c[4], hp[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int ge = e0 + 4 * rg + p;
-        const bool rs = a.reset && ge < B && a.reset[ge];
-        const float h0 = (ge < B && a.h0) ? a.h0[(size_t)ge * MH + u] : 0.f;
-        const float c0 = (ge < B && a.c0) ? a.c0[(size_t)ge * MH + u] : 0.f;
-        hp[p] = rs ? 0.f : h0;
-        c[p] = rs ? 0.f : c0;
-        put(0, (4 * rg + p) * MLDA + MKX + u, hp[p]);
-    }
-    // next step's reset flags of the lane's 4 envs, loaded a step ahead
-    const bool has_reset = a.reset != nullptr;
-    const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
-    auto rload = [&](int t, uint8_t* r) {
-        const size_t tc = (size_t)min(t, T - 1) * B;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) r[p] = rbase[tc + min(e0 + 4 * rg + p, B - 1)];
-    };
-    uint8_t rnx[4];
-    rload(1, rnx);
-    xload(0);
-    xstore(0, 0);
-    if (T > 1) xload(1);
-    __syncthreads();
-    for (int t = 0; t < T; ++t) {
-        const int cur = t & 1;
-        bool rn[4];  // a reset at t + 1 (rows past B never matter)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) rn[p] = has_reset && t + 1 < T && rnx[p] != 0;
-        rload(t + 2, rnx);
-        mfloatx4 acc[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int p = 0; p < 4; ++p) acc[q][p] = bias[q];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {  // four independent accumulator chains per product
-            const int o = j * MLDA + s * 32 + 8 * rg;
-            const mbf16x8 ah = *(const mbf16x8*)(&A[0][cur][o]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[0][q][s], acc[q], 0, 0, 0);
-            if constexpr (NP == 2) {
-                const mbf16x8 al = *(const mbf16x8*)(&A[NP - 1][cur][o]);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wf[NP - 1][q][s], acc[q], 0, 0, 0);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[0][q][s], acc[q], 0, 0, 0);
-            }
-        }
-        const int nxt = cur ^ 1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int ge = e0 + 4 * rg + p;
-            const float ig = fsig(acc[0][p]), fg = fsig(acc[1][p]), gg = ftanh(acc[2][p]), og = fsig(acc[3][p]);
-            const float cn = fg * c[p] + ig * gg;
-            const float hn = og * ftanh(cn);
-            if (ge < B) {
-                const size_t row = (size_t)t * B + ge;
-                if (a.gact) {
-                    float* gr = a.gact + row * MG;
-                    gr[u] = ig; gr[MH + u] = fg; gr[2 * MH + u] = gg; gr[3 * MH + u] = og;
-                }
-                if (a.c_out) a.c_out[row * MH + u] = cn;
-                if (a.h_out) a.h_out[row * MH + u] = hn;
-                if (a.xh) a.xh[row * RL + I + u] = hp[p];  // the state this step started from
-            }
-            c[p] = rn[p] ? 0.f : cn;  // a reset at t + 1 starts that step from zero
-            hp[p] = rn[p] ? 0.f : hn;
-            if (t + 1 < T) put(nxt, (4 * rg + p) * MLDA + MKX + u, hp[p]);
-        }
-        if (t + 1 < T) xstore(nxt, t + 1);
-        xload(t + 2);  // clamped to T - 1 past the end
-        __syncthreads();
-    }
-}
-
-// The same forward on 8 waves (512 threads, two waves per SIMD): wave w owns units
-// 8w .. 8w + 7 as two 16-column tiles, [i | f] and [g | o] (8 units each), so a step is 24
-// MFMAs per wave instead of 48.  A lane (column j) then holds i, g (j < 8) or f, o (j >= 8)
-// of unit 8w + (j & 7) for its 4 rows; the partner lane j ^ 8 (DPP row_ror:8, one VALU move
-// per value) supplies the other two gates, and each lane updates 2 of the 4 (env, unit) pairs
-// (j < 8: rows 0, 1; j >= 8: rows 2, 3).  Same products and operation order per element as
-// the 4-wave kernel.
+// Eight waves (512 threads, two waves per SIMD): wave w owns units 8w .. 8w + 7 as two
+// 16-column tiles, [i | f] and [g | o] (8 units each), so a step is 24 MFMAs per wave (a
+// 4-wave form with the four gate tiles of 16 units per wave ran 68 vs 59 us at H1 scale).
+// A lane (column j) holds i, g (j < 8) or f, o (j >= 8) of unit 8w + (j & 7) for its 4 rows;
+// the partner lane j ^ 8 (DPP row_ror:8, one VALU move per value) supplies the other two
+// gates, and each lane updates 2 of the 4 (env, unit) pairs (j < 8: rows 0, 1; else 2, 3).
 __device__ __forceinline__ float ror8(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
 }
@@ -1202,15 +1063,6 @@ __global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
     }
 }
 
-// operand precision of the MFMA sequence kernels: 3 = split bf16 (default), 1 = plain bf16
-static int mfma_split() {
-    static const int v = [] {
-        const char* e = getenv("LSTM_MFMA_SPLIT");
-        return (e && atoi(e) == 1) ? 1 : 3;
-    }();
-    return v;
-}
-
 thread_local std::string g_err;
 
 int fail(const std::string& m) {
@@ -1314,16 +1166,7 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
     if (T <= 0 || B <= 0 || !x || !wih || !bih || !bhh || !whh) return fail("pmlp_lstm_fwd_mfma: empty sequence or null input");
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
     MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh, nullptr, nullptr};
-    static const bool w8 = [] { const char* e = getenv("LSTM_FWD8"); return !(e && e[0] == '0'); }();
-    const dim3 g((B + ME - 1) / ME);
-    hipStream_t st = (hipStream_t)stream;
-    if (w8) {
-        if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma8<1>, g, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, g, dim3(512), 0, st, a);
-    } else {
-        if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma<1>, g, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(k_lstm_fwd_mfma<3>, g, dim3(256), 0, st, a);
-    }
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma: ") + hipGetErrorString(e));
 }
@@ -1334,8 +1177,7 @@ PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* wh
     if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !dgx) return fail("pmlp_lstm_bwd_mfma: null buffer");
     if (H != MH) return fail("pmlp_lstm_bwd_mfma: hidden 64");
     MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, dgx, nullptr, 0, nullptr};
-    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((k_lstm_bwd_mfma<3, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_mfma: ") + hipGetErrorString(e));
 }
@@ -1349,8 +1191,7 @@ PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, c
         return fail("pmlp_lstm_bwd_dw_mfma: null buffer");
     if (H != MH || I <= 0 || I + MH + 1 > MXC) return fail("pmlp_lstm_bwd_dw_mfma: hidden 64, I + 65 <= 128");
     MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, nullptr, xh, I, slab};
-    if (mfma_split() == 1) hipLaunchKernelGGL((k_lstm_bwd_mfma<1, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma: ") + hipGetErrorString(e));
 }
@@ -1418,9 +1259,7 @@ PMLP_API int pmlp_lstm_step_mfma(int32_t B, int32_t H, int32_t I, const float* x
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_step_mfma: hidden 64, input 1..64");
     if ((h_save == nullptr) != (c_save == nullptr)) return fail("pmlp_lstm_step_mfma: h_save and c_save together");
     MFwdArgs a{1, B, I, x, wih, bih, bhh, whh, h, c, nullptr, h, c, nullptr, nullptr, h_save, c_save};
-    const dim3 g((B + ME - 1) / ME);
-    if (mfma_split() == 1) hipLaunchKernelGGL(k_lstm_fwd_mfma8<1>, g, dim3(512), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, g, dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma: ") + hipGetErrorString(e));
 }
