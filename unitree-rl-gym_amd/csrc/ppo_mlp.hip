@@ -1479,15 +1479,19 @@ struct FmlpJobs {
 
 // One layer: D[R, N] = act(A[R, K] . W[N, K]^T + b), A in LDS (ld lda); wave w takes the
 // 32-column tiles w, w + 8, ...; every row tile of the workgroup per column tile, so a
-// B fragment (one 16-byte load per lane per k-step) feeds RT MFMAs.
+// B fragment (one 16-byte load per lane per k-step) feeds RT MFMAs.  A layer with fewer
+// column tiles than waves (128 -> 4 tiles, the output layer 1) splits each column tile's
+// row tiles between wpc waves instead of leaving waves idle (same chain per element).
 template <int R, bool LAST>
 __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const bf16* __restrict__ W,
                                            const float* __restrict__ bias, int N, bf16* D, int ldd,
                                            float* __restrict__ out, int ldo, int r0, int M) {
-    constexpr int RT = R / 32;
+    constexpr int RT = R / 32, NW = FMLP_THREADS / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nct = (N + 31) >> 5, ks = K >> 4;
-    for (int ct = wid; ct < nct; ct += FMLP_THREADS / 64) {
+    const int wpc = nct >= NW ? 1 : min(NW / nct, RT), part = wid % wpc;
+    const int i0 = part * RT / wpc, i1 = (part + 1) * RT / wpc;  // this wave's row tiles
+    for (int ct = wid / wpc; ct < nct; ct += NW / wpc) {
         floatx16 acc[RT];
 #pragma unroll
         for (int i = 0; i < RT; ++i)
@@ -1498,49 +1502,68 @@ __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const 
         const bf16* wrow = W + (size_t)(nv ? n : 0) * K + 8 * (lane >> 5);
         const bf16* arow = A + (lane & 31) * lda + 8 * (lane >> 5);
         // B fragments in groups of FG k-steps, the next group's loads in flight while this
-        // group's MFMAs run (k ascending, as the per-layer GEMM)
+        // group's MFMAs run (k ascending, as the per-layer GEMM).  The loads are unconditional,
+        // at clamped addresses (a column past N reads row 0 and is never stored; a k-step past
+        // the end re-reads the last one and feeds no MFMA): a load under a branch would make
+        // the compiler drain every load in flight at the branch's end.
         constexpr int FG = 4;
         bf16x8 bq[FG], bn[FG];
         auto loadg = [&](int s0, bf16x8(&b)[FG]) {
 #pragma unroll
-            for (int u = 0; u < FG; ++u) {
-                if (nv && s0 + u < ks) {
-                    b[u] = *(const bf16x8*)(wrow + (s0 + u) * 16);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) b[u][e] = (bf16)0.f;
-                }
-            }
+            for (int u = 0; u < FG; ++u) b[u] = *(const bf16x8*)(wrow + min(s0 + u, ks - 1) * 16);
         };
-        loadg(0, bq);
-        for (int s0 = 0; s0 < ks; s0 += FG) {
-            if (s0 + FG < ks) loadg(s0 + FG, bn);
+        auto mfmas = [&](int s0, const bf16x8(&b)[FG]) {
 #pragma unroll
             for (int u = 0; u < FG; ++u) {
                 if (s0 + u < ks) {
 #pragma unroll
                     for (int i = 0; i < RT; ++i) {
+                        if (i < i0 || i >= i1) continue;
                         const bf16x8 af = *(const bf16x8*)(arow + i * 32 * lda + (s0 + u) * 16);
-                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq[u], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[u], af, acc[i], 0, 0, 0);
                     }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < FG; ++u) bq[u] = bn[u];
+        };
+        // two fragment sets used in turn (a register copy from one to the other would wait
+        // for the loads it is meant to overlap)
+        loadg(0, bq);
+        for (int s0 = 0; s0 < ks; s0 += 2 * FG) {
+            loadg(s0 + FG, bn);
+            mfmas(s0, bq);
+            loadg(s0 + 2 * FG, bq);
+            mfmas(s0 + FG, bn);
         }
-        if (!nv) continue;
-        const float bv = bias ? bias[n] : 0.f;
+        // the tile was formed transposed (W . A^T: the weight fragment is the MFMA's first
+        // operand), so a lane holds row (lane & 31) of its row tile and, per quad q, the 4
+        // consecutive columns 8q + 4 (lane >> 5) + 0..3: one 8-byte LDS store per quad (the
+        // same products and k order per element as A . W^T: bitwise the same values)
+        const int rl = lane & 31;
 #pragma unroll
-        for (int i = 0; i < RT; ++i)
+        for (int q = 0; q < 4; ++q) {
+            const int n0 = ct * 32 + 8 * q + 4 * (lane >> 5);
+            if (LAST && n0 >= N) continue;
+            float bq4[4];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int r = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * (lane >> 5);
+            for (int c = 0; c < 4; ++c) bq4[c] = bias ? bias[min(n0 + c, N - 1)] : 0.f;
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                if (i < i0 || i >= i1) continue;
+                const int r = i * 32 + rl;
                 if constexpr (LAST) {
-                    if (r0 + r < M) out[(size_t)(r0 + r) * ldo + n] = acc[i][t] + bv;
+                    if (r0 + r < M) {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            if (n0 + c < N) out[(size_t)(r0 + r) * ldo + n0 + c] = acc[i][4 * q + c] + bq4[c];
+                    }
                 } else {
-                    D[r * ldd + n] = (bf16)elu(acc[i][t] + bv);
+                    bf16x4 v;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) v[c] = (bf16)elu(acc[i][4 * q + c] + bq4[c]);
+                    *(bf16x4*)(D + r * ldd + n0) = v;
                 }
             }
+        }
     }
 }
 
@@ -1555,6 +1578,22 @@ __device__ __forceinline__ void fmlp_store(const bf16* D, int lds_ld, int N, bf1
     }
 }
 
+#ifdef PMLP_FMLP_STAMPS
+// diagnostic build only (never the shipped library): per-block phase clocks of k_mlp_fwd
+#define FMLP_NSTAMP 20
+__device__ unsigned long long g_fmlp_stamps[4096 * FMLP_NSTAMP];
+#define FMLP_STAMP(k)                                                                          \
+    do {                                                                                       \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_fmlp_stamps[blockIdx.x * FMLP_NSTAMP + (k)] = t_; \
+    } while (0)
+extern "C" int pmlp_diag_fmlp_stamps(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fmlp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#else
+#define FMLP_STAMP(k) ((void)(k))
+#endif
+
 template <int R>
 __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) {
     // y0 (then y2) and x (then y1); row strides 8 elements past the width: ds_read_b128
@@ -1566,6 +1605,8 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) 
     const int jb = gridDim.y > 1 ? blockIdx.y : 0, je = gridDim.y > 1 ? blockIdx.y + 1 : jobs.njobs;
     for (int jj = jb; jj < je; ++jj) {
         const FmlpJob& J = jobs.j[jj];
+        const int sb = 9 * (jj - jb);
+        FMLP_STAMP(sb + 0);
         // input rows: gathered, fp32 -> bf16 (columns >= kx are 0), into LDS (+ the bf16 copy)
         const int cpr = J.K0 >> 3;
         for (int i = threadIdx.x; i < R * cpr; i += FMLP_THREADS) {
@@ -1588,17 +1629,25 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) 
             *(bf16x8*)(Y1 + r * LD1 + k) = t;
         }
         __syncthreads();
+        FMLP_STAMP(sb + 1);
         fmlp_layer<R, false>(Y1, LD1, J.K0, J.W[0], J.b[0], J.N[0], Y0, LD0, nullptr, 0, r0, M);
+        FMLP_STAMP(sb + 2);
         __syncthreads();
         fmlp_store<R>(Y0, LD0, J.N[0], J.y[0], J.ldy[0], r0, M);
+        FMLP_STAMP(sb + 3);
         fmlp_layer<R, false>(Y0, LD0, J.N[0], J.W[1], J.b[1], J.N[1], Y1, LD1, nullptr, 0, r0, M);
+        FMLP_STAMP(sb + 4);
         __syncthreads();
         fmlp_store<R>(Y1, LD1, J.N[1], J.y[1], J.ldy[1], r0, M);
+        FMLP_STAMP(sb + 5);
         fmlp_layer<R, false>(Y1, LD1, J.N[1], J.W[2], J.b[2], J.N[2], Y0, LD0, nullptr, 0, r0, M);
+        FMLP_STAMP(sb + 6);
         __syncthreads();
         fmlp_store<R>(Y0, LD0, J.N[2], J.y[2], J.ldy[2], r0, M);
+        FMLP_STAMP(sb + 7);
         fmlp_layer<R, true>(Y0, LD0, J.N[2], J.W[3], J.b[3], J.N[3], nullptr, 0, J.out, J.ldo, r0, M);
         __syncthreads();  // (the next job restages x over y1)
+        FMLP_STAMP(sb + 8);
     }
 }
 
