@@ -171,12 +171,17 @@ PMLP_API int pmlp_loss_bookkeeping(const float* stats, float* lr, float* acc, fl
                                    void* stream);
 /* pmlp_adam that also refreshes bf16 copies of the updated weights (the GEMM operands):
  * param[offset + r*cols + c] -> dst[r*ld + c] for every mirror job, so no conversion launch
- * precedes the next forward.  At most PMLP_MAX_MIRROR jobs, disjoint parameter ranges.   */
+ * precedes the next forward.  At most PMLP_MAX_MIRROR jobs, disjoint parameter ranges.
+ * frag (optional, ld a multiple of 16): the same weight also into the fragment-packed
+ * layout pmlp_mlp_forward reads (pmlp_mlp_fwd_job.Wf): element (r, c) at
+ *   ((((r / 32) * (ld / 16) + c / 16) * 64 + r % 32 + 32 * ((c / 8) % 2)) * 8 + c % 8
+ * (ceil(rows / 32) * 32 * ld elements; the padding entries are the caller's zeros).      */
 #define PMLP_MAX_MIRROR 8
 typedef struct {
     int64_t offset;
     int32_t rows, cols, ld;
     pmlp_bf16* dst;
+    pmlp_bf16* frag;
 } pmlp_mirror_job;
 PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                               float grad_scale, const float* partial, const float* step, const float* lr,
@@ -242,6 +247,9 @@ typedef struct {
     int32_t ldy[3];
     float* out;
     int32_t ldo;
+    /* optional: W[l] fragment-packed (the pmlp_mirror_job.frag layout with ld = K_l): each
+     * wave's weight-fragment load is then 1 KB contiguous instead of 32 row pieces */
+    const pmlp_bf16* Wf[4];
 } pmlp_mlp_fwd_job;
 PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream);
 

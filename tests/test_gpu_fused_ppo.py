@@ -472,26 +472,28 @@ def test_load_between_learn_calls_reaches_the_captured_rollout(tmp_path):
 def test_fused_mlp_forward_is_bitwise_the_per_layer_gemms(M, rows):
     """pmlp_mlp_forward (both nets' 4 layers in one launch, activations in LDS) == the
     per-layer pmlp_gemm forward (af gather/convert, FWD_HIDDEN x3, FWD_OUT) bitwise: the
-    converted input rows, every hidden output and both outputs; ragged M included."""
+    converted input rows, every hidden output and both outputs; ragged M included; the
+    weights read row-major (W) and fragment-packed (Wf, the Adam mirror's second copy)."""
     torch.manual_seed(0)
     N, T, O, A = 1024, 24, 48, 12
     alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), num_learning_epochs=1,
               num_mini_batches=1, device="cuda")
     alg.init_storage(N, T, [O], [None], [A])
     f = alg._fused
-    assert f.fused_fwd
+    assert f.fused_fwd and f.wf is not None
     f.ensure_weights()
     g = torch.Generator(device="cuda").manual_seed(M)
     x = 2.0 * torch.randn(T * N, O, device="cuda", generator=g)
     idx = torch.randperm(T * N, device="cuda", generator=g)[:M] if rows else None
     outs = {}
-    for fused in (True, False):
+    for fused in ("frag", True, False):
         y = [[torch.full((M, lin.out_features), float("nan"), dtype=torch.bfloat16, device="cuda") for lin in ls[:-1]]
              for ls in f.lins]
         out = [torch.full((M, ls[-1].out_features), float("nan"), device="cuda") for ls in f.lins]
         xa = torch.full((M, f.k0p[0]), float("nan"), dtype=torch.bfloat16, device="cuda")
         if fused:
             mfma_mlp.mlp_forward([dict(x=x, kx=O, rows=idx, xa=xa if n == 0 else None, K0=f.k0p[n], W=f.wb[n],
+                                       Wf=f.wf[n] if fused == "frag" else None,
                                        b=[lin.bias.detach() for lin in f.lins[n]],
                                        N=[lin.out_features for lin in f.lins[n]], y=y[n], out=out[n])
                                   for n in range(2)], M)
@@ -508,9 +510,38 @@ def test_fused_mlp_forward_is_bitwise_the_per_layer_gemms(M, rows):
                 mfma_mlp._gemm(mfma_mlp.EPI_FWD_OUT if last else mfma_mlp.EPI_FWD_HIDDEN, gj)
         torch.cuda.synchronize()
         outs[fused] = (xa, y, out)
-    (xa1, y1, o1), (xa0, y0, o0) = outs[True], outs[False]
-    assert torch.equal(xa1, xa0)
+    for form in ("frag", True):
+        (xa1, y1, o1), (xa0, y0, o0) = outs[form], outs[False]
+        assert torch.equal(xa1, xa0)
+        for n in range(2):
+            for a, b in zip(y1[n], y0[n]):
+                assert torch.equal(a, b)
+            assert torch.equal(o1[n], o0[n])
+
+
+def test_adam_mirror_writes_the_fragment_packed_weights():
+    """After fused optimizer steps, the Adam mirror's fragment-packed copies (pmlp_mirror_job
+    .frag) equal frag_pack of its row-major bf16 copies, which equal bf16 of the fp32 weights."""
+    torch.manual_seed(0)
+    N, T, O, A = 512, 24, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), num_learning_epochs=1,
+              num_mini_batches=2, device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    st = alg.storage
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for k in ("observations", "actions", "values", "returns", "advantages", "mu"):
+        getattr(st, k).copy_(torch.randn(getattr(st, k).shape, device="cuda", generator=g))
+    st.sigma.fill_(1.0)
+    st.actions_log_prob.copy_(-12.0 + torch.randn(st.actions_log_prob.shape, device="cuda", generator=g))
+    st.step = T
+    f = alg._fused
+    assert f.wf is not None
+    alg.use_graph = False
+    alg.update()
+    torch.cuda.synchronize()
+    assert not f.weights_changed
     for n in range(2):
-        for a, b in zip(y1[n], y0[n]):
-            assert torch.equal(a, b)
-        assert torch.equal(o1[n], o0[n])
+        for l, lin in enumerate(f.lins[n]):
+            wb, wf = f.wb[n][l], f.wf[n][l]
+            assert torch.equal(wb[:lin.out_features, :lin.in_features], lin.weight.detach().to(torch.bfloat16))
+            assert torch.equal(wf, mfma_mlp.frag_pack(wb, wf.numel() // wb.shape[1]))

@@ -26,12 +26,16 @@ M = T * N // 4
 idx = torch.randperm(T * N, device="cuda")[:M]
 
 
-def jobs(M, rows, ys, nets=(0, 1)):
+x2 = x.clone()  # the same rows in another tensor: the kernel cannot reuse job 0's staged input
+
+
+def jobs(M, rows, ys, nets=(0, 1), frag=True, share=True):
     y = [[torch.empty((M, lin.out_features), dtype=torch.bfloat16, device="cuda") for lin in ls[:-1]]
          for ls in f.lins]
     out = [torch.empty((M, ls[-1].out_features), device="cuda") for ls in f.lins]
     xa = torch.empty((M, f.k0p[0]), dtype=torch.bfloat16, device="cuda")
-    return [dict(x=x, kx=O, rows=rows, xa=xa if (n == 0 and ys) else None, K0=f.k0p[n], W=f.wb[n],
+    return [dict(x=x if (n == 0 or share) else x2, kx=O, rows=rows, xa=xa if (n == 0 and ys) else None,
+                 K0=f.k0p[n], W=f.wb[n], Wf=f.wf[n] if (f.wf and frag) else None,
                  b=[lin.bias.detach() for lin in f.lins[n]], N=[lin.out_features for lin in f.lins[n]],
                  y=y[n] if ys else None, out=out[n]) for n in nets]
 
@@ -50,10 +54,13 @@ def time_it(js, M, R=200):
 
 
 cases = [("update: both nets, gather, y stores", jobs(M, idx, True), M),
+         ("update: .. critic input gathered again", jobs(M, idx, True, share=False), M),
+         ("update: .. row-major weights", jobs(M, idx, True, frag=False), M),
+         ("update: .. row-major, gathered again", jobs(M, idx, True, frag=False, share=False), M),
          ("update: no y stores", jobs(M, idx, False), M),
          ("update: no gather", jobs(M, None, True), M),
          ("update: actor only", jobs(M, idx, True, (0,)), M),
          ("rollout: 4096 rows, no y", jobs(N, None, False), N)]
 for rnd in range(2):
     for name, js, m in cases:
-        print(f"round {rnd}  {name:38s} {time_it(js, m):7.1f} us", flush=True)
+        print(f"round {rnd}  {name:42s} {time_it(js, m):7.1f} us", flush=True)

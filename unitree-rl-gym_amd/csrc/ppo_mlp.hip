@@ -1407,6 +1407,7 @@ struct MirrorJobs {
     int64_t off[PMLP_MAX_MIRROR];
     int rows[PMLP_MAX_MIRROR], cols[PMLP_MAX_MIRROR], ld[PMLP_MAX_MIRROR];
     bf16* dst[PMLP_MAX_MIRROR];
+    bf16* frag[PMLP_MAX_MIRROR];
     int n;
 };
 __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p, const float* __restrict__ g,
@@ -1439,6 +1440,9 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
                 // VALU sequence per element)
                 const int oi = (int)o, r = oi / mj.cols[j], c = oi - r * mj.cols[j];
                 mj.dst[j][(size_t)r * mj.ld[j] + c] = (bf16)pi;
+                if (mj.frag[j])  // the fragment-packed copy (include/ppo_mlp.h)
+                    mj.frag[j][((((size_t)(r >> 5) * (mj.ld[j] >> 4) + (c >> 4)) * 64 + (r & 31) + 32 * ((c >> 3) & 1))
+                                << 3) + (c & 7)] = (bf16)pi;
             }
         }
     }
@@ -1471,6 +1475,7 @@ struct FmlpJob {
     int ldy[3];
     float* out;             // fp32 [M, N[3]] (ld ldo)
     int ldo;
+    const bf16* Wf[4];      // optional fragment-packed W[l] (include/ppo_mlp.h)
 };
 struct FmlpJobs {
     FmlpJob j[2];
@@ -1479,19 +1484,16 @@ struct FmlpJobs {
 
 // One layer: D[R, N] = act(A[R, K] . W[N, K]^T + b), A in LDS (ld lda); wave w takes the
 // 32-column tiles w, w + 8, ...; every row tile of the workgroup per column tile, so a
-// B fragment (one 16-byte load per lane per k-step) feeds RT MFMAs.  A layer with fewer
-// column tiles than waves (128 -> 4 tiles, the output layer 1) splits each column tile's
-// row tiles between wpc waves instead of leaving waves idle (same chain per element).
+// B fragment (one 16-byte load per lane per k-step) feeds RT MFMAs.
 template <int R, bool LAST>
 __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const bf16* __restrict__ W,
+                                           const bf16* __restrict__ Wf,
                                            const float* __restrict__ bias, int N, bf16* D, int ldd,
                                            float* __restrict__ out, int ldo, int r0, int M) {
     constexpr int RT = R / 32, NW = FMLP_THREADS / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nct = (N + 31) >> 5, ks = K >> 4;
-    const int wpc = nct >= NW ? 1 : min(NW / nct, RT), part = wid % wpc;
-    const int i0 = part * RT / wpc, i1 = (part + 1) * RT / wpc;  // this wave's row tiles
-    for (int ct = wid / wpc; ct < nct; ct += NW / wpc) {
+    for (int ct = wid; ct < nct; ct += NW) {
         floatx16 acc[RT];
 #pragma unroll
         for (int i = 0; i < RT; ++i)
@@ -1499,7 +1501,10 @@ __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const 
             for (int t = 0; t < 16; ++t) acc[i][t] = 0.f;
         const int n = ct * 32 + (lane & 31);
         const bool nv = n < N;
-        const bf16* wrow = W + (size_t)(nv ? n : 0) * K + 8 * (lane >> 5);
+        // this lane's B fragment of k-step s at wrow + s * wstep: W[n][16 s + 8 (lane >> 5) ..]
+        // (32 row pieces per load), or the fragment-packed copy (1 KB contiguous per load)
+        const bf16* wrow = Wf ? Wf + ((size_t)ct * ks * 64 + lane) * 8 : W + (size_t)(nv ? n : 0) * K + 8 * (lane >> 5);
+        const int wstep = Wf ? 512 : 16;
         const bf16* arow = A + (lane & 31) * lda + 8 * (lane >> 5);
         // B fragments in groups of FG k-steps, the next group's loads in flight while this
         // group's MFMAs run (k ascending, as the per-layer GEMM).  The loads are unconditional,
@@ -1509,30 +1514,59 @@ __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const 
         constexpr int FG = 4;
         bf16x8 bq[FG], bn[FG];
         auto loadg = [&](int s0, bf16x8(&b)[FG]) {
+#if defined(PMLP_FMLP_STAMPS) && PMLP_FMLP_STAMPS == 2  // diagnostic: no weight loads
 #pragma unroll
-            for (int u = 0; u < FG; ++u) b[u] = *(const bf16x8*)(wrow + min(s0 + u, ks - 1) * 16);
+            for (int u = 0; u < FG; ++u)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) b[u][e] = (bf16)(float)(s0 + u + e + lane);
+#else
+#pragma unroll
+            for (int u = 0; u < FG; ++u) b[u] = *(const bf16x8*)(wrow + min(s0 + u, ks - 1) * wstep);
+#endif
         };
-        auto mfmas = [&](int s0, const bf16x8(&b)[FG]) {
+        // one k-step's RT MFMAs; the whole-group form has no branch between its MFMAs (a
+        // uniform branch per k-step splits the loop into blocks the scheduler cannot overlap)
+        auto step = [&](int s, const bf16x8& b) {
 #pragma unroll
-            for (int u = 0; u < FG; ++u) {
-                if (s0 + u < ks) {
-#pragma unroll
-                    for (int i = 0; i < RT; ++i) {
-                        if (i < i0 || i >= i1) continue;
-                        const bf16x8 af = *(const bf16x8*)(arow + i * 32 * lda + (s0 + u) * 16);
-                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[u], af, acc[i], 0, 0, 0);
-                    }
-                }
+            for (int i = 0; i < RT; ++i) {
+                const bf16x8 af = *(const bf16x8*)(arow + i * 32 * lda + s * 16);
+#if defined(PMLP_FMLP_STAMPS) && PMLP_FMLP_STAMPS == 3  // diagnostic: no MFMAs
+                acc[i][s & 15] += (float)af[0] * (float)b[0];
+#else
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, af, acc[i], 0, 0, 0);
+#endif
             }
         };
+        auto group = [&](int s0, const bf16x8(&b)[FG]) {
+#pragma unroll
+            for (int u = 0; u < FG; ++u) step(s0 + u, b[u]);
+        };
+        auto tail = [&](int s0, const bf16x8(&b)[FG]) {
+#pragma unroll
+            for (int u = 0; u < FG; ++u)
+                if (s0 + u < ks) step(s0 + u, b[u]);
+        };
+        // the epilogue's 16 bias values (this lane's columns), loaded ahead of the k-loop
+        float bq4[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                bq4[q][c] = bias ? bias[min(ct * 32 + 8 * q + 4 * (lane >> 5) + c, N - 1)] : 0.f;
         // two fragment sets used in turn (a register copy from one to the other would wait
         // for the loads it is meant to overlap)
         loadg(0, bq);
-        for (int s0 = 0; s0 < ks; s0 += 2 * FG) {
+        int s0 = 0;
+        for (; s0 + 2 * FG <= ks; s0 += 2 * FG) {
             loadg(s0 + FG, bn);
-            mfmas(s0, bq);
+            group(s0, bq);
             loadg(s0 + 2 * FG, bq);
-            mfmas(s0 + FG, bn);
+            group(s0 + FG, bn);
+        }
+        if (s0 < ks) {  // (ks not a multiple of 2 FG: the 48-wide input layer)
+            loadg(s0 + FG, bn);
+            tail(s0, bq);
+            tail(s0 + FG, bn);
         }
         // the tile was formed transposed (W . A^T: the weight fragment is the MFMA's first
         // operand), so a lane holds row (lane & 31) of its row tile and, per quad q, the 4
@@ -1543,23 +1577,19 @@ __device__ __forceinline__ void fmlp_layer(const bf16* A, int lda, int K, const 
         for (int q = 0; q < 4; ++q) {
             const int n0 = ct * 32 + 8 * q + 4 * (lane >> 5);
             if (LAST && n0 >= N) continue;
-            float bq4[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) bq4[c] = bias ? bias[min(n0 + c, N - 1)] : 0.f;
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
-                if (i < i0 || i >= i1) continue;
                 const int r = i * 32 + rl;
                 if constexpr (LAST) {
                     if (r0 + r < M) {
 #pragma unroll
                         for (int c = 0; c < 4; ++c)
-                            if (n0 + c < N) out[(size_t)(r0 + r) * ldo + n0 + c] = acc[i][4 * q + c] + bq4[c];
+                            if (n0 + c < N) out[(size_t)(r0 + r) * ldo + n0 + c] = acc[i][4 * q + c] + bq4[q][c];
                     }
                 } else {
                     bf16x4 v;
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) v[c] = (bf16)elu(acc[i][4 * q + c] + bq4[c]);
+                    for (int c = 0; c < 4; ++c) v[c] = (bf16)elu(acc[i][4 * q + c] + bq4[q][c]);
                     *(bf16x4*)(D + r * ldd + n0) = v;
                 }
             }
@@ -1599,17 +1629,28 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) 
     // y0 (then y2) and x (then y1); row strides 8 elements past the width: ds_read_b128
     // fragment reads of 32 consecutive rows hit 4-bank groups 4 apart (conflict-free)
     constexpr int LD0 = FMLP_MAX_H0 + 8, LD1 = FMLP_MAX_H1 + 8;
+    // the 96-row form keeps the input rows in a region of their own (LDX = 64 + 4: the 160 KB
+    // hold it), so a second job on the same rows (the critic on the actor's observations)
+    // does not gather them again; the 32-row form stages them in Y1 (3 workgroups per CU)
+    constexpr bool XR = R >= 96;
+    constexpr int LDX = 68;
     __shared__ __attribute__((aligned(16))) bf16 Y0[R * LD0];
     __shared__ __attribute__((aligned(16))) bf16 Y1[R * LD1];
+    __shared__ __attribute__((aligned(16))) bf16 X[XR ? R * LDX : 8];
+    bf16* const xs = XR ? X : Y1;
+    const int ldxs = XR ? LDX : LD1;
     const int r0 = blockIdx.x * R;
     const int jb = gridDim.y > 1 ? blockIdx.y : 0, je = gridDim.y > 1 ? blockIdx.y + 1 : jobs.njobs;
     for (int jj = jb; jj < je; ++jj) {
         const FmlpJob& J = jobs.j[jj];
         const int sb = 9 * (jj - jb);
         FMLP_STAMP(sb + 0);
+        const FmlpJob& P = jobs.j[jj > 0 ? jj - 1 : 0];
+        const bool same_rows = XR && jj > jb && !J.xa && J.x == P.x && J.rows == P.rows && J.ldx == P.ldx &&
+                               J.kx == P.kx && J.K0 == P.K0;
         // input rows: gathered, fp32 -> bf16 (columns >= kx are 0), into LDS (+ the bf16 copy)
         const int cpr = J.K0 >> 3;
-        for (int i = threadIdx.x; i < R * cpr; i += FMLP_THREADS) {
+        for (int i = threadIdx.x; i < (same_rows ? 0 : R * cpr); i += FMLP_THREADS) {
             const int r = i / cpr, k = (i - r * cpr) * 8, m = r0 + r;
             bf16x8 t;
 #pragma unroll
@@ -1626,26 +1667,26 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) 
                 }
                 if (J.xa) *(bf16x8*)(J.xa + (size_t)m * J.ldxa + k) = t;
             }
-            *(bf16x8*)(Y1 + r * LD1 + k) = t;
+            *(bf16x8*)(xs + r * ldxs + k) = t;
         }
         __syncthreads();
         FMLP_STAMP(sb + 1);
-        fmlp_layer<R, false>(Y1, LD1, J.K0, J.W[0], J.b[0], J.N[0], Y0, LD0, nullptr, 0, r0, M);
+        fmlp_layer<R, false>(xs, ldxs, J.K0, J.W[0], J.Wf[0], J.b[0], J.N[0], Y0, LD0, nullptr, 0, r0, M);
         FMLP_STAMP(sb + 2);
         __syncthreads();
         fmlp_store<R>(Y0, LD0, J.N[0], J.y[0], J.ldy[0], r0, M);
         FMLP_STAMP(sb + 3);
-        fmlp_layer<R, false>(Y0, LD0, J.N[0], J.W[1], J.b[1], J.N[1], Y1, LD1, nullptr, 0, r0, M);
+        fmlp_layer<R, false>(Y0, LD0, J.N[0], J.W[1], J.Wf[1], J.b[1], J.N[1], Y1, LD1, nullptr, 0, r0, M);
         FMLP_STAMP(sb + 4);
         __syncthreads();
         fmlp_store<R>(Y1, LD1, J.N[1], J.y[1], J.ldy[1], r0, M);
         FMLP_STAMP(sb + 5);
-        fmlp_layer<R, false>(Y1, LD1, J.N[1], J.W[2], J.b[2], J.N[2], Y0, LD0, nullptr, 0, r0, M);
+        fmlp_layer<R, false>(Y1, LD1, J.N[1], J.W[2], J.Wf[2], J.b[2], J.N[2], Y0, LD0, nullptr, 0, r0, M);
         FMLP_STAMP(sb + 6);
         __syncthreads();
         fmlp_store<R>(Y0, LD0, J.N[2], J.y[2], J.ldy[2], r0, M);
         FMLP_STAMP(sb + 7);
-        fmlp_layer<R, true>(Y0, LD0, J.N[2], J.W[3], J.b[3], J.N[3], nullptr, 0, J.out, J.ldo, r0, M);
+        fmlp_layer<R, true>(Y0, LD0, J.N[2], J.W[3], J.Wf[3], J.b[3], J.N[3], nullptr, 0, J.out, J.ldo, r0, M);
         __syncthreads();  // (the next job restages x over y1)
         FMLP_STAMP(sb + 8);
     }
@@ -2234,9 +2275,10 @@ PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, f
     for (int j = 0; j < nmirror; ++j) {
         const pmlp_mirror_job& J = mirror[j];
         if (!J.dst || J.offset < 0 || J.rows <= 0 || J.cols <= 0 || J.ld < J.cols ||
-            J.offset + (int64_t)J.rows * J.cols > n)
+            J.offset + (int64_t)J.rows * J.cols > n || (J.frag && J.ld % 16))
             return fail(-1, "pmlp_adam_mirror: bad mirror job " + std::to_string(j));
         mj.off[j] = J.offset; mj.rows[j] = J.rows; mj.cols[j] = J.cols; mj.ld[j] = J.ld; mj.dst[j] = (bf16*)J.dst;
+        mj.frag[j] = (bf16*)J.frag;
     }
     // grid cap 1024 blocks: for the Go2 parameters (1,486 blocks at one element per thread)
     // uncapped / 1024 / 512 / 256 measured 9.2-9.5 / 7.5-8.1 / 8.5-10.0 / 12.1-12.7 us
@@ -2331,7 +2373,9 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
         if (J.N[3] <= 0 || J.N[3] > 32 || !J.out || J.ldo < J.N[3]) return fail(-1, w + "output: 0 < N3 <= 32, ldo >= N3");
         FmlpJob& f = fj.j[i];
         f.x = J.x; f.rows = J.rows; f.ldx = J.ldx; f.kx = J.kx; f.xa = (bf16*)J.xa; f.ldxa = J.ldxa;
-        for (int l = 0; l < 4; ++l) { f.W[l] = (const bf16*)J.W[l]; f.b[l] = J.b[l]; f.N[l] = J.N[l]; }
+        for (int l = 0; l < 4; ++l) {
+            f.W[l] = (const bf16*)J.W[l]; f.Wf[l] = (const bf16*)J.Wf[l]; f.b[l] = J.b[l]; f.N[l] = J.N[l];
+        }
         f.K0 = J.K0;
         for (int l = 0; l < 3; ++l) { f.y[l] = (bf16*)J.y[l]; f.ldy[l] = J.ldy[l]; }
         f.out = J.out; f.ldo = J.ldo;
@@ -2339,7 +2383,8 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
     // rows per workgroup: 96 (one 150 KB workgroup per CU, every job in turn) for the update's
     // mini-batches; 32 with one job per workgroup for the rollout's num_envs rows
     hipStream_t st = (hipStream_t)stream;
-    if (M >= 96 * 192)
+    static const int rows_ab = getenv("PMLP_FMLP_ROWS") ? atoi(getenv("PMLP_FMLP_ROWS")) : 0;  // (A/B knob)
+    if (rows_ab ? rows_ab == 96 : M >= 96 * 192)
         hipLaunchKernelGGL(k_mlp_fwd<96>, dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0, st, fj, M);
     else
         hipLaunchKernelGGL(k_mlp_fwd<32>, dim3((M + 31) / 32, njobs), dim3(FMLP_THREADS), 0, st, fj, M);

@@ -97,10 +97,6 @@ class FusedPPOStep:
         self.tn = os.environ.get("PMLP_TN", "1") != "0"
         self.sync_optimizer_state(alg.optimizer)
         self._alloc()
-        # the whole forward of both nets in ONE launch (pmlp_mlp_forward: activations kept on
-        # chip between layers, bitwise the per-layer GEMMs); PMLP_FUSED_FWD=0: per-layer GEMMs
-        self.fused_fwd = os.environ.get("PMLP_FUSED_FWD", "1") != "0" and self.tn and \
-            all(mm.mlp_forward_supported(self.lins[n], self.k0p[n]) for n in range(2))
 
     # ------------------------------------------------------------ buffers --
     def _alloc(self):
@@ -123,9 +119,17 @@ class FusedPPOStep:
         self.wb = [[torch.zeros(_ceil8(lin.out_features) if l == len(ls) - 1 else lin.out_features,
                                 self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
                     for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
+        # the whole forward of both nets in ONE launch (pmlp_mlp_forward: activations kept on
+        # chip between layers, bitwise the per-layer GEMMs); PMLP_FUSED_FWD=0: per-layer GEMMs
+        self.fused_fwd = os.environ.get("PMLP_FUSED_FWD", "1") != "0" and self.tn and \
+            all(mm.mlp_forward_supported(self.lins[n], self.k0p[n]) for n in range(2))
+        # its weight operands fragment-packed (include/ppo_mlp.h, pmlp_mirror_job.frag): one
+        # contiguous 1 KB per wave and k-step; PMLP_FRAG_W=0 reads the row-major wb instead
+        self.wf = [[torch.zeros(-(-w.shape[0] // 32) * 32 * w.shape[1], dtype=bf, device=dev) for w in ws]
+                   for ws in self.wb] if self.fused_fwd and os.environ.get("PMLP_FRAG_W", "1") != "0" else None
         self.mirror = (mm.MirrorJob * (2 * len(self.lins[0])))(*[
             mm.MirrorJob(self._offset[id(lin.weight)], lin.out_features, lin.in_features, self.wb[n][l].shape[1],
-                         self.wb[n][l].data_ptr())
+                         self.wb[n][l].data_ptr(), self.wf[n][l].data_ptr() if self.wf else None)
             for n, ls in enumerate(self.lins) for l, lin in enumerate(ls)])
         self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
         self.yt = [[None if tn else
@@ -196,6 +200,10 @@ class FusedPPOStep:
             for l, lin in enumerate(self.lins[n]):
                 jobs.append((lin.weight.detach(), self.wb[n][l].shape[1], self.wb[n][l][:lin.out_features], None))
         mm._convert(jobs)
+        if self.wf:
+            for n in range(2):
+                for wb, wf in zip(self.wb[n], self.wf[n]):
+                    wf.copy_(mm.frag_pack(wb, wf.numel() // wb.shape[1]))
         self.weights_changed = False
 
     # -------------------------------------------------------------- step ----
@@ -225,7 +233,8 @@ class FusedPPOStep:
         if self.fused_fwd:
             mm.mlp_forward([dict(x=fobs[n], kx=self.lins[n][0].in_features, rows=rows,
                                  xa=self.xb[n] if (n == 0 or not shared) else None, K0=self.k0p[n],
-                                 W=self.wb[n], b=[lin.bias.detach() for lin in self.lins[n]],
+                                 W=self.wb[n], Wf=self.wf[n] if self.wf else None,
+                                 b=[lin.bias.detach() for lin in self.lins[n]],
                                  N=[lin.out_features for lin in self.lins[n]], y=self.y[n], out=self.out[n])
                             for n in range(2)], M)
         for l in range(L if not self.fused_fwd else 0):
@@ -354,7 +363,7 @@ class FusedRollout:
         xs = [obs, cobs]
         if f.fused_fwd:  # one launch for both nets (pmlp_mlp_forward)
             mm.mlp_forward([dict(x=xs[n], kx=f.lins[n][0].in_features, K0=f.k0p[n], W=f.wb[n],
-                                 b=[lin.bias.detach() for lin in f.lins[n]],
+                                 Wf=f.wf[n] if f.wf else None, b=[lin.bias.detach() for lin in f.lins[n]],
                                  N=[lin.out_features for lin in f.lins[n]], out=self.out[n]) for n in range(2)], N)
             return self.out
         for l in range(f.L):

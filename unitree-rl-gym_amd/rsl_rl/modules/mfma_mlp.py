@@ -47,7 +47,7 @@ class GemmJob(C.Structure):
 
 class MirrorJob(C.Structure):
     _fields_ = [("offset", C.c_int64), ("rows", C.c_int32), ("cols", C.c_int32), ("ld", C.c_int32),
-                ("dst", C.c_void_p)]
+                ("dst", C.c_void_p), ("frag", C.c_void_p)]
 
 
 class ReduceJob(C.Structure):
@@ -64,7 +64,7 @@ class MlpFwdJob(C.Structure):
     _fields_ = [("x", C.c_void_p), ("rows", C.c_void_p), ("ldx", C.c_int32), ("kx", C.c_int32), ("xa", C.c_void_p),
                 ("ldxa", C.c_int32), ("W", C.c_void_p * 4), ("b", C.c_void_p * 4), ("N", C.c_int32 * 4),
                 ("K0", C.c_int32), ("y", C.c_void_p * 3), ("ldy", C.c_int32 * 3), ("out", C.c_void_p),
-                ("ldo", C.c_int32)]
+                ("ldo", C.c_int32), ("Wf", C.c_void_p * 4)]
 
 
 class HeadJob(C.Structure):
@@ -165,11 +165,22 @@ def mlp_forward_supported(lins, k0p):
         lins[3].out_features <= 32
 
 
+def frag_pack(w, rows32):
+    """The fragment-packed copy of a bf16 weight w [R, K] (K a multiple of 16) that
+    pmlp_mlp_forward's Wf reads and pmlp_mirror_job.frag writes (include/ppo_mlp.h): rows
+    zero-padded to rows32 (a multiple of 32), element (r, c) at
+    ((((r / 32) * (K / 16) + c / 16) * 64 + r % 32 + 32 * ((c / 8) % 2)) * 8 + c % 8."""
+    R, K = w.shape
+    p = torch.zeros(rows32, K, dtype=w.dtype, device=w.device)
+    p[:R] = w
+    return p.view(rows32 // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).reshape(-1)
+
+
 def mlp_forward(nets, M):
     """One launch of the whole forward of up to two 4-layer MLPs (pmlp_mlp_forward).  nets:
     dicts x (fp32 [*, ldx]), kx, rows (int64 [M] | None), xa (bf16 [M, K0] | None), K0,
-    W (4 bf16 [N, K] tensors), b (4 fp32 tensors), N (4 ints), y (3 bf16 [M, N] tensors or
-    None), out (fp32 [M, N3])."""
+    W (4 bf16 [N, K] tensors), Wf (None or 4 frag_pack copies of W), b (4 fp32 tensors),
+    N (4 ints), y (3 bf16 [M, N] tensors or None), out (fp32 [M, N3])."""
     def mk(n):
         y = n.get("y") or (None, None, None)
         return MlpFwdJob(_p(n["x"]), _p(n.get("rows")), n["x"].stride(0), n["kx"], _p(n.get("xa")),
@@ -177,7 +188,7 @@ def mlp_forward(nets, M):
                          (C.c_void_p * 4)(*[_p(w) for w in n["W"]]), (C.c_void_p * 4)(*[_p(b) for b in n["b"]]),
                          (C.c_int32 * 4)(*n["N"]), n["K0"], (C.c_void_p * 3)(*[_p(t) for t in y]),
                          (C.c_int32 * 3)(*[0 if t is None else t.stride(0) for t in y]), _p(n["out"]),
-                         n["out"].stride(0))
+                         n["out"].stride(0), (C.c_void_p * 4)(*[_p(w) for w in (n.get("Wf") or (None,) * 4)]))
     arr = (MlpFwdJob * len(nets))(*[mk(n) for n in nets])
     _ok(load().pmlp_mlp_forward(len(nets), arr, int(M), _stream()), "pmlp_mlp_forward")
 
