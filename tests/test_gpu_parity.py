@@ -372,6 +372,26 @@ def test_two_envs_per_wave_is_bitwise_one_env_per_wave(monkeypatch):
     assert_exact(outs[1], outs[0], STATE + POST, 512, "two envs per wave vs one")
 
 
+@pytest.mark.parametrize("task", ["h1", "g1", "h1_2"])
+def test_humanoid_32_row_variant_two_envs_per_wave(task, monkeypatch):
+    """The humanoids' 32-row capacity (8 contacts: 4 sole corners per foot, 8 limit rows)
+    runs two envs per wave like Go2; it must equal the oracle bit for bit and the
+    one-env-per-wave build of the same capacity over a rollout with resets."""
+    from legged_gym.envs.base.humanoid import HumanoidRobot
+    monkeypatch.setattr(HumanoidRobot, "max_contacts", 8)
+    monkeypatch.setattr(HumanoidRobot, "max_rows", 32)
+    monkeypatch.setattr(HumanoidRobot, "max_self_contacts", 2)
+    outs = []
+    for epw in ("1", "2"):
+        monkeypatch.setenv("LGS_ENVS_PER_WAVE", epw)
+        env, g = warm(task, 256, steps=40, seed=5)
+        outs.append(env_arrays(env))
+        if epw == "2":
+            fused_vs_oracle(env, g, 2, f"{task} 32 rows")
+        env.close()
+    assert_exact(outs[1], outs[0], STATE + POST, 256, f"{task} 32 rows: two envs per wave vs one")
+
+
 # --------------------------------------------------- another robot (plugin) --
 def _register_g1_23dof():
     """A plugin task on a robot the built-in kernels do not cover: the G1 23-DOF description

@@ -2023,7 +2023,7 @@ struct lgs_sim {
 // row capacity sets the LDS footprint (Y, A): the 32-row variant is the Go2 one.  The
 // chain length CH is the sparsity the Cholesky exploits (l_nz); a tree that is not
 // D/CH equal chains hanging from the base takes the dense (CH = 0) variant.
-enum Variant { V_12_19, V_12_13, V_10_11, V_12_19_48, V_EXTRA, V_NONE };
+enum Variant { V_12_19, V_12_13_32, V_10_11_32, V_12_13, V_10_11, V_12_19_48, V_EXTRA, V_NONE };
 
 // Build-time instantiation hook for other robots: every X(D, B) listed here compiles the
 // 48-row, one-env-per-wave kernels (dense Cholesky) for models with exactly D DOFs and at
@@ -2044,6 +2044,9 @@ static bool extra_shape(const lgs_sim* s) {
 }
 
 static Variant pick(const lgs_sim* s) {
+    // 32-row humanoid variants (8 contacts): two envs per wave, as Go2
+    if (s->D == 12 && s->B <= 13 && s->rows <= 32) return V_12_13_32;
+    if (s->D == 10 && s->B <= 11 && s->rows <= 32) return V_10_11_32;
     if (s->D == 12 && s->B <= 19 && s->rows <= 32) return V_12_19;
     if (s->D == 12 && s->B <= 13) return V_12_13;
     if (s->D == 12 && s->B <= 19) return V_12_19_48;
@@ -2051,8 +2054,10 @@ static Variant pick(const lgs_sim* s) {
     if (extra_shape(s)) return V_EXTRA;
     return V_NONE;
 }
-static int variant_rows(Variant v) { return v == V_12_19 ? 32 : 48; }  // (V_EXTRA: 48)
-static int variant_chain(Variant v) { return v == V_12_13 ? 6 : (v == V_10_11 ? 5 : 3); }
+static int variant_rows(Variant v) { return (v == V_12_19 || v == V_12_13_32 || v == V_10_11_32) ? 32 : 48; }  // (V_EXTRA: 48)
+static int variant_chain(Variant v) {
+    return (v == V_12_13 || v == V_12_13_32) ? 6 : ((v == V_10_11 || v == V_10_11_32) ? 5 : 3);
+}
 
 #define LGS_LAUNCH(sim, KERNEL, D_, B_, R_, ...)                                                         \
     do {                                                                                                 \
@@ -2140,6 +2145,14 @@ static int extra_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_tas
         if ((sim)->epw == 2) LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 2, __VA_ARGS__);                     \
         else LGS_LAUNCH_EPW(sim, KERNEL, 12, 19, 32, 1, __VA_ARGS__);                                     \
         break;                                                                                            \
+    case V_12_13_32:                                                                                      \
+        if ((sim)->epw == 2) LGS_LAUNCH_EPW(sim, KERNEL, 12, 13, 32, 2, __VA_ARGS__);                     \
+        else LGS_LAUNCH_EPW(sim, KERNEL, 12, 13, 32, 1, __VA_ARGS__);                                     \
+        break;                                                                                            \
+    case V_10_11_32:                                                                                      \
+        if ((sim)->epw == 2) LGS_LAUNCH_EPW(sim, KERNEL, 10, 11, 32, 2, __VA_ARGS__);                     \
+        else LGS_LAUNCH_EPW(sim, KERNEL, 10, 11, 32, 1, __VA_ARGS__);                                     \
+        break;                                                                                            \
     case V_12_13: LGS_LAUNCH_48(sim, KERNEL, 12, 13, __VA_ARGS__); break;                                 \
     case V_10_11: LGS_LAUNCH_48(sim, KERNEL, 10, 11, __VA_ARGS__); break;                                 \
     case V_12_19_48: LGS_LAUNCH_48(sim, KERNEL, 12, 19, __VA_ARGS__); break;                              \
@@ -2148,6 +2161,8 @@ static int extra_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_tas
 #define LGS_DISPATCH(sim, KERNEL, ...)                                                                    \
     switch (pick(sim)) {                                                                                  \
     case V_12_19: LGS_LAUNCH(sim, KERNEL, 12, 19, 32, __VA_ARGS__); break;                                \
+    case V_12_13_32: LGS_LAUNCH(sim, KERNEL, 12, 13, 32, __VA_ARGS__); break;                             \
+    case V_10_11_32: LGS_LAUNCH(sim, KERNEL, 10, 11, 32, __VA_ARGS__); break;                             \
     case V_12_13: LGS_LAUNCH(sim, KERNEL, 12, 13, 48, __VA_ARGS__); break;                                \
     case V_10_11: LGS_LAUNCH(sim, KERNEL, 10, 11, 48, __VA_ARGS__); break;                                \
     case V_12_19_48: LGS_LAUNCH(sim, KERNEL, 12, 19, 48, __VA_ARGS__); break;                             \
@@ -2209,7 +2224,8 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     {
         const char* ev = getenv("LGS_ENVS_PER_WAVE");
         const bool one = ev && atoi(ev) == 1;
-        s->epw = (!one && num_envs % 2 == 0 && s->D == 12 && s->B <= 19 && s->rows <= 32) ? 2 : 1;
+        const Variant v = pick(s);
+        s->epw = (!one && num_envs % 2 == 0 && (v == V_12_19 || v == V_12_13_32 || v == V_10_11_32)) ? 2 : 1;
     }
     if (pick(s) == V_NONE) {
         delete s;

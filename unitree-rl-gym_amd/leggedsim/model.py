@@ -85,14 +85,47 @@ class Model:
         return m
 
     def reorder_points(self, first_bodies):
-        """Put the contact candidates of ``first_bodies`` first (contact-slot priority
-        when more candidates touch than the solver has rows for)."""
-        pri = np.array([0 if b in first_bodies else 1 for b in self.pt_body])
-        order = np.argsort(pri, kind="stable")
+        """Put the contact candidates of ``first_bodies`` (the feet) first: the contact
+        kernel fills its slots with the touching candidates in index order, so this is
+        the slot priority when more candidates touch than the solver has rows for.
+
+        The feet's candidates are dealt round-robin over the feet (1st of every foot,
+        then the 2nd, ...), and each foot's own list starts with its sole points in
+        farthest-point order: with two flat soles down and 8 slots, each foot gets 4
+        spread-out sole corners (PhysX's convex-vs-plane manifold also keeps at most 4
+        points per patch) instead of one foot taking every slot.  A foot with one
+        candidate (Go2) keeps the previous order exactly."""
+        feet = sorted(set(int(b) for b in first_bodies))
+        per_foot = [self._sole_first_order(np.nonzero(self.pt_body == b)[0]) for b in feet]
+        head = []
+        for k in range(max((len(p) for p in per_foot), default=0)):
+            head.extend(int(p[k]) for p in per_foot if k < len(p))
+        in_head = np.zeros(len(self.pt_body), bool)
+        in_head[head] = True
+        order = np.array(head + [i for i in range(len(self.pt_body)) if not in_head[i]], dtype=np.int64)
         self.pt_body = self.pt_body[order].copy()
         self.pt_pos = self.pt_pos[order].copy()
         self.pt_radius = self.pt_radius[order].copy()
         self.pt_shape = self.pt_shape[order].copy()
+
+    def _sole_first_order(self, idx, sole_band=0.005):
+        """Indices idx of one body's candidates: the sole (sphere bottoms within
+        sole_band of the lowest, body frame) in farthest-point order over x-y, starting
+        from the one farthest from the sole's centre; then the rest in their order."""
+        if len(idx) <= 1:
+            return list(idx)
+        bottom = self.pt_pos[idx, 2] - self.pt_radius[idx]
+        sole = [int(i) for i, z in zip(idx, bottom) if z <= bottom.min() + sole_band]
+        xy = self.pt_pos[sole, :2].astype(np.float64)
+        first = int(np.argmax(((xy - xy.mean(0)) ** 2).sum(1)))
+        chosen, dist = [first], ((xy - xy[first]) ** 2).sum(1)
+        while len(chosen) < len(sole):
+            dist[chosen] = -1.0
+            nxt = int(np.argmax(dist))  # ties: the lowest index
+            chosen.append(nxt)
+            dist = np.minimum(dist, ((xy - xy[nxt]) ** 2).sum(1))
+        ordered = [sole[c] for c in chosen]
+        return ordered + [int(i) for i in idx if int(i) not in set(ordered)]
 
 
 def _shape_points(s):
