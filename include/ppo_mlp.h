@@ -357,5 +357,22 @@ PMLP_API int32_t pmlp_lstm_bwd_dw_blocks(int32_t B);
 PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* whh, const float* c0,
                                    const uint8_t* reset, const float* c_out, const float* gact, const float* dh_out,
                                    const float* xh, float* slab, void* stream);
+/* The actor's and the critic's memory in ONE launch each way (rsl_rl ActorCriticRecurrent's
+ * memory_a / memory_c: independent sequences over the same [T, B] mini-batch and reset mask;
+ * one 2,048-env mini-batch is 128 workgroups, half of the 256 CUs).  Per job exactly
+ * pmlp_lstm_fwd_mfma (x, w_ih, b_ih, b_hh, w_hh, h0, c0 -> h_out, c_out, gact, xh) and
+ * pmlp_lstm_bwd_dw_mfma (w_hh, c0, c_out, gact, dh_out, xh -> slab).  1 <= njobs <= 2. */
+typedef struct pmlp_lstm_job {
+    int32_t I;                                   /* input width, 1..63                   */
+    const float *x, *w_ih, *b_ih, *b_hh, *w_hh;  /* [T,B,I], torch nn.LSTM parameters   */
+    const float *h0, *c0;                        /* [B,64] state the sequence starts from */
+    float *h_out, *c_out, *gact, *xh;            /* forward outputs (backward inputs)     */
+    const float* dh_out;                         /* backward: gradient of h_out [T,B,64]  */
+    float* slab;                                 /* backward: weight-gradient partials    */
+} pmlp_lstm_job;
+PMLP_API int pmlp_lstm_fwd_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
+                                     const uint8_t* reset, void* stream);
+PMLP_API int pmlp_lstm_bwd_dw_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
+                                        const uint8_t* reset, void* stream);
 
 #endif

@@ -39,11 +39,14 @@ def test_ctypes_job_structs_match_c_layout(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "ppo_mlp.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
                    ' sizeof(pmlp_gemm_job), sizeof(pmlp_mirror_job), sizeof(pmlp_convert_job),'
-                   ' sizeof(pmlp_reduce_job)); return 0;}\n')
+                   ' sizeof(pmlp_reduce_job)); printf("%zu %zu\\n", sizeof(pmlp_head_job), sizeof(pmlp_lstm_job));'
+                   ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
-    assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob)]
+    from rsl_rl.modules import lstm_seq
+    assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob),
+                   C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob)]
 
 
 def _job(**kw):
@@ -99,6 +102,12 @@ def test_recurrent_and_bookkeeping_entries_refuse_bad_arguments(lib):
     assert L.pmlp_lstm_fwd_x(4, 8, 64, 65, 16, 16, None, None, 16, None, None, None, None, None, None, None, None,
                              None, None) != 0  # input wider than 64
     assert b"input size" in L.pmlp_lstm_last_error()
+    jobs = (lstm_seq.LstmJob * 3)()
+    assert L.pmlp_lstm_fwd_mfma_jobs(3, jobs, 24, 64, 64, None, None) != 0  # at most two memories
+    assert b"1..2 jobs" in L.pmlp_lstm_last_error()
+    jobs[0].I = 44
+    assert L.pmlp_lstm_bwd_dw_mfma_jobs(1, jobs, 24, 64, 64, None, None) != 0  # null buffers
+    assert b"pmlp_lstm_bwd_dw_mfma_jobs" in L.pmlp_lstm_last_error()
     lib.pmlp_loss_bookkeeping.restype = C.c_int
     assert lib.pmlp_loss_bookkeeping(None, None, None, C.c_float(0.01), 1, None) != 0
     assert b"pmlp_loss_bookkeeping" in lib.pmlp_last_error()

@@ -403,13 +403,20 @@ __device__ __forceinline__ float ror8(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
 }
 
+// Up to two independent sequences per launch (the actor's and the critic's memory: a
+// 2,048-env mini-batch is 128 workgroups, half the CUs, so one launch of both fills them):
+// blockIdx.y selects the job; a job with fewer workgroups than the grid's x leaves the rest.
+struct MFwdBatch { MFwdArgs m[2]; };
+
 template <int SPLIT>
-__global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdArgs a) {
+__global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab) {
     constexpr int NP = SPLIT == 3 ? 2 : 1;  // operand parts (hi, lo)
     __shared__ __attribute__((aligned(16))) mbf16 A[NP][2][ME * MLDA];
+    const MFwdArgs a = ab.m[blockIdx.y];
     const int T = a.T, B = a.B, I = a.I, RL = I + MH + 1;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int e0 = blockIdx.x * ME;
+    if (e0 >= B) return;  // (whole workgroup)
     const int j = lane & 15, rg = lane >> 4;  // column in the tile; row group (envs 4 rg .. 4 rg + 3)
     const int hj = j >> 3;                    // 0: this column holds i / g, 1: f / o
     const int uu = 8 * w + (j & 7);           // this lane's unit
@@ -579,9 +586,13 @@ struct MBwdArgs {
 constexpr int MXC = 128;  // xh columns covered (I + H + 1 <= 128)
 typedef float mfloatx16 __attribute__((ext_vector_type(16)));
 
+struct MBwdBatch { MBwdArgs m[2]; };  // as MFwdBatch
+
 template <int SPLIT, bool DW>
-__global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdArgs a) {
+__global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) {
     constexpr int NP = SPLIT == 3 ? 2 : 1;
+    const MBwdArgs a = ab.m[blockIdx.y];
+    if ((int)blockIdx.x * ME >= a.B) return;  // (whole workgroup)
     __shared__ __attribute__((aligned(16))) mbf16 G[NP][2][ME * MLDG];
     // DW operands, transposed so a fragment is 8 consecutive envs (one 16-byte read):
     // GT[perm gate col][env], XT[xh col][env]
@@ -1165,7 +1176,8 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
                                 const uint8_t* reset, float* h_out, float* c_out, float* gact, float* xh, void* stream) {
     if (T <= 0 || B <= 0 || !x || !wih || !bih || !bhh || !whh) return fail("pmlp_lstm_fwd_mfma: empty sequence or null input");
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
-    MFwdArgs a{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh, nullptr, nullptr};
+    MFwdBatch a{};
+    a.m[0] = MFwdArgs{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh, nullptr, nullptr};
     hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma: ") + hipGetErrorString(e));
@@ -1176,7 +1188,8 @@ PMLP_API int pmlp_lstm_bwd_mfma(int32_t T, int32_t B, int32_t H, const float* wh
                                 float* dgx, void* stream) {
     if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !dgx) return fail("pmlp_lstm_bwd_mfma: null buffer");
     if (H != MH) return fail("pmlp_lstm_bwd_mfma: hidden 64");
-    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, dgx, nullptr, 0, nullptr};
+    MBwdBatch a{};
+    a.m[0] = MBwdArgs{T, B, whh, c0, reset, c_out, gact, dh_out, dgx, nullptr, 0, nullptr};
     hipLaunchKernelGGL((k_lstm_bwd_mfma<3, false>), dim3((B + ME - 1) / ME), dim3(256), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_mfma: ") + hipGetErrorString(e));
@@ -1190,7 +1203,8 @@ PMLP_API int pmlp_lstm_bwd_dw_mfma(int32_t T, int32_t B, int32_t H, int32_t I, c
     if (T <= 0 || B <= 0 || !whh || !c_out || !gact || !dh_out || !xh || !slab)
         return fail("pmlp_lstm_bwd_dw_mfma: null buffer");
     if (H != MH || I <= 0 || I + MH + 1 > MXC) return fail("pmlp_lstm_bwd_dw_mfma: hidden 64, I + 65 <= 128");
-    MBwdArgs a{T, B, whh, c0, reset, c_out, gact, dh_out, nullptr, xh, I, slab};
+    MBwdBatch a{};
+    a.m[0] = MBwdArgs{T, B, whh, c0, reset, c_out, gact, dh_out, nullptr, xh, I, slab};
     hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma: ") + hipGetErrorString(e));
@@ -1258,8 +1272,52 @@ PMLP_API int pmlp_lstm_step_mfma(int32_t B, int32_t H, int32_t I, const float* x
     if (B <= 0 || !x || !wih || !bih || !bhh || !whh || !h || !c) return fail("pmlp_lstm_step_mfma: null input");
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_step_mfma: hidden 64, input 1..64");
     if ((h_save == nullptr) != (c_save == nullptr)) return fail("pmlp_lstm_step_mfma: h_save and c_save together");
-    MFwdArgs a{1, B, I, x, wih, bih, bhh, whh, h, c, nullptr, h, c, nullptr, nullptr, h_save, c_save};
+    MFwdBatch a{};
+    a.m[0] = MFwdArgs{1, B, I, x, wih, bih, bhh, whh, h, c, nullptr, h, c, nullptr, nullptr, h_save, c_save};
     hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma: ") + hipGetErrorString(e));
+}
+
+/* Both memories of the fused recurrent step in one launch each way (include/ppo_mlp.h,
+ * pmlp_lstm_job): the same kernels and arithmetic as pmlp_lstm_fwd_mfma /
+ * pmlp_lstm_bwd_dw_mfma per job, the jobs side by side in the grid's y. */
+static int lstm_jobs_check(const char* w, int njobs, const pmlp_lstm_job* jobs, int T, int B, int H, bool bwd) {
+    if (njobs < 1 || njobs > 2 || !jobs || T <= 0 || B <= 0) return fail(std::string(w) + ": 1..2 jobs, T, B > 0");
+    if (H != MH) return fail(std::string(w) + ": hidden 64");
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_lstm_job& J = jobs[i];
+        if (J.I <= 0 || J.I > MKX || J.I + MH + 1 > MXC) return fail(std::string(w) + ": input 1..63");
+        if (!J.w_hh || !J.c_out || !J.gact || !J.xh) return fail(std::string(w) + ": null w_hh / c_out / gact / xh");
+        if (!bwd && (!J.x || !J.w_ih || !J.b_ih || !J.b_hh || !J.h_out)) return fail(std::string(w) + ": null forward input");
+        if (bwd && (!J.dh_out || !J.slab)) return fail(std::string(w) + ": null dh_out / slab");
+    }
+    return 0;
+}
+
+PMLP_API int pmlp_lstm_fwd_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
+                                     const uint8_t* reset, void* stream) {
+    if (int e = lstm_jobs_check("pmlp_lstm_fwd_mfma_jobs", njobs, jobs, T, B, H, false)) return e;
+    MFwdBatch a{};
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_lstm_job& J = jobs[i];
+        a.m[i] = MFwdArgs{T, B, J.I, J.x, J.w_ih, J.b_ih, J.b_hh, J.w_hh, J.h0, J.c0, reset,
+                          J.h_out, J.c_out, J.gact, J.xh, nullptr, nullptr};
+    }
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma_jobs: ") + hipGetErrorString(e));
+}
+
+PMLP_API int pmlp_lstm_bwd_dw_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
+                                        const uint8_t* reset, void* stream) {
+    if (int e = lstm_jobs_check("pmlp_lstm_bwd_dw_mfma_jobs", njobs, jobs, T, B, H, true)) return e;
+    MBwdBatch a{};
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_lstm_job& J = jobs[i];
+        a.m[i] = MBwdArgs{T, B, J.w_hh, J.c0, reset, J.c_out, J.gact, J.dh_out, nullptr, J.xh, J.I, J.slab};
+    }
+    hipLaunchKernelGGL((k_lstm_bwd_mfma<3, true>), dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma_jobs: ") + hipGetErrorString(e));
 }

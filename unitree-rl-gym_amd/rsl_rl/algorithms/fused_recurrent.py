@@ -1,5 +1,5 @@
 """One PPO mini-batch optimizer step of the recurrent actor-critic (ActorCriticRecurrent:
-one-layer LSTM memories + Linear/ELU/Linear heads, the G1 / H1 / H1_2 policies) as ~14
+one-layer LSTM memories + Linear/ELU/Linear heads, the G1 / H1 / H1_2 policies) as ~12
 kernel launches, with no autograd (rsl_rl v1.0.2 PPO.update body on the dense recurrent
 mini-batches; the dense form is storage.recurrent_dense_mini_batch_generator).
 
@@ -7,12 +7,14 @@ What the autograd update ran per mini-batch: the two LSTM kernels, ~10 library G
 heads' forward and backward, ELU / ELU' / bias-sum / copy launches, the loss kernels, the
 LSTM weight-gradient product, clip_grad_norm_'s per-tensor norms and torch's Adam.  Here
 (csrc/lstm_seq.hip, csrc/ppo_mlp.hip through include/ppo_mlp.h):
-    2   LSTM forward, actor and critic memories (matrix-core kernels, fp32 state)
+    1   LSTM forward, actor and critic memories side by side (matrix-core kernels, fp32
+        state, pmlp_lstm_fwd_mfma_jobs: one 2,048-env memory alone fills half the CUs)
     1   both heads forward, fp32 (pmlp_heads_forward)
     2   the PPO loss and its fp32 output gradients (pmlp_ppo_loss_step_f32)
     1   both heads backward: the LSTM output gradients and per-block weight-gradient partials
-    2   LSTM backward, each accumulating its weight gradients dG^T [x | h_prev | 1] on the
-        matrix cores into per-workgroup partials (pmlp_lstm_bwd_dw_mfma)
+    1   LSTM backward of both memories, each accumulating its weight gradients
+        dG^T [x | h_prev | 1] on the matrix cores into per-workgroup partials
+        (pmlp_lstm_bwd_dw_mfma_jobs)
     1   every partial (heads, memories) summed into the flat gradient (pmlp_reduce_slabs)
     2   grad-norm partials (+ step / adaptive LR / loss bookkeeping) and Adam
 Every parameter is a view of ONE flat fp32 buffer (each tensor starting on 16 bytes), the
@@ -188,7 +190,16 @@ class FusedRecurrentStep:
         reset = reset.contiguous()
         # 1. the memories over the T steps (zeroing the state where reset[t])
         xs, hids = (obs, cobs), (hid_a, hid_c)
-        for n in range(2):
+        both = self.mfma[0] and self.mfma[1]  # both memories in one launch each way
+        if both:
+            jobs = (lstm_seq.LstmJob * 2)()
+            for n in range(2):
+                r, (h0, c0) = self.rnns[n], (t.reshape(mb, H) for t in hids[n])
+                jobs[n] = lstm_seq.LstmJob(self.I[n], P(xs[n]), P(r.weight_ih_l0), P(r.bias_ih_l0), P(r.bias_hh_l0),
+                                           P(r.weight_hh_l0), P(h0), P(c0), P(self.h_out[n]), P(self.c_out[n]),
+                                           P(self.gact[n]), P(self.xh[n]), P(self.dh[n]), P(self.lslab[n]))
+            lstm_seq._ok(L.pmlp_lstm_fwd_mfma_jobs(2, jobs, T, mb, H, P(reset), st), "pmlp_lstm_fwd_mfma_jobs")
+        for n in range(0 if both else 2):
             r = self.rnns[n]
             h0, c0 = (t.reshape(mb, H) for t in hids[n])
             args = (T, mb, H, self.I[n], P(xs[n]), P(r.weight_ih_l0), P(r.bias_ih_l0), P(r.bias_hh_l0),
@@ -211,7 +222,9 @@ class FusedRecurrentStep:
         # 4. both heads backward: the memories' output gradients + weight-gradient partials
         mm._ok(lib.pmlp_heads_backward(2, self._head_jobs, M, H, st), "pmlp_heads_backward")
         # 5. the memories backward, with their weight gradients (slab partials) on the matrix cores
-        for n in range(2):
+        if both:
+            lstm_seq._ok(L.pmlp_lstm_bwd_dw_mfma_jobs(2, jobs, T, mb, H, P(reset), st), "pmlp_lstm_bwd_dw_mfma_jobs")
+        for n in range(0 if both else 2):
             r, I = self.rnns[n], self.I[n]
             c0 = hids[n][1].reshape(mb, H)
             if self.mfma[n]:

@@ -23,6 +23,14 @@ from . import mfma_mlp as mm
 _bound = False
 
 
+class LstmJob(C.Structure):
+    """include/ppo_mlp.h pmlp_lstm_job: one memory's sequence in a two-memory launch."""
+    _fields_ = [("I", C.c_int32), ("x", C.c_void_p), ("w_ih", C.c_void_p), ("b_ih", C.c_void_p),
+                ("b_hh", C.c_void_p), ("w_hh", C.c_void_p), ("h0", C.c_void_p), ("c0", C.c_void_p),
+                ("h_out", C.c_void_p), ("c_out", C.c_void_p), ("gact", C.c_void_p), ("xh", C.c_void_p),
+                ("dh_out", C.c_void_p), ("slab", C.c_void_p)]
+
+
 def _lib():
     global _bound
     L = mm.load()
@@ -40,6 +48,8 @@ def _lib():
         L.pmlp_lstm_bwd_dw_blocks.restype = i32
         L.pmlp_lstm_bwd_dw_mfma.argtypes = [i32, i32, i32, i32] + [vp] * 8 + [vp]
         L.pmlp_lstm_step_mfma.argtypes = [i32, i32, i32] + [vp] * 9 + [vp]
+        L.pmlp_lstm_fwd_mfma_jobs.argtypes = [i32, C.POINTER(LstmJob), i32, i32, i32, vp, vp]
+        L.pmlp_lstm_bwd_dw_mfma_jobs.argtypes = [i32, C.POINTER(LstmJob), i32, i32, i32, vp, vp]
         _bound = True
     return L
 
