@@ -130,6 +130,7 @@ struct DevState {
     const float* friction;    // [N]
     const float* added_mass;  // [N]
     const float* torques_in;  // [N,D] (lgs_simulate)
+    float* vsim;              // [N,2] the step's base xy velocity before the all-env push draw (k_step_extras)
 };
 
 __device__ __forceinline__ float rl(float x, int l) {
@@ -1741,7 +1742,8 @@ enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
 
 template <int D, int B, int ROWS, int EPW>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
-                             const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL) {
+                             const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL,
+                             float* vsim = nullptr) {
     const int lane = hl<EPW>();
     const int A = T.num_actions;
     const uint64_t seed = T.seed;
@@ -1850,7 +1852,17 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     // bookkeeping (:707-709)
     if (lane < A) E.last_actions[A * e + lane] = act[lane];
     if (lane < D) E.last_dof_vel[D * e + lane] = s.qd[lane];
-    if (lane < 6) E.last_root_vel[6 * e + lane] = s.root[7 + lane];
+    if (vsim && T.push_robots && lane < 2) {
+        // last_root_vel[:, 0:2]: the all-env push draw whenever any env is pushed this step
+        // (legged_robot.py:549-550, 709), which is nearly every step; the simulated values
+        // go to vsim, and k_step_extras puts them back on the steps where no env is pushed
+        vsim[2 * e + lane] = s.root[7 + lane];
+        E.last_root_vel[6 * e + lane] =
+            rand_range(-T.max_push_vel_xy, T.max_push_vel_xy, philox_uniform(seed, e, step, LGS_STREAM_PUSH, lane));
+    } else if (lane < 6) {
+        E.last_root_vel[6 * e + lane] = s.root[7 + lane];
+    }
+    if (vsim && lane >= 2 && lane < 6) E.last_root_vel[6 * e + lane] = s.root[7 + lane];
 }
 
 // k_step modes: the fused control step (lgs_step), or its two halves -- the physics
@@ -1916,7 +1928,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     STAMP(15);
     if (mode != MODE_PHYSICS)
         post_physics<D, B, ROWS, EPW>(s, T, E, rbs, N, e, step, RESET_STEP,
-                                      mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL));
+                                      mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL),
+                                      st.vsim);
     __syncthreads();
     STAMP(16);
     store_state<D, B, ROWS, EPW>(s, st, e);
@@ -1954,24 +1967,27 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
 // tensor into last_root_vel.  root_states here IS the simulation state, so it keeps the
 // simulated velocities of the envs not pushed; last_root_vel[:, 0:2] takes
 // the draws for every env, as in the reference (the pushed envs' draws are the ones
-// k_step applied: same Philox key).
+// k_step applied: same Philox key).  k_step itself writes every env's draw there (and its
+// simulated xy velocity to vsim): this one-workgroup kernel only restores vsim on the
+// rare steps where no env was pushed (it drew 2 Philox per env itself before: 4.6 -> 9.5 us).
 __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
-                                                      int N, int advance, uint32_t step) {
+                                                      int N, int advance, uint32_t step, const float* vsim) {
     const lgs_task_params& T = *Tp;
     const int nsum = num_sums(T);
     const float cnt = E.episode_acc[nsum];
     const bool any = cnt > 0.f;
     const int t = threadIdx.x;
     if (E.step_counter) step = (uint32_t)*E.step_counter;  // the key k_step used (read before the advance)
-    if (advance && T.push_robots && E.last_root_vel) {
-        // pushed envs: episode_length % push_interval == 0 after this step (reset ones at 0)
+    if (advance && T.push_robots && E.last_root_vel && vsim) {
+        // k_step wrote every env's draw; no env pushed (episode_length % push_interval == 0
+        // after this step, reset ones at 0): the simulated velocities go back
         int pushed = 0;
         for (int e = t; e < N && !pushed; e += blockDim.x) pushed = (E.episode_length[e] % T.push_interval) == 0;
-        if (__syncthreads_or(pushed))
-            for (int e = t; e < N; e += blockDim.x)
-                for (int j = 0; j < 2; ++j)
-                    E.last_root_vel[6 * e + j] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy,
-                                                            philox_uniform(T.seed, e, step, LGS_STREAM_PUSH, j));
+        if (!__syncthreads_or(pushed))
+            for (int e = t; e < N; e += blockDim.x) {
+                E.last_root_vel[6 * e] = vsim[2 * e];
+                E.last_root_vel[6 * e + 1] = vsim[2 * e + 1];
+            }
     }
     if (E.ep_means && t < nsum) {
         float m = E.ep_means[t];
@@ -2004,6 +2020,7 @@ struct lgs_sim {
     void* model_mem = nullptr;
     float* friction = nullptr;
     float* added_mass = nullptr;
+    float* vsim = nullptr;  // [N,2] scratch of the all-env push bookkeeping (DevState::vsim)
     float* root = nullptr;
     float* dofs = nullptr;
     float* cforce = nullptr;
@@ -2195,7 +2212,7 @@ static int dof_chain_length(const lgs_model_desc* m) {
 static DevState state_of(lgs_sim* s) {
     DevState st;
     st.root = s->root; st.dofs = s->dofs; st.cforce = s->cforce; st.rbs = s->rbs;
-    st.friction = s->friction; st.added_mass = s->added_mass; st.torques_in = s->torques;
+    st.friction = s->friction; st.added_mass = s->added_mass; st.torques_in = s->torques; st.vsim = s->vsim;
     return st;
 }
 
@@ -2289,6 +2306,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     sp.selfp = nullptr; sp.n_selfp = 0; sp.max_self = 0;
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
+    HIP_TRY(hipMalloc(&s->vsim, sizeof(float) * 2 * num_envs));
     HIP_TRY(hipMemset(s->added_mass, 0, sizeof(float) * num_envs));
     {
         float* ones = (float*)malloc(sizeof(float) * num_envs);
@@ -2306,6 +2324,7 @@ LGS_API int lgs_destroy_sim(lgs_sim* s) {
     (void)hipFree(s->model_mem);
     (void)hipFree(s->friction);
     (void)hipFree(s->added_mass);
+    (void)hipFree(s->vsim);
     (void)hipFree(s->task_dev);
     (void)hipFree(s->hf_mem);
     (void)hipFree(s->self_mem);
@@ -2490,7 +2509,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     HIP_TRY(hipGetLastError());
     if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
-                           (uint32_t)step_counter);
+                           (uint32_t)step_counter, (const float*)s->vsim);
         HIP_TRY(hipGetLastError());
     }
     return LGS_OK;
@@ -2543,7 +2562,7 @@ LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t*
     HIP_TRY(hipGetLastError());
     // extras["episode"] over the reset envs and extras["time_outs"]; no step-counter advance
     hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0,
-                       (uint32_t)step_counter);
+                       (uint32_t)step_counter, (const float*)s->vsim);
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }
