@@ -115,6 +115,28 @@ typedef struct {
     int32_t nslabs, cols_in, cols_out;
 } pmlp_reduce_job;
 PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream);
+/* pmlp_reduce_slabs plus the end of the PPO loss and, at world size 1, pmlp_opt_prepare, in
+ * ONE launch (FusedPPOStep): the loss step ran with stats = dstd = NULL (partials only); one
+ * more workgroup sums its partials into stats [surrogate, value, kl, entropy] and the std
+ * gradient dstd (bitwise what pmlp_ppo_loss_step writes).  norm_partial (optional): every
+ * workgroup writes the sum of squares of the gradient elements it produced, the std
+ * gradient's included, and the loss workgroup advances step, accumulates acc and adapts lr
+ * as pmlp_opt_prepare at scale 1; nparts (out) is the count for pmlp_adam_mirror_n.  The
+ * jobs' outputs and dstd must be the whole gradient for the norm to be clip_grad_norm_'s. */
+typedef struct pmlp_reduce_step {
+    const float* loss_partial;  /* pmlp_ppo_loss_step's partial buffer             */
+    int32_t loss_blocks;        /* pmlp_ppo_loss_step_parts(M, A) / (3 + A)         */
+    int32_t A, M;
+    float ecoef;
+    const float* stdv;
+    float *stats, *dstd;
+    float* norm_partial;        /* optional: >= nparts floats                        */
+    float *step, *lr, *acc;
+    float desired_kl;
+    int32_t adaptive;
+    int32_t nparts;             /* out                                               */
+} pmlp_reduce_step;
+PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, pmlp_reduce_step* r, void* stream);
 
 /* out[r] = sum_c x[r*ld + c], c < cols (bf16 in, fp32 sum): bias gradients. */
 typedef struct {
@@ -187,6 +209,11 @@ PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, f
                               float grad_scale, const float* partial, const float* step, const float* lr,
                               float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
                               const pmlp_mirror_job* mirror, void* stream);
+/* pmlp_adam_mirror with the norm partials' count given (pmlp_reduce_slabs_step's nparts). */
+PMLP_API int pmlp_adam_mirror_n(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                float grad_scale, const float* partial, int32_t nparts, const float* step,
+                                const float* lr, float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
+                                const pmlp_mirror_job* mirror, void* stream);
 
 /* RolloutStorage.compute_returns (rsl_rl v1.0.2): GAE(gamma, lam) over [T,N]
  * rewards/dones(bool bytes)/values with last_values[N], writing returns and
@@ -280,7 +307,8 @@ PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32
  * operands, dmu[M,Ap] + dmu_t[Ap,M] and dvalue[M,Vp] + dvalue_t[Vp,M]
  * (padding columns/rows written as zero; dmu_t / dvalue_t may be NULL), dstd[A] (incl. the entropy term) and
  * stats[4] = {surrogate_loss, value_loss, kl_mean, entropy_mean}.
- * partial: pmlp_ppo_loss_step_parts(M, A) floats of scratch.                */
+ * partial: pmlp_ppo_loss_step_parts(M, A) floats of scratch.  stats = dstd = NULL: only the
+ * per-block partials are written, and pmlp_reduce_slabs_step finishes the loss.        */
 PMLP_API int32_t pmlp_ppo_loss_step_parts(int32_t M, int32_t A);
 PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float* value, const float* actions,
                                 const float* old_logp, const float* old_mu, const float* old_sigma, const float* adv,

@@ -39,14 +39,14 @@ def test_ctypes_job_structs_match_c_layout(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "ppo_mlp.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
                    ' sizeof(pmlp_gemm_job), sizeof(pmlp_mirror_job), sizeof(pmlp_convert_job),'
-                   ' sizeof(pmlp_reduce_job)); printf("%zu %zu\\n", sizeof(pmlp_head_job), sizeof(pmlp_lstm_job));'
+                   ' sizeof(pmlp_reduce_job)); printf("%zu %zu %zu\\n", sizeof(pmlp_head_job), sizeof(pmlp_lstm_job), sizeof(pmlp_reduce_step));'
                    ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     from rsl_rl.modules import lstm_seq
     assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob),
-                   C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob)]
+                   C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob), C.sizeof(mm.ReduceStep)]
 
 
 def _job(**kw):
@@ -93,8 +93,10 @@ def test_adam_mirror_checks_its_jobs(lib):
 
 
 def test_recurrent_and_bookkeeping_entries_refuse_bad_arguments(lib):
-    """The LSTM entries and the loss bookkeeping check their arguments before any launch."""
+    """The LSTM entries, the folded reduce step and the loss bookkeeping check their
+    arguments before any launch."""
     from rsl_rl.modules import lstm_seq
+    from rsl_rl.modules import mfma_mlp as mm
     L = lstm_seq._lib()
     assert L.pmlp_lstm_step(0, 64, 16, 16, 16, 16, None, None, None) != 0  # empty batch
     assert L.pmlp_lstm_step(8, 64, 16, 8, 16, 16, None, None, None) != 0  # whh not 16-byte aligned
@@ -108,6 +110,14 @@ def test_recurrent_and_bookkeeping_entries_refuse_bad_arguments(lib):
     jobs[0].I = 44
     assert L.pmlp_lstm_bwd_dw_mfma_jobs(1, jobs, 24, 64, 64, None, None) != 0  # null buffers
     assert b"pmlp_lstm_bwd_dw_mfma_jobs" in L.pmlp_lstm_last_error()
+    job = (mm.ReduceJob * 1)(mm.ReduceJob(16, 16, None, 64, 64, 2, 0, 0))
+    rs = mm.ReduceStep()
+    assert lib.pmlp_reduce_slabs_step(1, job, C.byref(rs), None) != 0  # no loss partials
+    assert b"pmlp_reduce_slabs_step" in lib.pmlp_last_error()
+    rs.loss_partial, rs.loss_blocks, rs.A, rs.M, rs.stdv, rs.stats, rs.dstd, rs.norm_partial = 16, 4, 12, 256, 16, 16, 16, 16
+    assert lib.pmlp_reduce_slabs_step(1, job, C.byref(rs), None) != 0  # norm partials without step / lr
+    assert b"step and lr" in lib.pmlp_last_error()
+    assert lib.pmlp_adam_mirror_n(16, 16, 16, 16, 16, 1.0, 16, 0, 16, 16, 1.0, 0.9, 0.999, 1e-8, 0, None, None) != 0
     lib.pmlp_loss_bookkeeping.restype = C.c_int
     assert lib.pmlp_loss_bookkeeping(None, None, None, C.c_float(0.01), 1, None) != 0
     assert b"pmlp_loss_bookkeeping" in lib.pmlp_last_error()

@@ -714,14 +714,103 @@ struct RedJobs {
 // A job with many slabs (the small layers' weight gradients: 64-96 slabs) splits them over
 // G = J.groups threads per element quad (slabs g, g+G, ...), summed through LDS in group
 // order: its serial chain of dependent adds is G times shorter.
-__global__ __launch_bounds__(256) void k_reduce_jobs(RedJobs jobs) {
+// RedStep (pmlp_reduce_slabs_step): one more workgroup finishes the PPO loss (the
+// per-block partials of k_ppo_loss_step*: stats and the std gradient, what
+// k_ppo_loss_step_final computed, same summation order), and with norm set every
+// workgroup writes the sum of squares of the gradient elements it produced (the last one:
+// of the std gradient) and the loss one does k_opt_prepare's step / loss / LR bookkeeping
+// -- one launch instead of three (world size 1: nothing is all-reduced in between).
+struct RedStep {
+    const float* lpartial;  // null: no loss finish (plain pmlp_reduce_slabs)
+    int lblocks, A, M;
+    float ecoef;
+    const float* stdv;
+    float* stats;
+    float* dstd;
+    float* norm;  // null: no norm partials / bookkeeping
+    float* step;
+    float* lr;
+    float* acc;
+    float desired_kl;
+    int adaptive;
+};
+
+__device__ __forceinline__ float red_block_sum(float v, float* sh) {  // 256 threads
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__device__ void reduce_step_finish(const RedStep& r) {
+    __shared__ float q_out[64];
+    __shared__ float sh[4];
+    const int W = 3 + r.A, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // one wave per quantity q (q = w, w + 4, ...): k_ppo_loss_step_final's order exactly
+    for (int q = w; q < W; q += 4) {
+        float x = 0.f;
+#pragma unroll 8
+        for (int b = lane; b < r.lblocks; b += 64) x += r.lpartial[(size_t)b * W + q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        if (lane == 0) q_out[q] = x;
+    }
+    __syncthreads();
+    float sq = 0.f;
+    if (threadIdx.x < W) {
+        const int q = threadIdx.x;
+        const float x = q_out[q];
+        if (q < 3) {
+            r.stats[q] = x * (1.f / (float)r.M);
+        } else {
+            const float d = x - r.ecoef / r.stdv[q - 3];
+            r.dstd[q - 3] = d;
+            sq = d * d;
+        }
+    }
+    if (threadIdx.x == 0) {
+        float ent = 0.f;
+        for (int k = 0; k < r.A; ++k) ent += 0.5f + 0.91893853320467274f + logf(r.stdv[k]);  // log(sqrt(2 pi))
+        r.stats[3] = ent;
+    }
+    if (!r.norm) return;  // (block-uniform)
+    sq = red_block_sum(sq, sh);
+    if (threadIdx.x == 0) {
+        r.norm[blockIdx.x] = sq;
+        // k_opt_prepare's block-0 bookkeeping at scale 1 (the stats of this launch)
+        r.step[0] += 1.f;
+        const float s0 = q_out[0] * (1.f / (float)r.M), s1 = q_out[1] * (1.f / (float)r.M);
+        if (r.acc) {
+            r.acc[0] += s1;
+            r.acc[1] += s0;
+        }
+        if (r.adaptive) {
+            const float kl = q_out[2] * (1.f / (float)r.M);
+            float l = r.lr[0];
+            if (kl > r.desired_kl * 2.f) l = fmaxf(l / 1.5f, 1e-5f);
+            else if (kl < r.desired_kl / 2.f && kl > 0.f) l = fminf(l * 1.5f, 1e-2f);
+            r.lr[0] = l;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_reduce_jobs(RedJobs jobs, RedStep rs) {
     __shared__ float4 red[256];
+    __shared__ float sh[4];
+    // the loss workgroup is the first one (dispatched first: its serial sums overlap the rest)
+    if (rs.lpartial && blockIdx.x == 0) {
+        reduce_step_finish(rs);
+        return;
+    }
+    const int bx = (int)blockIdx.x - (rs.lpartial ? 1 : 0);
     int jb = 0;
-    while (jb + 1 < jobs.njobs && (int)blockIdx.x >= jobs.start[jb + 1]) ++jb;
+    while (jb + 1 < jobs.njobs && bx >= jobs.start[jb + 1]) ++jb;
     const RedJob J = jobs.j[jb];
     const int G = J.groups, EQ = 256 / G;  // block-uniform
     const int sg = threadIdx.x / EQ, eq = threadIdx.x % EQ;
-    const int64_t i0 = 4 * ((int64_t)(blockIdx.x - jobs.start[jb]) * EQ + eq);
+    const int64_t i0 = 4 * ((int64_t)(bx - jobs.start[jb]) * EQ + eq);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     if (i0 < J.n) {
         if (i0 + 4 <= J.n && (J.stride % 4) == 0 && ((uintptr_t)J.slab & 15) == 0) {
@@ -740,30 +829,37 @@ __global__ __launch_bounds__(256) void k_reduce_jobs(RedJobs jobs) {
     if (G > 1) {
         red[threadIdx.x] = make_float4(s[0], s[1], s[2], s[3]);
         __syncthreads();
-        if (sg != 0) return;
-        for (int g = 1; g < G; ++g) {
-            const float4 v = red[g * EQ + eq];
-            s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-        }
-    }
-    if (i0 >= J.n) return;
-    for (int e = 0; e < 4 && i0 + e < J.n; ++e) {
-        const int64_t i = i0 + e;
-        int64_t o = i;
-        float* dst = J.out;
-        if (J.bias_out) {
-            const int64_t row = i / J.cols_in, col = i % J.cols_in;
-            if (col < J.cols_out) {
-                o = row * J.cols_out + col;
-            } else if (col == J.cols_out) {
-                dst = J.bias_out;
-                o = row;
-            } else {
-                continue;
+        if (sg != 0 && !rs.norm) return;
+        if (sg == 0)
+            for (int g = 1; g < G; ++g) {
+                const float4 v = red[g * EQ + eq];
+                s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
             }
-        }
-        dst[o] = s[e];
     }
+    float sq = 0.f;
+    if (i0 < J.n && sg == 0) {
+        for (int e = 0; e < 4 && i0 + e < J.n; ++e) {
+            const int64_t i = i0 + e;
+            int64_t o = i;
+            float* dst = J.out;
+            if (J.bias_out) {
+                const int64_t row = i / J.cols_in, col = i % J.cols_in;
+                if (col < J.cols_out) {
+                    o = row * J.cols_out + col;
+                } else if (col == J.cols_out) {
+                    dst = J.bias_out;
+                    o = row;
+                } else {
+                    continue;
+                }
+            }
+            dst[o] = s[e];
+            sq = fmaf(s[e], s[e], sq);
+        }
+    }
+    if (!rs.norm) return;  // (block-uniform)
+    sq = red_block_sum(sq, sh);
+    if (threadIdx.x == 0) rs.norm[blockIdx.x] = sq;
 }
 
 struct SumJob {
@@ -2128,10 +2224,10 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
     return 0;
 }
 
-PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream) {
+static int reduce_pack(int32_t njobs, const pmlp_reduce_job* jobs, RedJobs& rj, int64_t& nb) {
     if (njobs <= 0 || njobs > PMLP_MAX_JOBS || !jobs) return fail(-1, "pmlp_reduce_slabs: 1..PMLP_MAX_JOBS jobs");
-    RedJobs rj{};
-    int64_t nb = 0;
+    rj = RedJobs{};
+    nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_reduce_job& J = jobs[i];
         if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n ||
@@ -2154,8 +2250,33 @@ PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void*
     }
     rj.start[njobs] = (int)nb;
     rj.njobs = njobs;
-    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, rj);
+    return 0;
+}
+
+PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void* stream) {
+    RedJobs rj;
+    int64_t nb;
+    if (int e = reduce_pack(njobs, jobs, rj, nb)) return e;
+    const RedStep none{};
+    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, rj, none);
     PMLP_CHECK_LAUNCH("pmlp_reduce_slabs");
+    return 0;
+}
+
+PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, pmlp_reduce_step* r, void* stream) {
+    RedJobs rj;
+    int64_t nb;
+    if (int e = reduce_pack(njobs, jobs, rj, nb)) return e;
+    if (!r || !r->loss_partial || r->loss_blocks <= 0 || r->A <= 0 || r->A > 61 || r->M <= 0 || !r->stdv ||
+        !r->stats || !r->dstd)
+        return fail(-1, "pmlp_reduce_slabs_step: loss partials / stats / dstd / 0 < A <= 61");
+    if (r->norm_partial && (!r->step || !r->lr))
+        return fail(-1, "pmlp_reduce_slabs_step: norm_partial needs step and lr");
+    const RedStep rs{r->loss_partial, r->loss_blocks, r->A, r->M, r->ecoef, r->stdv, r->stats, r->dstd,
+                     r->norm_partial, r->step, r->lr, r->acc, r->desired_kl, r->adaptive};
+    r->nparts = (int32_t)(nb + 1);  // + the loss-finishing workgroup
+    hipLaunchKernelGGL(k_reduce_jobs, dim3((unsigned)(nb + 1)), dim3(256), 0, (hipStream_t)stream, rj, rs);
+    PMLP_CHECK_LAUNCH("pmlp_reduce_slabs_step");
     return 0;
 }
 
@@ -2262,12 +2383,12 @@ PMLP_API int pmlp_adam(float* param, const float* grad, float* exp_avg, float* e
     return 0;
 }
 
-PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                              float grad_scale, const float* partial, const float* step, const float* lr,
-                              float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
-                              const pmlp_mirror_job* mirror, void* stream) {
-    if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !partial || !step || !lr)
-        return fail(-1, "pmlp_adam_mirror: null buffer or empty parameter set");
+PMLP_API int pmlp_adam_mirror_n(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                float grad_scale, const float* partial, int32_t nparts, const float* step,
+                                const float* lr, float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
+                                const pmlp_mirror_job* mirror, void* stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !partial || nparts <= 0 || !step || !lr)
+        return fail(-1, "pmlp_adam_mirror: null buffer, empty parameter set or no norm partials");
     if (nmirror < 0 || nmirror > PMLP_MAX_MIRROR || (nmirror && !mirror))
         return fail(-1, "pmlp_adam_mirror: 0..PMLP_MAX_MIRROR mirror jobs");
     MirrorJobs mj{};
@@ -2289,9 +2410,17 @@ PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, f
     }();
     const int blocks = (int)std::min<int64_t>(cap, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
     hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
-                       exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr, max_norm, beta1, beta2, eps, mj);
+                       exp_avg_sq, n, grad_scale, partial, nparts, step, lr, max_norm, beta1, beta2, eps, mj);
     PMLP_CHECK_LAUNCH("pmlp_adam_mirror");
     return 0;
+}
+
+PMLP_API int pmlp_adam_mirror(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                              float grad_scale, const float* partial, const float* step, const float* lr,
+                              float max_norm, float beta1, float beta2, float eps, int32_t nmirror,
+                              const pmlp_mirror_job* mirror, void* stream) {
+    return pmlp_adam_mirror_n(param, grad, exp_avg, exp_avg_sq, n, grad_scale, partial, PMLP_OPT_PARTS, step, lr,
+                              max_norm, beta1, beta2, eps, nmirror, mirror, stream);
 }
 
 PMLP_API int32_t pmlp_gae_parts(int32_t num_envs) { return (num_envs + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS; }
@@ -2437,8 +2566,9 @@ static int loss_step_launch(const LossArgs& a, const LossStepOut& o, int M, int 
         hipLaunchKernelGGL(k_ppo_loss_step_reg<16>, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
     else
         hipLaunchKernelGGL(k_ppo_loss_step, dim3(nb), dim3(64), 0, (hipStream_t)stream, a, o);
-    hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(3 + A), dim3(64), 0, (hipStream_t)stream, a, partial, nb, stats,
-                       dstd);
+    if (stats)  // (stats = dstd = NULL: pmlp_reduce_slabs_step finishes the loss)
+        hipLaunchKernelGGL(k_ppo_loss_step_final, dim3(3 + A), dim3(64), 0, (hipStream_t)stream, a, partial, nb,
+                           stats, dstd);
     PMLP_CHECK_LAUNCH("pmlp_ppo_loss_step");
     return 0;
 }
@@ -2453,7 +2583,7 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
     if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
                           clipped_value, vcoef, ecoef))
         return e;
-    if (!partial || !stats || !dstd || !dmu || !dvalue || Ap < A || Vp < 1)
+    if (!partial || (!stats != !dstd) || !dmu || !dvalue || Ap < A || Vp < 1)
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp, nullptr, nullptr};
     return loss_step_launch(a, o, M, A, Ap, partial, stats, dstd, stream);

@@ -164,6 +164,14 @@ class FusedPPOStep:
             self.dw_stage.append([None if kps[n] == self.lins[n][l].in_features else
                                   torch.empty(self.lins[n][l].out_features, kps[n], device=dev) for n in range(2)])
         self.opt_partial = torch.empty(mm.load().pmlp_opt_parts(), device=dev)
+        # the loss end (and, at world size 1, the optimizer's norm partials and bookkeeping)
+        # inside the slab-reduce launch (pmlp_reduce_slabs_step): two launches fewer per step.
+        # The reduce jobs plus the std gradient must then be the whole gradient.
+        covered = sum(lin.out_features * (lin.in_features + 1) for ls in self.lins for lin in ls) + A
+        self.fold_loss = 2 * L <= mm.MAX_JOBS and os.environ.get("PMLP_FOLD_OPT", "1") != "0"
+        self.fold_opt = self.fold_loss and covered == self.n and all(d is None for ds in self.dw_stage for d in ds)
+        self.norm_partial = torch.empty(16384, device=dev) if self.fold_opt else None
+        self.nparts = 0
 
     @staticmethod
     def _ones_row(t, k):
@@ -263,8 +271,10 @@ class FusedPPOStep:
         mm._ok(lib.pmlp_ppo_loss_step(P(self.out[0]), P(std), P(self.out[1]), P(actions), P(logp), P(mu_old),
                                       P(sigma_old), P(adv), P(ret), P(values), P(rows), M, A, float(alg.clip_param),
                                       int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
-                                      float(alg.entropy_coef), P(self.loss_partial), P(self.stats),
-                                      P(self._gview[id(ac.std)]), P(self.dz_out[0]), mm._p(self.dzt_out[0]),
+                                      float(alg.entropy_coef), P(self.loss_partial),
+                                      None if self.fold_loss else P(self.stats),
+                                      None if self.fold_loss else P(self._gview[id(ac.std)]),
+                                      P(self.dz_out[0]), mm._p(self.dzt_out[0]),
                                       self.dz_out[0].shape[1], P(self.dz_out[1]), mm._p(self.dzt_out[1]),
                                       self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
@@ -300,7 +310,19 @@ class FusedPPOStep:
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
                 dzt = [self.dzt[n][l] for n in range(2)]
-        mm._reduce(red)
+        adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
+        dkl = float(alg.desired_kl if alg.desired_kl is not None else 0.0)
+        fold_opt = self.fold_opt and alg.world_size == 1
+        if self.fold_loss:
+            rs = mm.ReduceStep(P(self.loss_partial), self.loss_partial.numel() // (3 + A), A, M,
+                               float(alg.entropy_coef), P(std), P(self.stats), P(self._gview[id(ac.std)]),
+                               P(self.norm_partial) if fold_opt else None, P(self.step_t), P(alg._lr), P(acc), dkl,
+                               adaptive, 0)
+            self.nparts = mm._reduce_step(red, rs)
+            if fold_opt and self.nparts > self.norm_partial.numel():
+                raise RuntimeError(f"fused PPO step: {self.nparts} norm partials > {self.norm_partial.numel()}")
+        else:
+            mm._reduce(red)
         for dst, srcv in copies:
             dst.copy_(srcv)
         # 5. data-parallel: one bucket (gradient + loss statistics)
@@ -312,17 +334,17 @@ class FusedPPOStep:
         grp = alg.optimizer.param_groups[0]
         b1, b2 = grp.get("betas", (0.9, 0.999))
         eps = grp.get("eps", 1e-8)
-        adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
-        mm._ok(lib.pmlp_opt_prepare(mm._p(self.grad), self.n, scale, mm._p(self.opt_partial), mm._p(self.step_t),
-                                    mm._p(self.stats), mm._p(alg._lr), mm._p(acc),
-                                    float(alg.desired_kl if alg.desired_kl is not None else 0.0), adaptive, st),
-               "pmlp_opt_prepare")
+        if not fold_opt:
+            mm._ok(lib.pmlp_opt_prepare(mm._p(self.grad), self.n, scale, mm._p(self.opt_partial), mm._p(self.step_t),
+                                        mm._p(self.stats), mm._p(alg._lr), mm._p(acc), dkl, adaptive, st),
+                   "pmlp_opt_prepare")
         max_norm = float(alg.max_grad_norm) if alg.max_grad_norm is not None else 0.0
         # Adam, and the bf16 weight copies of the next forward written on the way
-        mm._ok(lib.pmlp_adam_mirror(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg), mm._p(self.exp_avg_sq),
-                                    self.n, scale, mm._p(self.opt_partial), mm._p(self.step_t), mm._p(alg._lr),
-                                    max_norm, float(b1), float(b2), float(eps), len(self.mirror), self.mirror, st),
-               "pmlp_adam_mirror")
+        part, nparts = (self.norm_partial, self.nparts) if fold_opt else (self.opt_partial, self.opt_partial.numel())
+        mm._ok(lib.pmlp_adam_mirror_n(mm._p(self.flat), mm._p(self.grad), mm._p(self.exp_avg),
+                                      mm._p(self.exp_avg_sq), self.n, scale, mm._p(part), nparts, mm._p(self.step_t),
+                                      mm._p(alg._lr), max_norm, float(b1), float(b2), float(eps), len(self.mirror),
+                                      self.mirror, st), "pmlp_adam_mirror_n")
 
 
 class FusedRollout:

@@ -55,6 +55,14 @@ class ReduceJob(C.Structure):
                 ("n", C.c_int64), ("nslabs", C.c_int32), ("cols_in", C.c_int32), ("cols_out", C.c_int32)]
 
 
+class ReduceStep(C.Structure):
+    """include/ppo_mlp.h pmlp_reduce_step (pmlp_reduce_slabs_step)."""
+    _fields_ = [("loss_partial", C.c_void_p), ("loss_blocks", C.c_int32), ("A", C.c_int32), ("M", C.c_int32),
+                ("ecoef", C.c_float), ("stdv", C.c_void_p), ("stats", C.c_void_p), ("dstd", C.c_void_p),
+                ("norm_partial", C.c_void_p), ("step", C.c_void_p), ("lr", C.c_void_p), ("acc", C.c_void_p),
+                ("desired_kl", C.c_float), ("adaptive", C.c_int32), ("nparts", C.c_int32)]
+
+
 class RowsumJob(C.Structure):
     _fields_ = [("x", C.c_void_p), ("out", C.c_void_p), ("rows", C.c_int32), ("cols", C.c_int32),
                 ("ld", C.c_int32)]
@@ -89,6 +97,7 @@ def load():
         L.pmlp_convert.argtypes = [i32, C.POINTER(ConvertJob), vp]
         L.pmlp_gemm.argtypes = [i32, i32, C.POINTER(GemmJob), i32, vp]
         L.pmlp_reduce_slabs.argtypes = [i32, C.POINTER(ReduceJob), vp]
+        L.pmlp_reduce_slabs_step.argtypes = [i32, C.POINTER(ReduceJob), C.POINTER(ReduceStep), vp]
         L.pmlp_rowsum.argtypes = [i32, C.POINTER(RowsumJob), vp]
         f32 = C.c_float
         L.pmlp_ppo_loss_blocks.argtypes = [i32]
@@ -102,6 +111,8 @@ def load():
         L.pmlp_adam.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, vp]
         L.pmlp_adam_mirror.argtypes = [vp, vp, vp, vp, i64, f32, vp, vp, vp, f32, f32, f32, f32, i32,
                                        C.POINTER(MirrorJob), vp]
+        L.pmlp_adam_mirror_n.argtypes = [vp, vp, vp, vp, i64, f32, vp, i32, vp, vp, f32, f32, f32, f32, i32,
+                                         C.POINTER(MirrorJob), vp]
         L.pmlp_gae_parts.argtypes = [i32]
         L.pmlp_gae_parts.restype = i32
         L.pmlp_gae.argtypes = [vp] * 6 + [i32, i32, f32, f32, vp, vp]
@@ -229,12 +240,23 @@ def _gemm(epi, jobs, ksplit=0):
     _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
 
 
+def _reduce_job(j):
+    sl, out, n, ns = j[:4]
+    bias, ci, co = j[4:7] if len(j) > 4 else (None, 0, 0)
+    return ReduceJob(_p(sl), _p(out), _p(bias), n, n, ns, ci, co)
+
+
+def _reduce_step(jobs, rs):
+    """pmlp_reduce_slabs_step: the slab jobs (as _reduce, at most MAX_JOBS) + the loss end
+    (+ the optimizer preparation when rs.norm_partial is set); returns rs.nparts."""
+    arr = (ReduceJob * len(jobs))(*[_reduce_job(j) for j in jobs])
+    _ok(load().pmlp_reduce_slabs_step(len(jobs), arr, C.byref(rs), _stream()), "pmlp_reduce_slabs_step")
+    return rs.nparts
+
+
 def _reduce(jobs):
     """jobs: (slab, out, n, nslabs[, bias_out, cols_in, cols_out])"""
-    def mk(j):
-        sl, out, n, ns = j[:4]
-        bias, ci, co = j[4:7] if len(j) > 4 else (None, 0, 0)
-        return ReduceJob(_p(sl), _p(out), _p(bias), n, n, ns, ci, co)
+    mk = _reduce_job
     for i in range(0, len(jobs), MAX_JOBS):
         chunk = jobs[i:i + MAX_JOBS]
         arr = (ReduceJob * len(chunk))(*[mk(j) for j in chunk])
