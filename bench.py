@@ -94,8 +94,8 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-# the committed rocprofv3 summaries of the current build (tools/gpu_round2_profile.sh)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "round2", "go2_4096")
+# the committed rocprofv3 summaries of the current build (tools/gpu_round3_profile.sh)
+PROFILE_DIR = os.path.join(ROOT, "profiles", "round3", "env_go2_4096")
 
 
 def load_pmc():
