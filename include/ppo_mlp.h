@@ -397,10 +397,15 @@ typedef struct pmlp_lstm_job {
     float *h_out, *c_out, *gact, *xh;            /* forward outputs (backward inputs)     */
     const float* dh_out;                         /* backward: gradient of h_out [T,B,64]  */
     float* slab;                                 /* backward: weight-gradient partials    */
+    float *h_save, *c_save;                      /* step: the state the step starts from  */
 } pmlp_lstm_job;
 PMLP_API int pmlp_lstm_fwd_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
                                      const uint8_t* reset, void* stream);
 PMLP_API int pmlp_lstm_bwd_dw_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t T, int32_t B, int32_t H,
                                         const uint8_t* reset, void* stream);
+/* The rollout's memory step of both memories in one launch: per job pmlp_lstm_step_mfma with
+ * h = h_out, c = c_out (the state [B,64], updated in place), h_save / c_save optional (both
+ * or neither); x, w_ih, b_ih, b_hh, w_hh as above; the other fields are ignored.          */
+PMLP_API int pmlp_lstm_step_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t B, int32_t H, void* stream);
 
 #endif

@@ -1321,3 +1321,20 @@ PMLP_API int pmlp_lstm_bwd_dw_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_bwd_dw_mfma_jobs: ") + hipGetErrorString(e));
 }
+
+PMLP_API int pmlp_lstm_step_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, int32_t B, int32_t H, void* stream) {
+    if (njobs < 1 || njobs > 2 || !jobs || B <= 0) return fail("pmlp_lstm_step_mfma_jobs: 1..2 jobs, B > 0");
+    if (H != MH) return fail("pmlp_lstm_step_mfma_jobs: hidden 64");
+    MFwdBatch a{};
+    for (int i = 0; i < njobs; ++i) {
+        const pmlp_lstm_job& J = jobs[i];
+        if (J.I <= 0 || J.I > MKX || !J.x || !J.w_ih || !J.b_ih || !J.b_hh || !J.w_hh || !J.h_out || !J.c_out ||
+            (J.h_save == nullptr) != (J.c_save == nullptr))
+            return fail("pmlp_lstm_step_mfma_jobs: input 1..64, null input / state, h_save and c_save together");
+        a.m[i] = MFwdArgs{1, B, J.I, J.x, J.w_ih, J.b_ih, J.b_hh, J.w_hh, J.h_out, J.c_out, nullptr,
+                          J.h_out, J.c_out, nullptr, nullptr, J.h_save, J.c_save};
+    }
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma_jobs: ") + hipGetErrorString(e));
+}

@@ -463,14 +463,19 @@ class RecurrentRollout:
             self.y0 = [torch.empty(self.N, s[0].out_features, device=dev) for s in self.heads]
             self.out = [torch.empty(self.N, s[2].out_features, device=dev) for s in self.heads]
 
-    def _mstep(self, mem, x, save):
-        """Memory.step_ on pmlp_lstm_step_mfma (state buffers created as step_ creates them)."""
+    def _mstate(self, mem, x):
+        """The memory's static state buffers (created as Memory.step_ creates them)."""
         B, H = x.shape[0], mem.rnn.hidden_size
         hs = mem.hidden_states
         if hs is None or not isinstance(hs, tuple) or hs[0].shape != (1, B, H) or hs[0].device != x.device:
             with torch.inference_mode(False):
                 mem.hidden_states = (torch.zeros(1, B, H, device=x.device), torch.zeros(1, B, H, device=x.device))
-        return lstm_seq.lstm_step_mfma_(mem.rnn, x, mem.hidden_states[0], mem.hidden_states[1], save=save)
+        return mem.hidden_states
+
+    def _mstep_pair(self, ma, obs, sa, mc, cobs, sc):
+        """Both memories' Memory.step_ on ONE pmlp_lstm_step_mfma_jobs launch."""
+        (ha, ca), (hc, cc) = self._mstate(ma, obs), self._mstate(mc, cobs)
+        return lstm_seq.lstm_step_mfma_pair_([(ma.rnn, obs, ha, ca, sa), (mc.rnn, cobs, hc, cc, sc)])
 
     def usable(self, obs, cobs, storage):
         ok = lambda t: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
@@ -489,9 +494,8 @@ class RecurrentRollout:
             # the state BEFORE this step goes to the storage slot from inside the step kernel
             shape = (1, self.N, H)
             sa, sc = storage.hidden_state_slots(t, [shape, shape], [(1, self.N, mc.rnn.hidden_size)] * 2)
-            if self.mfma_step:  # the update's matrix-core arithmetic, one launch per memory
-                ha = self._mstep(ma, obs, (sa[0], sa[1]))
-                hc = self._mstep(mc, cobs, (sc[0], sc[1]))
+            if self.mfma_step:  # the update's matrix-core arithmetic, both memories in one launch
+                ha, hc = self._mstep_pair(ma, obs, (sa[0], sa[1]), mc, cobs, (sc[0], sc[1]))
             else:
                 ha = ma.step_(obs, save=(sa[0], sa[1]))
                 hc = mc.step_(cobs, save=(sc[0], sc[1]))

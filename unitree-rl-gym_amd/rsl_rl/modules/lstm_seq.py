@@ -28,7 +28,7 @@ class LstmJob(C.Structure):
     _fields_ = [("I", C.c_int32), ("x", C.c_void_p), ("w_ih", C.c_void_p), ("b_ih", C.c_void_p),
                 ("b_hh", C.c_void_p), ("w_hh", C.c_void_p), ("h0", C.c_void_p), ("c0", C.c_void_p),
                 ("h_out", C.c_void_p), ("c_out", C.c_void_p), ("gact", C.c_void_p), ("xh", C.c_void_p),
-                ("dh_out", C.c_void_p), ("slab", C.c_void_p)]
+                ("dh_out", C.c_void_p), ("slab", C.c_void_p), ("h_save", C.c_void_p), ("c_save", C.c_void_p)]
 
 
 def _lib():
@@ -50,6 +50,7 @@ def _lib():
         L.pmlp_lstm_step_mfma.argtypes = [i32, i32, i32] + [vp] * 9 + [vp]
         L.pmlp_lstm_fwd_mfma_jobs.argtypes = [i32, C.POINTER(LstmJob), i32, i32, i32, vp, vp]
         L.pmlp_lstm_bwd_dw_mfma_jobs.argtypes = [i32, C.POINTER(LstmJob), i32, i32, i32, vp, vp]
+        L.pmlp_lstm_step_mfma_jobs.argtypes = [i32, C.POINTER(LstmJob), i32, i32, vp]
         _bound = True
     return L
 
@@ -207,6 +208,23 @@ def lstm_step_(rnn, x, h, c, save=None):
         _ok(_lib().pmlp_lstm_step(B, H, p(gx), p(rnn.weight_hh_l0.detach().contiguous()), p(h), p(c), p(hs), p(cs),
                                   mm._stream()), "pmlp_lstm_step")
     return h
+
+
+def lstm_step_mfma_pair_(steps):
+    """Both memories' rollout step in ONE launch (pmlp_lstm_step_mfma_jobs: the kernel of
+    lstm_step_mfma_ per job, side by side in the grid).  steps: [(rnn, x, h, c, save)] x 2,
+    same batch size.  Returns the h buffers."""
+    p = mm._p
+    B = steps[0][1].shape[0]
+    jobs = (LstmJob * len(steps))()
+    for n, (rnn, x, h, c, save) in enumerate(steps):
+        hs, cs = (None, None) if save is None else save
+        jobs[n] = LstmJob(x.shape[1], p(x), p(rnn.weight_ih_l0), p(rnn.bias_ih_l0), p(rnn.bias_hh_l0),
+                          p(rnn.weight_hh_l0), None, None, p(h), p(c), None, None, None, None, p(hs), p(cs))
+    with torch.no_grad():
+        _ok(_lib().pmlp_lstm_step_mfma_jobs(len(steps), jobs, B, steps[0][0].hidden_size, mm._stream()),
+            "pmlp_lstm_step_mfma_jobs")
+    return [st[2] for st in steps]
 
 
 def lstm_step_mfma_(rnn, x, h, c, save=None):
