@@ -250,6 +250,10 @@ PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, co
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream);
+/* The update's mini-batch permutation (RolloutStorage.mini_batch_generator's
+ * torch.randperm(num_mini_batches * mini_batch_size)): out[i], i < n, a keyed pseudo-random
+ * permutation of [0, n) (4-round Feistel, Philox round function, cycle walking), no sort. */
+PMLP_API int pmlp_permutation(int64_t* out, int64_t n, uint64_t seed, void* stream);
 
 /* The whole forward of 4-layer Linear/ELU MLPs (rsl_rl's actor and critic) in ONE launch
  * (PPO.act's policy inference, the update's forward): per job

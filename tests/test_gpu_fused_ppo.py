@@ -545,3 +545,23 @@ def test_adam_mirror_writes_the_fragment_packed_weights():
             wb, wf = f.wb[n][l], f.wf[n][l]
             assert torch.equal(wb[:lin.out_features, :lin.in_features], lin.weight.detach().to(torch.bfloat16))
             assert torch.equal(wf, mfma_mlp.frag_pack(wb, wf.numel() // wb.shape[1]))
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 98304, 100003])
+def test_minibatch_permutation_kernel_is_a_permutation(n):
+    """pmlp_permutation (the fused update's mini-batch permutation in place of
+    torch.randperm): every index of [0, n) exactly once, the same permutation for the same
+    torch seed, a different one for the next draw, and no visible order left (the mean
+    displacement of a uniform permutation is n/3)."""
+    out = torch.empty(n, dtype=torch.int64, device="cuda")
+    torch.manual_seed(5)
+    a = mfma_mlp.permutation_(out).clone()
+    b = mfma_mlp.permutation_(out).clone()
+    torch.manual_seed(5)
+    c = mfma_mlp.permutation_(out).clone()
+    assert torch.equal(torch.sort(a).values, torch.arange(n, device="cuda"))
+    assert torch.equal(a, c)
+    if n >= 4096:
+        assert not torch.equal(a, b)
+        disp = (a - torch.arange(n, device="cuda")).abs().double().mean().item()
+        assert abs(disp - n / 3) < 0.02 * n

@@ -23,6 +23,7 @@ from rsl_rl.algorithms import fused_recurrent, fused_step
 from rsl_rl.modules import ActorCritic
 from rsl_rl.modules import mfma_mlp
 from rsl_rl.storage import RolloutStorage
+from rsl_rl.storage.rollout_storage import minibatch_permutation
 
 
 def _dist_world():
@@ -433,7 +434,7 @@ class PPO:
         if st.advantages.data_ptr() != self._fadv.data_ptr():
             self._fadv.copy_(st.advantages)
             st.advantages = self._fadv
-        self._fperm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
+        mfma_mlp.permutation_(self._fperm)  # as minibatch_permutation (no device sort)
 
         def body():
             self._facc.zero_()
@@ -526,7 +527,7 @@ class PPO:
         mb = batch // self.num_mini_batches
         if self._graph is None:
             self._perm = None if self._dense_recurrent else \
-                torch.randperm(self.num_mini_batches * mb, device=self.device)
+                minibatch_permutation(self.num_mini_batches * mb, self.device)
             self._acc = torch.zeros(2, device=self.device)
             flat = [st.observations.flatten(0, 1),
                     st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None
@@ -581,6 +582,6 @@ class PPO:
             self._adv_static.copy_(st.advantages)
             st.advantages = self._adv_static
         if not self._dense_recurrent:  # one randperm per update (mini_batch_generator's rule)
-            self._perm.copy_(torch.randperm(self.num_mini_batches * mb, device=self.device))
+            self._perm.copy_(minibatch_permutation(self.num_mini_batches * mb, self.device))
         self._graph.replay()
         return self._acc

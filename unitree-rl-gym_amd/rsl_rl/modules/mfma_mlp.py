@@ -98,6 +98,7 @@ def load():
         L.pmlp_gemm.argtypes = [i32, i32, C.POINTER(GemmJob), i32, vp]
         L.pmlp_reduce_slabs.argtypes = [i32, C.POINTER(ReduceJob), vp]
         L.pmlp_reduce_slabs_step.argtypes = [i32, C.POINTER(ReduceJob), C.POINTER(ReduceStep), vp]
+        L.pmlp_permutation.argtypes = [vp, C.c_int64, C.c_uint64, vp]
         L.pmlp_rowsum.argtypes = [i32, C.POINTER(RowsumJob), vp]
         f32 = C.c_float
         L.pmlp_ppo_loss_blocks.argtypes = [i32]
@@ -238,6 +239,15 @@ def _gemm(epi, jobs, ksplit=0):
                        int(bool(g("b_kn"))), int(g("sum_col") or 0))
     arr = (GemmJob * len(jobs))(*[mk(j) for j in jobs])
     _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
+
+
+def permutation_(out):
+    """out (int64 [n], device) = a random permutation of [0, n) (pmlp_permutation: the
+    mini-batch permutation without torch.randperm's device sort); the key comes from
+    torch's seeded CPU generator."""
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    _ok(load().pmlp_permutation(_p(out), out.numel(), seed, _stream()), "pmlp_permutation")
+    return out
 
 
 def _reduce_job(j):

@@ -3,6 +3,17 @@ import torch
 from rsl_rl.utils import split_and_pad_trajectories
 
 
+def minibatch_permutation(n, device):
+    """The mini-batch permutation (rsl_rl v1.0.2: torch.randperm(n, device=device)).  On the
+    GPU it is pmlp_permutation's keyed Feistel permutation (no device sort: ~3 instead of
+    ~60 us per update), keyed from torch's seeded CPU generator, so the generic and the
+    fused update draw the same permutation for the same seed; on the CPU torch.randperm."""
+    if torch.device(device).type != "cuda":
+        return torch.randperm(n, requires_grad=False, device=device)
+    from rsl_rl.modules import mfma_mlp
+    return mfma_mlp.permutation_(torch.empty(n, dtype=torch.int64, device=device))
+
+
 class RolloutStorage:
     """[T, N, ...] rollout buffers + GAE + mini-batch generators (rsl_rl v1.0.2)."""
 
@@ -124,7 +135,7 @@ class RolloutStorage:
     def mini_batch_generator(self, num_mini_batches, num_epochs=8):
         batch_size = self.num_envs * self.num_transitions_per_env
         mini_batch_size = batch_size // num_mini_batches
-        indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
+        indices = minibatch_permutation(num_mini_batches * mini_batch_size, self.device)
         observations = self.observations.flatten(0, 1)
         critic_observations = self.privileged_observations.flatten(0, 1) if self.privileged_observations is not None else observations
         actions = self.actions.flatten(0, 1)
