@@ -110,8 +110,19 @@ typedef struct lgs_sim_params {
     int32_t clamp_joint_velocity;    /* clamp |qd| to the URDF velocity limit */
     int32_t max_contacts;            /* contact slots per env               */
     int32_t max_rows;                /* constraint rows per env (<= compiled capacity);
-                                        joint-limit rows are capped at max_rows - 3*max_contacts */
+                                        joint-limit rows: max_rows - 3*max_contacts, plus the
+                                        rows of the contact slots a substep leaves unused */
 } lgs_sim_params;
+/* Contact slots per substep (PhysX reports every touching shape; a fixed-capacity solver has
+ * to choose).  In this order, while slots last:
+ *   1. every body touching the ground gets ONE slot, for its first touching candidate point
+ *      (candidate order; bodies in the order of those candidates),
+ *   2. self contacts (pair order), at most max_self_contacts,
+ *   3. the remaining touching ground candidates, in candidate order.
+ * So planted feet cannot take the slots of a knee, hip or pelvis on the ground (its contact
+ * force, the collision penalty and contact terminations depend on them).  Joint limits take
+ * the limit rows in DOF order, then the rows of unused contact slots.  Whatever still does not
+ * fit is counted: lgs_get_contact_stats. */
 
 /* ---- self-collision (IsaacGym create_actor collision filter, legged_robot.py:373-374:
  *      cfg.asset.self_collisions == 0 lets the links of one actor collide; see
@@ -121,9 +132,8 @@ typedef struct lgs_sim_params {
  *      radii and rest_offset, active below contact_offset.  A touching pair is one contact
  *      (normal from the second body to the first, a friction pair, the env's shape friction)
  *      in the slots after the ground contacts; up to max_self_contacts of them per substep,
- *      first in pair order, and the ground contacts are then capped at max_contacts minus
- *      the self contacts taken.  The contact force joins both bodies' net contact force
- *      with opposite signs.                                                            */
+ *      first in pair order, after one slot per touching ground body (the slot order above).
+ *      The contact force joins both bodies' net contact force with opposite signs.      */
 typedef struct lgs_self_collision_desc {
     int32_t num_proxies;          /* S <= LGS_MAX_SELF_PROXIES                          */
     const int32_t* proxy_body;    /* [S]                                                */
@@ -346,6 +356,16 @@ LGS_API const char* lgs_get_body_name(lgs_sim* sim, int32_t index);
 LGS_API const char* lgs_get_dof_name(lgs_sim* sim, int32_t index);
 LGS_API int32_t lgs_find_body(lgs_sim* sim, const char* name);
 LGS_API int32_t lgs_find_dof(lgs_sim* sim, const char* name);
+
+/* capacity diagnostics (see the slot order above lgs_self_collision_desc): counts summed
+ * over every env and substep of lgs_step / lgs_step_physics / lgs_simulate since the sim was
+ * created or last reset:
+ *   out[0] touching bodies that got no contact slot
+ *   out[1] touching self-collision pairs without a slot
+ *   out[2] violated joint limits without a constraint row
+ * Synchronises the sim's stream; reset != 0 zeroes the counters afterwards. */
+#define LGS_NUM_CONTACT_STATS 3
+LGS_API int lgs_get_contact_stats(lgs_sim* sim, uint64_t* out, int32_t reset);
 
 /* diagnostics: per-phase s_memtime cycle sums [N][24] of the last lgs_step
  * (only in a library built with -DLGS_PHASE_STAMPS; otherwise LGS_ERR_STATE) */

@@ -130,11 +130,12 @@ typedef struct pmlp_reduce_step {
     float ecoef;
     const float* stdv;
     float *stats, *dstd;
-    float* norm_partial;        /* optional: >= nparts floats                        */
+    float* norm_partial;        /* optional: nparts (in) floats                      */
     float *step, *lr, *acc;
     float desired_kl;
     int32_t adaptive;
-    int32_t nparts;             /* out                                               */
+    int32_t nparts;             /* in: norm_partial's capacity (floats; checked before the launch,
+                                   -1 when short); out: the partials written           */
 } pmlp_reduce_step;
 PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, pmlp_reduce_step* r, void* stream);
 
@@ -287,7 +288,7 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
 /* ---- recurrent heads (the fused recurrent optimizer step, rsl_rl/algorithms/fused_recurrent.py):
  * the MLP heads of ActorCriticRecurrent on the LSTM output h [M, H] (rsl_rl
  * actor_critic_recurrent.py: the actor / critic Sequential(Linear(H, N0), ELU, Linear(N0, N1))),
- * fp32, up to two nets per launch.  H in {32, 64, 128}; N0 <= 32 a multiple of 4; N1 <= 16.
+ * fp32, up to two nets per launch.  H in {32, 64, 128}; N0 <= 32 a multiple of 8; N1 <= 16.
  * pmlp_heads_forward:  y0 = elu(W0 h + b0) [M, N0], out = W1 y0 + b1 [M, N1]
  * pmlp_heads_backward: from dout [M, N1] (the loss gradient): dh = W0^T ((W1^T dout) * elu'(y0))
  *   [M, H] (the LSTM's output gradient, elu' from the output as torch), and the partial

@@ -332,6 +332,22 @@ static void bwd_sub(const float* L, const float* invd, int n, float* x) {
     }
 }
 
+/* capacity-drop counters (lgs_get_contact_stats semantics): bodies touching the ground
+ * without a slot, self contacts without a slot, violated joint limits without a row */
+static uint64_t g_stats[LGS_NUM_CONTACT_STATS];
+static void stats_add(int k, int v) {
+    if (v > 0) {
+#pragma omp atomic
+        g_stats[k] += (uint64_t)v;
+    }
+}
+void orc_contact_stats(uint64_t* out, int reset) {
+    for (int k = 0; k < LGS_NUM_CONTACT_STATS; ++k) {
+        out[k] = g_stats[k];
+        if (reset) g_stats[k] = 0;
+    }
+}
+
 /* One physics substep of one env (gym.simulate, legged_robot.py:630).
  * root13/dof (in/out), tau [D], contact forces out [B][3], added base mass, friction. */
 void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* root13, float* dofs,
@@ -503,7 +519,13 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
 
     /* ---- constraint rows: contacts (n, t1, t2) first, then joint limits.
      * Gauss-Seidel visits them in this order (the HIP kernel keeps contact c at
-     * rows 3c..3c+2 so its row registers are compile-time indexed). ---- */
+     * rows 3c..3c+2 so its row registers are compile-time indexed).
+     * Contact slots (include/leggedsim.h, above lgs_self_collision_desc): one per body
+     * touching the ground, for its first touching candidate (candidate order); then up to
+     * max_self self contacts (pair order); then the other touching ground candidates
+     * (candidate order), while the max_contacts slots last.  Joint limits (DOF order) take
+     * max_rows - 3*max_contacts rows plus those of the unused contact slots.  What does not
+     * fit is counted (orc_contact_stats). ---- */
     static __thread float J[ROWMAX][NMAX];
     float tgt[ROWMAX], lam[ROWMAX], v[ROWMAX];
     int kind[ROWMAX]; /* 0 unilateral, 1 friction pair head, 2 friction pair tail */
@@ -513,49 +535,52 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
     int nr = 0;
     const float beta = sp->baumgarte;
     const int max_rows = sp->max_rows < ROWMAX ? sp->max_rows : ROWMAX;
-    const int max_limit = max_rows - 3 * sp->max_contacts;
+    const int maxc = sp->max_contacts;
+    const int max_limit = max_rows - 3 * maxc;
     int nc = 0;
     float cpt[ROWMAX / 3 + 1][3];
     float cfr[ROWMAX / 3 + 1][3][3]; /* contact frame: normal, tangent 1, tangent 2 */
-    /* self contacts first (pair order, at most max_self of them), so the ground leaves their
-     * slots free; they join the row list after the ground contacts */
-    int nsc = 0, sc_body[ROWMAX / 3 + 1][2];
+    /* self contacts: every pair tested, the first maxc (pair order) kept */
+    int nsf = 0, sc_body[ROWMAX / 3 + 1][2];
     float sc_pt[ROWMAX / 3 + 1][3], sc_sep[ROWMAX / 3 + 1], sc_n[ROWMAX / 3 + 1][3];
-    {
-        int maxs = g_self.max_self < sp->max_contacts ? g_self.max_self : sp->max_contacts;
-        for (int q = 0; q < g_self.npairs && nsc < maxs; ++q) {
-            float seg[2][2][3];
-            for (int h = 0; h < 2; ++h) {
-                int b = g_self.body[q][h];
-                for (int e = 0; e < 2; ++e) {
-                    matvec(K.R[b], g_self.cap[q][h] + 3 * e, seg[h][e]);
-                    for (int k = 0; k < 3; ++k) seg[h][e][k] += K.p[b][k];
-                }
+    for (int q = 0; q < g_self.npairs; ++q) {
+        float seg[2][2][3];
+        for (int h = 0; h < 2; ++h) {
+            int b = g_self.body[q][h];
+            for (int e = 0; e < 2; ++e) {
+                matvec(K.R[b], g_self.cap[q][h] + 3 * e, seg[h][e]);
+                for (int k = 0; k < 3; ++k) seg[h][e][k] += K.p[b][k];
             }
-            float c1[3], c2[3];
-            seg_closest(seg[0][0], seg[0][1], seg[1][0], seg[1][1], c1, c2);
-            float dx[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
-            float dist = sqrtf(dot3(dx, dx));
-            float nrm[3] = {0.f, 0.f, 1.f};
-            if (dist > 1e-9f) {
-                float inv = 1.f / dist;
-                for (int k = 0; k < 3; ++k) nrm[k] = dx[k] * inv;
-            }
-            float ra = g_self.cap[q][0][6], rb = g_self.cap[q][1][6];
-            float sep = dist - ra - rb - sp->rest_offset;
-            if (!(sep < sp->contact_offset)) continue;
-            sc_body[nsc][0] = g_self.body[q][0];
-            sc_body[nsc][1] = g_self.body[q][1];
-            for (int k = 0; k < 3; ++k) {
-                sc_pt[nsc][k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
-                sc_n[nsc][k] = nrm[k];
-            }
-            sc_sep[nsc] = sep;
-            ++nsc;
         }
+        float c1[3], c2[3];
+        seg_closest(seg[0][0], seg[0][1], seg[1][0], seg[1][1], c1, c2);
+        float dx[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
+        float dist = sqrtf(dot3(dx, dx));
+        float nrm[3] = {0.f, 0.f, 1.f};
+        if (dist > 1e-9f) {
+            float inv = 1.f / dist;
+            for (int k = 0; k < 3; ++k) nrm[k] = dx[k] * inv;
+        }
+        float ra = g_self.cap[q][0][6], rb = g_self.cap[q][1][6];
+        float sep = dist - ra - rb - sp->rest_offset;
+        if (!(sep < sp->contact_offset)) continue;
+        if (nsf < maxc) {
+            sc_body[nsf][0] = g_self.body[q][0];
+            sc_body[nsf][1] = g_self.body[q][1];
+            for (int k = 0; k < 3; ++k) {
+                sc_pt[nsf][k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
+                sc_n[nsf][k] = nrm[k];
+            }
+            sc_sep[nsf] = sep;
+        }
+        ++nsf;
     }
+    /* ground candidates: primaries (a body's first touching candidate) and the others */
+    struct gcand { int b; float pc[3], sep, nrm[3]; } prim[ROWMAX / 3 + 1], sec[ROWMAX / 3 + 1];
+    int np = 0, nsec = 0;
+    int seen[LGS_MAX_BODIES];
+    memset(seen, 0, sizeof(seen));
     for (int k = 0; k < md->num_points; ++k) {
-        if (nc >= sp->max_contacts - nsc || nr + 3 > max_rows) break;
         int b = md->pt_body[k];
         float c[3];
         matvec(K.R[b], md->pt_pos + 3 * k, c);
@@ -566,11 +591,35 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         /* signed distance of the sphere centre to the ground triangle's plane */
         float sep = (c[2] - hg) * nrm[2] - rad - sp->rest_offset;
         if (!(sep < sp->contact_offset)) continue;
-        float pc[3] = {c[0] - rad * nrm[0], c[1] - rad * nrm[1], c[2] - rad * nrm[2]};
+        struct gcand* g = NULL;
+        if (!seen[b]) {
+            seen[b] = 1;
+            if (np < maxc) g = &prim[np];
+            ++np;
+        } else {
+            if (nsec < maxc) g = &sec[nsec];
+            ++nsec;
+        }
+        if (!g) continue;
+        g->b = b;
+        g->sep = sep;
+        for (int t = 0; t < 3; ++t) { g->pc[t] = c[t] - rad * nrm[t]; g->nrm[t] = nrm[t]; }
+    }
+    const int npg = np < maxc ? np : maxc;
+    int nsc = nsf < g_self.max_self ? nsf : g_self.max_self;
+    if (nsc > maxc - npg) nsc = maxc - npg;
+    const int nsu = nsec < maxc - npg - nsc ? nsec : maxc - npg - nsc;
+    stats_add(0, np - npg);
+    stats_add(1, nsf - nsc);
+    for (int i = 0; i < npg + nsu; ++i) {
+        const struct gcand* g = i < npg ? &prim[i] : &sec[i - npg];
+        const int b = g->b;
+        const float* pc = g->pc;
+        const float sep = g->sep;
         float r[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]};
         float dirs[3][3];
-        memcpy(dirs[0], nrm, 12);
-        contact_tangents(nrm, dirs[1], dirs[2]);
+        memcpy(dirs[0], g->nrm, 12);
+        contact_tangents(g->nrm, dirs[1], dirs[2]);
         memcpy(cfr[nc], dirs, 36);
         for (int dd = 0; dd < 3; ++dd) {
             const float* d = dirs[dd];
@@ -637,24 +686,27 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
         nr += 3;
         ++nc;
     }
-    const int nr_c = nr;
-    for (int j = 0; j < D && nr - nr_c < max_limit; ++j) {
+    /* joint limits in DOF order: max_limit rows, then the rows of the unused contact slots */
+    const int max_lim_all = max_limit + 3 * (maxc - nc);
+    int nl = 0;
+    for (int j = 0; j < D; ++j) {
         float q = dofs[2 * j], lo = md->dof_lower[j], hi = md->dof_upper[j];
         float qn = q + dt * qf[6 + j];
+        if (!(qn < lo) && !(qn > hi)) continue;
+        if (nl++ >= max_lim_all) continue;
+        memset(J[nr], 0, sizeof(float) * n);
+        float gap;
         if (qn < lo) {
-            memset(J[nr], 0, sizeof(float) * n);
             J[nr][6 + j] = 1.f;
-            float gap = q - lo;
-            tgt[nr] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
-            kind[nr++] = 0;
-        } else if (qn > hi) {
-            memset(J[nr], 0, sizeof(float) * n);
+            gap = q - lo;
+        } else {
             J[nr][6 + j] = -1.f;
-            float gap = hi - q;
-            tgt[nr] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
-            kind[nr++] = 0;
+            gap = hi - q;
         }
+        tgt[nr] = gap >= 0.f ? -gap * idt : -beta * gap * idt;
+        kind[nr++] = 0;
     }
+    stats_add(2, nl > max_lim_all ? nl - max_lim_all : 0);
     /* Y = L^-1 J^T (leaves-first columns) ; A = Y^T Y ; v = J qf (natural order) */
     static __thread float Y[ROWMAX][NMAX];
     static __thread float A[ROWMAX][ROWMAX];

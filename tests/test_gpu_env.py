@@ -371,16 +371,19 @@ def test_fused_ppo_loss_matches_reference_loss(clipped):
         assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-4
 
 
-def test_rollout_graph_matches_eager_rollouts(tmp_path):
+@pytest.mark.parametrize("n", [512, 4])
+def test_rollout_graph_matches_eager_rollouts(tmp_path, n):
     """OnPolicyRunner's captured collection loop (_RolloutGraph) replays the same
     rollouts as the eager loop: same env states, storage, policy and logged
-    episode statistics (rewbuffer/lenbuffer/ep_infos) after several iterations."""
+    episode statistics (rewbuffer/lenbuffer/ep_infos) after several iterations.
+    4 envs is BASELINE configs[0]'s size (seed 1, legged_robot_config.py:245): 24-row
+    mini-batches through the fused update."""
     import json
     from legged_gym.utils.helpers import class_to_dict
     from rsl_rl.runners import OnPolicyRunner
     out = {}
     for graph in (False, True):
-        env = make("go2", 512, env__episode_length_s=0.5)  # 25-step episodes: resets inside every rollout
+        env = make("go2", n, env__episode_length_s=0.5)  # 25-step episodes: resets inside every rollout
         _, train_cfg = task_registry.get_cfgs("go2")
         cfg = class_to_dict(train_cfg)
         cfg["runner"]["rollout_graph"] = graph

@@ -277,35 +277,6 @@ def test_partial_tn_sum_col_is_the_ones_column_product(K, ks):
         assert err < 1e-5, (M, n, err)
 
 
-def test_fused_update_tn_is_bitwise_transposed_copies(monkeypatch):
-    """The whole fused update with row-major-only activations (PMLP_TN=1, the default)
-    equals the transposed-copy dataflow (PMLP_TN=0) bitwise: losses and parameters."""
-    torch.manual_seed(0)
-    N, T, O, A = 2048, 8, 48, 12
-    ac = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda()
-    algs = []
-    for tn in ("1", "0"):
-        monkeypatch.setenv("PMLP_TN", tn)
-        alg = PPO(copy.deepcopy(ac), num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3,
-                  schedule="adaptive", device="cuda")
-        alg.use_graph = False
-        alg.init_storage(N, T, [O], [None], [A])
-        assert alg._fused.tn == (tn == "1")
-        algs.append(alg)
-    for u in range(2):
-        data = _fill_storage(algs[1], T, N, O, A, seed=20 + u)
-        for k, v in data.items():
-            getattr(algs[0].storage, k).copy_(v)
-        algs[0].storage.step = T
-        torch.manual_seed(200 + u)
-        l0 = algs[0].update()
-        torch.manual_seed(200 + u)
-        l1 = algs[1].update()
-        assert l0 == l1
-        for a, b in zip(algs[0].actor_critic.parameters(), algs[1].actor_critic.parameters()):
-            assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("M,A,Ap", [(24576, 12, 16), (1000 + 37, 12, 16), (517, 8, 8), (2048, 10, 16)])
 def test_loss_step_kernel_matches_fp32_autograd(M, A, Ap):
     """pmlp_ppo_loss_step (the quad-per-row kernel for A % 4 == 0, the one-lane-per-row

@@ -295,12 +295,14 @@ def test_fused_step_matches_oracle_bitwise(task):
     fused_vs_oracle(env, g, 3, task)
 
 
-@pytest.mark.parametrize("task,n", [("go2", 1), ("go2", 37), ("h1_2", 65), ("go2", 4096), ("h1", 8192),
-                                    ("g1", 4096), ("h1_2", 8192)])
+@pytest.mark.parametrize("task,n", [("go2", 1), ("go2", 4), ("go2", 6), ("h1", 2), ("go2", 37), ("h1_2", 65),
+                                    ("go2", 4096), ("h1", 8192), ("g1", 4096), ("h1_2", 8192)])
 def test_fused_step_matches_oracle_bitwise_edge_and_full_sizes(task, n):
-    """Ragged env counts (partial XCD-mapped waves) and the BASELINE per-GPU sizes.  h1_2 at
-    65 envs, seed 65, is the case whose one-env torque mismatch round 1 hid behind a 1/n
-    allowance (fp contraction + libm vs ocml last-bit differences); it is exact now."""
+    """Ragged env counts (partial XCD-mapped waves) and the BASELINE per-GPU sizes.  Go2 at 4
+    envs is BASELINE configs[0]'s size; 4, 6 and 2 envs run two envs per wave on fewer
+    workgroups than the 8 XCDs xcd_env() deals over.  h1_2 at 65 envs, seed 65, is the case
+    whose one-env torque mismatch round 1 hid behind a 1/n allowance (fp contraction + libm vs
+    ocml last-bit differences); it is exact now."""
     env, g = warm(task, n, steps=8, seed=n)
     fused_vs_oracle(env, g, 2, f"{task} x{n}")
 
@@ -373,14 +375,10 @@ def test_two_envs_per_wave_is_bitwise_one_env_per_wave(monkeypatch):
 
 
 @pytest.mark.parametrize("task", ["h1", "g1", "h1_2"])
-def test_humanoid_32_row_variant_two_envs_per_wave(task, monkeypatch):
-    """The humanoids' 32-row capacity (8 contacts: 4 sole corners per foot, 8 limit rows)
-    runs two envs per wave like Go2; it must equal the oracle bit for bit and the
-    one-env-per-wave build of the same capacity over a rollout with resets."""
-    from legged_gym.envs.base.humanoid import HumanoidRobot
-    monkeypatch.setattr(HumanoidRobot, "max_contacts", 8)
-    monkeypatch.setattr(HumanoidRobot, "max_rows", 32)
-    monkeypatch.setattr(HumanoidRobot, "max_self_contacts", 2)
+def test_humanoid_two_envs_per_wave_is_bitwise_one_env_per_wave(task, monkeypatch):
+    """The humanoids' 32-row capacity (8 contact slots, 8 limit rows) runs two envs per wave
+    like Go2; it must equal the oracle bit for bit and the one-env-per-wave build of the same
+    capacity over a rollout with resets."""
     outs = []
     for epw in ("1", "2"):
         monkeypatch.setenv("LGS_ENVS_PER_WAVE", epw)

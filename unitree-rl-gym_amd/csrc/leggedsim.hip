@@ -18,6 +18,7 @@
 // reference's order; observation/noise/reset draws are spread over lanes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -70,6 +71,10 @@ __device__ unsigned long long* g_phase_buf;
 #endif
 #define MAXB LGS_MAX_BODIES
 #define MAXD LGS_MAX_DEPTH
+// contact candidates per model: at most 32 chunks of 32 (the pre-filter's chunk masks)
+#define LGS_MAX_CHUNKS 32
+// slack of the contact pre-filter's bounding-sphere test (m): far above fp32 rounding
+#define LGS_PREFILTER_MARGIN 1e-3f
 #define WAVE 64
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -105,6 +110,12 @@ struct DevModel {
     const int* pt_body;
     const float* pt_pos;
     const float* pt_radius;
+    // contact pre-filter (lgs_create_sim): per body a bounding sphere of its candidates
+    // [cx cy cz rho rmax] (body frame; rho = max |p - c|, rmax = max radius, rho < 0: no
+    // candidates), and per chunk of 32 candidates the bit mask of the bodies in it
+    const float* bsph;
+    const unsigned* chunk32;
+    int nch32;
 };
 
 struct DevSim {
@@ -116,11 +127,22 @@ struct DevSim {
     const int16_t* hf;
     int hf_rows, hf_cols;
     float hf_inv_hs, hf_vs, hf_border;
+    // the map's slope bound (lgs_set_heightfield): 1 + G and 1/sqrt(1 + G^2), G = the largest
+    // triangle gradient norm; the contact pre-filter's terrain margin
+    float hf_slope1, hf_nmin;
     // self-collision (lgs_set_self_collision): n_selfp pair records of 16 floats,
     // [p0(3) p1(3) r body] of the first proxy then of the second; n_selfp == 0: off
     const float4* selfp;
     int n_selfp, max_self;
+    // [8][LGS_NUM_CONTACT_STATS] capacity-drop counters, one row per XCD (lgs_get_contact_stats)
+    unsigned long long* stats;
 };
+
+// a substep's capacity drops into the per-XCD counter row (rare: atomics only when nonzero,
+// and no register holds a count across the substeps)
+__device__ __forceinline__ void count_drops(const DevSim& sp, int lane, int k, int v) {
+    if (lane == 0 && v > 0) atomicAdd(sp.stats + LGS_NUM_CONTACT_STATS * (blockIdx.x & 7u) + k, (unsigned long long)v);
+}
 
 struct DevState {
     float* root;     // [N,13]
@@ -335,7 +357,15 @@ struct ModelCache {
     unsigned char chain[B][MAXD];
     float jr[B][9], jp[B][3], ax[B][3], com[B][3], mass[B], in[B][6];
     float lo[D > 0 ? D : 1], hi[D > 0 ? D : 1], vl[D > 0 ? D : 1];
+    float bs[B][5];                 // candidates' bounding sphere per body (DevModel::bsph)
+    unsigned ch32[LGS_MAX_CHUNKS];  // bodies per chunk of 32 candidates (zero-padded)
 };
+
+// bodies with candidates in chunk ch of WAVE/EPW candidates
+template <int EPW, int D, int B>
+__device__ __forceinline__ unsigned chunk_bodies(const ModelCache<D, B>& mc, int ch) {
+    return EPW == 2 ? mc.ch32[ch] : (mc.ch32[2 * ch] | mc.ch32[2 * ch + 1]);
+}
 
 template <int D, int B, int ROWS>
 struct Smem {
@@ -367,6 +397,13 @@ struct Smem {
             float terms[LGS_MAX_REWARDS + 1];
             float misc[32];
         } post;
+        struct {  // contact selection (step 8, before any constraint row is written)
+            int pwin[B];              // per body: its first touching candidate so far (primary)
+            int sec_body[ROWS / 4];   // ground contacts beyond the primaries, in candidate order
+            float sec[ROWS / 4][7];   // point(3), separation, normal(3)
+            int sc_ab[ROWS / 4][2];   // self contacts, in pair order
+            float sc_tmp[ROWS / 4][7];  // point(3), separation, normal(3)
+        } sel;
     } u;
     static constexpr int LP = (n + 3) / 4 * 4;  // 16-byte rows: uniform row reads are ds_read_b128
     __attribute__((aligned(16))) float L[n][LP];
@@ -375,8 +412,6 @@ struct Smem {
     float tgt[ROWS];
     int c_body[ROWS / 3];
     int c_body2[ROWS / 3];    // self contact: the second body (its force enters with a minus sign)
-    int sc_ab[ROWS / 3][2];   // self contacts of this substep before their slots are known
-    float sc_tmp[ROWS / 3][7];  // point(3), separation, normal(3)
     float c_pt[ROWS / 3][3];
     float c_fr[ROWS / 3][9];  // contact frame: normal, tangent 1, tangent 2
     float c_sep[ROWS / 3];
@@ -408,6 +443,8 @@ __device__ __forceinline__ void load_model(ModelCache<D, B>& c, const DevModel& 
         (&c.com[0][0])[i] = md.com[i];
     }
     for (int i = lane; i < 6 * B; i += WAVE) (&c.in[0][0])[i] = md.inertia[i];
+    for (int i = lane; i < 5 * B; i += WAVE) (&c.bs[0][0])[i] = md.bsph[i];
+    if (lane < LGS_MAX_CHUNKS) c.ch32[lane] = lane < md.nch32 ? md.chunk32[lane] : 0u;
     if (lane < D) {
         int bj = 0;
         for (int b = 0; b < B; ++b) bj = md.dof[b] == lane ? b : bj;
@@ -784,7 +821,15 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
     }
     }
     // free velocity (classical velocity of the root origin after dt); lane i holds
-    // qdd of natural index r = n-1-i, s.qf is in the natural order
+    // qdd of natural index r = n-1-i, s.qf is in the natural order.  Lane b < B also runs
+    // the contact pre-filter: body b's candidates may touch the ground only if their
+    // bounding sphere (world centre C, radius rho, largest candidate radius rmax) reaches
+    // within contact_offset + margin of it.  Plane: C_z - rho - rmax - rest.  Heightfield
+    // (h piecewise linear with gradient norm <= G, normal n_z >= nmin): every candidate's
+    // height above the triangle under it is >= C_z - h(C) - (1 + G) rho, so its separation
+    // is >= nmin (C_z - h(C) - (1 + G) rho) - rmax - rest.  The test only skips candidates
+    // that cannot be active: the selected contacts are the ones a full scan selects.
+    uint32_t touch;
     {
         float wxv[3];
         cross3(w0, vO, wxv);
@@ -796,23 +841,50 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         if (lane < D) s.qf[r] = s.qd[r - 6] + dt * x;
         else if (lane < n - 3) s.qf[r] = vl + dt * (x + cl);
         else if (lane < n) s.qf[r] = wl + dt * x;
+        bool may = false;
+        if (lane < B) {
+            s.u.sel.pwin[lane] = 0x7fffffff;
+            const float* bs = mc.bs[lane];
+            if (bs[3] >= 0.f) {
+                float cw[3];
+                matvec(s.R[lane], bs, cw);
+                const float cz = cw[2] + s.p[lane][2];
+                float gap;
+                if (sp.hf) {
+                    float nrm[3];
+                    const float h = terrain_sample(sp, cw[0] + s.p[lane][0], cw[1] + s.p[lane][1], nrm);
+                    gap = sp.hf_nmin * (cz - h - sp.hf_slope1 * bs[3]) - bs[4];
+                } else {
+                    gap = cz - bs[3] - bs[4];
+                }
+                may = gap - sp.rest_offset < sp.contact_offset + LGS_PREFILTER_MARGIN;
+            }
+        }
+        touch = (uint32_t)hballot<EPW>(may);
     }
     __syncthreads();
     STAMP(7);
-    // ---- 8. constraint rows.  Fixed layout: contact c at rows 3c (normal),
-    // 3c+1, 3c+2 (friction), c < CM; joint limit l at row 3*CM + l, l < LM.
-    // Gauss-Seidel order: contacts ascending, then limits (oracle's row order).
+    // ---- 8. constraint rows.  Fixed layout: contact slot c at rows 3c (normal), 3c+1,
+    // 3c+2 (friction), c < CM; joint limit l at row 3*CM + l, l < LM, and the limits
+    // beyond LM in the rows of the unused contact slots (3*nc ...).
+    // Slot policy (the oracle's, oracle/lgs_oracle.c orc_substep_env): every touching
+    // body first gets ONE slot for its first touching candidate (the primaries, in
+    // candidate order: the feet's come first, Model.reorder_points), then the self
+    // contacts take up to max_self slots (pair order), then the remaining touching ground
+    // candidates fill what is left, in candidate order.  So two planted soles cannot
+    // starve a knee, hip or pelvis on the ground of its contact row.  What does not fit
+    // is counted (Drops, lgs_get_contact_stats).
+    // Gauss-Seidel order: contacts ascending, then limits in DOF order.
     constexpr int CM = ROWS / 4, LM = ROWS - 3 * CM;
     const float beta = sp.beta;
+    const int maxc = sp.max_contacts < CM ? sp.max_contacts : CM;
     int nc = 0, ncg = 0;  // contacts, of which the first ncg are ground contacts
     {
-        const int maxc_all = sp.max_contacts < CM ? sp.max_contacts : CM;
-        // self contacts (lane per proxy pair, first max_self in pair order) are found first,
-        // so the ground contacts can leave them their slots; they are appended below
-        int nsc = 0;
+        // self contacts: lane per proxy pair, every pair tested; the first maxc in pair
+        // order are staged
+        int nsf = 0;
         if (sp.n_selfp > 0) {
-            const int maxs = sp.max_self < maxc_all ? sp.max_self : maxc_all;
-            for (int base = 0; base < sp.n_selfp && nsc < maxs; base += WAVE / EPW) {
+            for (int base = 0; base < sp.n_selfp; base += WAVE / EPW) {
                 const int q = base + lane;
                 bool act = false;
                 float pc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 1.f}, sep = 0.f;
@@ -849,20 +921,26 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     for (int k = 0; k < 3; ++k) pc[k] = 0.5f * ((c1[k] - ra * nrm[k]) + (c2[k] + rb * nrm[k]));
                 }
                 const uint64_t mask = hballot<EPW>(act);
-                const int slot = nsc + __popcll(mask & ((1ull << lane) - 1ull));
-                if (act && slot < maxs) {
-                    s.sc_ab[slot][0] = ba; s.sc_ab[slot][1] = bb;
-                    float* t = s.sc_tmp[slot];
+                const int slot = nsf + __popcll(mask & ((1ull << lane) - 1ull));
+                if (act && slot < maxc) {
+                    s.u.sel.sc_ab[slot][0] = ba; s.u.sel.sc_ab[slot][1] = bb;
+                    float* t = s.u.sel.sc_tmp[slot];
                     t[0] = pc[0]; t[1] = pc[1]; t[2] = pc[2]; t[3] = sep;
                     t[4] = nrm[0]; t[5] = nrm[1]; t[6] = nrm[2];
                 }
-                nsc += __popcll(mask);
-                if (nsc > maxs) nsc = maxs;
+                nsf += __popcll(mask);
             }
         }
-        const int maxc = maxc_all - nsc;
-        for (int base = 0; base < md.P && nc < maxc; base += WAVE / EPW) {
-            const int k = base + lane;
+        // ground candidates: lane per candidate over the chunks that hold a body the
+        // pre-filter kept.  A touching candidate is its body's primary when it is the
+        // body's first touching candidate (LDS min of the candidate index over the chunks
+        // so far: chunks run in index order); primaries go straight to their slots, the
+        // others are staged in candidate order.
+        int np = 0, nsec = 0;
+        const int nch = (md.P + WAVE / EPW - 1) / (WAVE / EPW);
+        for (int ch = 0; ch < nch; ++ch) {
+            if (!(chunk_bodies<EPW>(mc, ch) & touch)) continue;  // (env-uniform)
+            const int k = ch * (WAVE / EPW) + lane;
             bool act = false;
             float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f, nrm[3] = {0.f, 0.f, 1.f};
             int b = 0;
@@ -880,46 +958,76 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                 sep = (c[2] - h) * nrm[2] - rad - sp.rest_offset;
                 act = sep < sp.contact_offset;
             }
-            const uint64_t mask = hballot<EPW>(act);
-            const int slot = nc + __popcll(mask & ((1ull << lane) - 1ull));
-            if (act && slot < maxc) {
-                s.c_body[slot] = b;
-                s.c_pt[slot][0] = c[0] - rad * nrm[0];
-                s.c_pt[slot][1] = c[1] - rad * nrm[1];
-                s.c_pt[slot][2] = c[2] - rad * nrm[2];
-                s.c_sep[slot] = sep;
+            if (act) atomicMin(&s.u.sel.pwin[b], k);
+            __syncthreads();
+            const bool prim = act && s.u.sel.pwin[b] == k;
+            const bool sec = act && !prim;
+            const uint64_t pm = hballot<EPW>(prim), sm_ = hballot<EPW>(sec);
+            const uint64_t below = (1ull << lane) - 1ull;
+            const int ps = np + __popcll(pm & below), ss = nsec + __popcll(sm_ & below);
+            const float pc[3] = {c[0] - rad * nrm[0], c[1] - rad * nrm[1], c[2] - rad * nrm[2]};
+            if (prim && ps < maxc) {
+                s.c_body[ps] = b;
+                s.c_pt[ps][0] = pc[0]; s.c_pt[ps][1] = pc[1]; s.c_pt[ps][2] = pc[2];
+                s.c_sep[ps] = sep;
                 float t1[3] = {1.f, 0.f, 0.f}, t2[3] = {0.f, 1.f, 0.f};  // plane: +x, +y
                 if (sp.hf) contact_tangents(nrm, t1, t2);
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
-                    s.c_fr[slot][t] = nrm[t]; s.c_fr[slot][3 + t] = t1[t]; s.c_fr[slot][6 + t] = t2[t];
+                    s.c_fr[ps][t] = nrm[t]; s.c_fr[ps][3 + t] = t1[t]; s.c_fr[ps][6 + t] = t2[t];
                 }
             }
-            nc += __popcll(mask);
-            if (nc > maxc) nc = maxc;
+            if (sec && ss < maxc) {
+                s.u.sel.sec_body[ss] = b;
+                float* t = s.u.sel.sec[ss];
+                t[0] = pc[0]; t[1] = pc[1]; t[2] = pc[2]; t[3] = sep;
+                t[4] = nrm[0]; t[5] = nrm[1]; t[6] = nrm[2];
+            }
+            np += __popcll(pm);
+            nsec += __popcll(sm_);
         }
-        ncg = nc;
-        if (nsc > 0) {
-            __syncthreads();
-            if (lane < nsc) {
-                const int slot = ncg + lane;
-                s.c_body[slot] = s.sc_ab[lane][0];
-                s.c_body2[slot] = s.sc_ab[lane][1];
-                const float* t = s.sc_tmp[lane];
-                s.c_pt[slot][0] = t[0]; s.c_pt[slot][1] = t[1]; s.c_pt[slot][2] = t[2];
-                s.c_sep[slot] = t[3];
-                const float nrm[3] = {t[4], t[5], t[6]};
-                float t1[3], t2[3];
-                self_tangents(nrm, t1, t2);
+        const int npg = np < maxc ? np : maxc;
+        int nsc = nsf < sp.max_self ? nsf : sp.max_self;
+        if (nsc > maxc - npg) nsc = maxc - npg;
+        const int nsu = nsec < maxc - npg - nsc ? nsec : maxc - npg - nsc;
+        ncg = npg + nsu;
+        nc = ncg + nsc;
+        count_drops(sp, lane, 0, np - npg);
+        count_drops(sp, lane, 1, nsf - nsc);
+        __syncthreads();
+        if (lane < nsu) {  // staged ground contacts after the primaries
+            const int slot = npg + lane;
+            const float* t = s.u.sel.sec[lane];
+            s.c_body[slot] = s.u.sel.sec_body[lane];
+            s.c_pt[slot][0] = t[0]; s.c_pt[slot][1] = t[1]; s.c_pt[slot][2] = t[2];
+            s.c_sep[slot] = t[3];
+            const float nrm[3] = {t[4], t[5], t[6]};
+            float t1[3] = {1.f, 0.f, 0.f}, t2[3] = {0.f, 1.f, 0.f};
+            if (sp.hf) contact_tangents(nrm, t1, t2);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    s.c_fr[slot][k] = nrm[k]; s.c_fr[slot][3 + k] = t1[k]; s.c_fr[slot][6 + k] = t2[k];
-                }
+            for (int k = 0; k < 3; ++k) {
+                s.c_fr[slot][k] = nrm[k]; s.c_fr[slot][3 + k] = t1[k]; s.c_fr[slot][6 + k] = t2[k];
             }
-            nc = ncg + nsc;
+        } else if (lane >= CM && lane < CM + nsc) {  // then the self contacts
+            const int j = lane - CM, slot = ncg + j;
+            s.c_body[slot] = s.u.sel.sc_ab[j][0];
+            s.c_body2[slot] = s.u.sel.sc_ab[j][1];
+            const float* t = s.u.sel.sc_tmp[j];
+            s.c_pt[slot][0] = t[0]; s.c_pt[slot][1] = t[1]; s.c_pt[slot][2] = t[2];
+            s.c_sep[slot] = t[3];
+            const float nrm[3] = {t[4], t[5], t[6]};
+            float t1[3], t2[3];
+            self_tangents(nrm, t1, t2);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s.c_fr[slot][k] = nrm[k]; s.c_fr[slot][3 + k] = t1[k]; s.c_fr[slot][6 + k] = t2[k];
+            }
         }
+        __syncthreads();  // the staging (s.u.sel) is dead before the constraint rows (s.u.con) are written
     }
-    int nlimit;
+    // joint limits: the first max_limit in DOF order take the limit block, the next ones the
+    // rows of the unused contact slots; the rest are counted (Drops::limits)
+    int nlimit, nover;
     {
         bool lo_act = false, hi_act = false;
         float gap = 0.f;
@@ -934,10 +1042,12 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         const int slot = __popcll(mask & ((1ull << lane) - 1ull));
         int max_limit = sp.max_rows - 3 * sp.max_contacts;
         if (max_limit > LM) max_limit = LM;
-        nlimit = __popcll(mask);
-        if (nlimit > max_limit) nlimit = max_limit;
-        if (act && slot < max_limit) {
-            const int r = 3 * CM + slot;
+        const int nl = __popcll(mask);
+        nlimit = nl < max_limit ? nl : max_limit;
+        nover = nl - nlimit < 3 * (maxc - nc) ? nl - nlimit : 3 * (maxc - nc);
+        count_drops(sp, lane, 2, nl - nlimit - nover);
+        if (act && slot < nlimit + nover) {
+            const int r = slot < nlimit ? 3 * CM + slot : 3 * nc + (slot - nlimit);
             float* row = s.u.con.Y[r];
             for (int i = 0; i < n; ++i) row[i] = 0.f;
             row[6 + lane] = lo_act ? 1.f : -1.f;
@@ -989,7 +1099,8 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
     }
     __syncthreads();
     STAMP(9);
-    const bool used = (lane < 3 * nc) || (lane >= 3 * CM && lane < 3 * CM + nlimit);
+    // rows in use: the contacts' and the overflow limits' (3nc ...), the limit block's
+    const bool used = (lane < 3 * nc + nover) || (lane >= 3 * CM && lane < 3 * CM + nlimit);
     // ---- 9. v = J qf ; Y = L^-1 J^T (lane r; L entries broadcast from their row lanes)
     float v = 0.f;
     float dg = 0.f;  // A_rr = |Y_r|^2 of this lane's row (the MFMA's fp32 chain, k ascending)
@@ -1089,7 +1200,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         // l holds column 32 tj + (l & 31), rows (t&3)+8(t>>2)+4(l>>5), and its partner
         // l ^ 32 the other half.  (A^T tile entries are the same products in the same order:
         // bit-identical to the mirrored tile.)  A never goes through LDS.
-        const int hi_row = nlimit > 0 ? 3 * CM + nlimit : 3 * nc;
+        const int hi_row = nlimit > 0 ? 3 * CM + nlimit : 3 * nc + nover;
         const int nt = (hi_row + 31) >> 5;
         const bool up = threadIdx.x >= 32;
 #pragma unroll
@@ -1193,6 +1304,17 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                         lamv[r] = ln;
                     }
                 }
+                if (nover > 0) {  // limits in the rows of unused contact slots (rare: their
+                                  // constants are broadcast per use, no registers held for them)
+#pragma unroll
+                    for (int r = 0; r < 3 * CM; ++r)
+                        if (r >= 3 * nc && r < 3 * nc + nover) {
+                            const float lo = lamv[r];
+                            const float ln = fmaxf(0.f, lo + (bc<EPW>(tg, r) - bc<EPW>(v, r)) * bc<EPW>(inv, r));
+                            v = fmaf(acol[r], ln - lo, v);
+                            lamv[r] = ln;
+                        }
+                }
             }
         } else
         for (int it = 0; it < sp.iters; ++it) {
@@ -1240,6 +1362,16 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     lam = lid == r ? ln : lam;
                 }
             }
+            if (nover > 0) {  // limits in the rows of unused contact slots
+#pragma unroll
+                for (int r = 0; r < 3 * CM; ++r)
+                    if (r >= 3 * nc && r < 3 * nc + nover) {
+                        const float lo = bc<EPW>(lam, r);
+                        const float ln = fmaxf(0.f, lo + (bc<EPW>(tg, r) - bc<EPW>(v, r)) * bc<EPW>(inv, r));
+                        v = fmaf(acol[r], ln - lo, v);
+                        lam = lid == r ? ln : lam;
+                    }
+            }
         }
     }
     STAMP(12);
@@ -1265,6 +1397,13 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
             const float ll = EPW == 2 ? lamv[3 * CM + l] : bc<EPW>(lam, 3 * CM + l);
             if (lane < n) z = fmaf(s.u.con.Y[3 * CM + l][lane], ll, z);
         }
+    if (nover > 0)
+#pragma unroll
+        for (int r = 0; r < 3 * CM; ++r)
+            if (r >= 3 * nc && r < 3 * nc + nover) {
+                const float ll = EPW == 2 ? lamv[r] : bc<EPW>(lam, r);
+                if (lane < n) z = fmaf(s.u.con.Y[r][lane], ll, z);
+            }
     if constexpr (EPW == 2) {  // the uniform backward solve of step 7
         __syncthreads();  // (every read of s.tgt / the limit rows is done: reuse s.tgt as scratch)
         if (lane < n) s.tgt[lane] = z;
@@ -2021,6 +2160,7 @@ struct lgs_sim {
     float* friction = nullptr;
     float* added_mass = nullptr;
     float* vsim = nullptr;  // [N,2] scratch of the all-env push bookkeeping (DevState::vsim)
+    unsigned long long* stats = nullptr;  // [8][LGS_NUM_CONTACT_STATS] capacity-drop counters (DevState::stats)
     float* root = nullptr;
     float* dofs = nullptr;
     float* cforce = nullptr;
@@ -2232,6 +2372,12 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
         return set_err(LGS_ERR_ARG, "lgs_create_sim: model exceeds LGS_MAX_BODIES/LGS_MAX_DOFS");
     for (int b = 0; b < m->num_bodies; ++b)
         if (m->depth[b] >= LGS_MAX_DEPTH) return set_err(LGS_ERR_ARG, "lgs_create_sim: tree deeper than LGS_MAX_DEPTH");
+    if (m->num_points < 0 || m->num_points > 32 * LGS_MAX_CHUNKS)
+        return set_err(LGS_ERR_ARG, "lgs_create_sim: more than " + std::to_string(32 * LGS_MAX_CHUNKS) +
+                                        " contact candidates");
+    for (int k = 0; k < m->num_points; ++k)
+        if (m->pt_body[k] < 0 || m->pt_body[k] >= m->num_bodies)
+            return set_err(LGS_ERR_ARG, "lgs_create_sim: contact candidate body out of range");
     HIP_TRY(hipSetDevice(device_id));
     lgs_sim* s = new lgs_sim();
     s->N = num_envs; s->B = m->num_bodies; s->D = m->num_dofs; s->P = m->num_points; s->device = device_id;
@@ -2266,9 +2412,42 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     if (m->dof_names)
         for (int j = 0; j < D; ++j) s->dof_names.emplace_back(m->dof_names[j] ? m->dof_names[j] : "");
     // pack the model into one device allocation
-    size_t ints = (size_t)B * (4 + LGS_MAX_DEPTH) + (size_t)P;
-    size_t floats = (size_t)B * (9 + 3 + 3 + 1 + 3 + 6) + (size_t)D * 3 + (size_t)P * 4;
-    size_t bytes = ints * 4 + floats * 4 + 256;
+    // contact pre-filter data: per body the bounding sphere of its candidates (centre = the
+    // middle of their box, rho = the largest distance to it, rmax = the largest radius, all
+    // rounded up), per chunk of 32 candidates the bit mask of their bodies
+    std::vector<float> bsph((size_t)5 * B, 0.f);
+    const int nch32 = (P + 31) / 32;
+    std::vector<unsigned> chunk32((size_t)(nch32 > 0 ? nch32 : 1), 0u);
+    for (int b = 0; b < B; ++b) {
+        double lo[3] = {1e30, 1e30, 1e30}, hi[3] = {-1e30, -1e30, -1e30}, rmax = 0.0;
+        int cnt = 0;
+        for (int k = 0; k < P; ++k) {
+            if (m->pt_body[k] != b) continue;
+            ++cnt;
+            for (int t = 0; t < 3; ++t) {
+                lo[t] = std::min(lo[t], (double)m->pt_pos[3 * k + t]);
+                hi[t] = std::max(hi[t], (double)m->pt_pos[3 * k + t]);
+            }
+            rmax = std::max(rmax, (double)m->pt_radius[k]);
+        }
+        float* o = &bsph[(size_t)5 * b];
+        if (!cnt) { o[3] = -1.f; continue; }
+        double c[3], rho = 0.0;
+        for (int t = 0; t < 3; ++t) c[t] = 0.5 * (lo[t] + hi[t]);
+        for (int k = 0; k < P; ++k) {
+            if (m->pt_body[k] != b) continue;
+            double d2 = 0.0;
+            for (int t = 0; t < 3; ++t) d2 += (m->pt_pos[3 * k + t] - c[t]) * (m->pt_pos[3 * k + t] - c[t]);
+            rho = std::max(rho, std::sqrt(d2));
+        }
+        for (int t = 0; t < 3; ++t) o[t] = (float)c[t];
+        o[3] = (float)(rho * (1.0 + 1e-6) + 1e-6);
+        o[4] = (float)(rmax * (1.0 + 1e-6) + 1e-6);
+    }
+    for (int k = 0; k < P; ++k) chunk32[k / 32] |= 1u << m->pt_body[k];
+    size_t ints = (size_t)B * (4 + LGS_MAX_DEPTH) + (size_t)P + chunk32.size();
+    size_t floats = (size_t)B * (9 + 3 + 3 + 1 + 3 + 6 + 5) + (size_t)D * 3 + (size_t)P * 4;
+    size_t bytes = ints * 4 + floats * 4 + 512;
     HIP_TRY(hipMalloc(&s->model_mem, bytes));
     char* host = (char*)calloc(1, bytes);
     size_t off = 0;
@@ -2284,6 +2463,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     size_t o_mass = put(m->mass, 4 * B), o_com = put(m->com, 12 * B), o_in = put(m->inertia, 24 * B);
     size_t o_lo = put(m->dof_lower, 4 * D), o_hi = put(m->dof_upper, 4 * D), o_vel = put(m->dof_velocity, 4 * D);
     size_t o_pb = put(m->pt_body, 4 * P), o_pp = put(m->pt_pos, 12 * P), o_pr = put(m->pt_radius, 4 * P);
+    size_t o_bs = put(bsph.data(), 20 * B), o_ch = put(chunk32.data(), 4 * chunk32.size());
     if (off > bytes) { free(host); return set_err(LGS_ERR_STATE, "model packing overflow"); }
     HIP_TRY(hipMemcpy(s->model_mem, host, off, hipMemcpyHostToDevice));
     free(host);
@@ -2296,6 +2476,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     md.mass = (const float*)(d + o_mass); md.com = (const float*)(d + o_com); md.inertia = (const float*)(d + o_in);
     md.dof_lower = (const float*)(d + o_lo); md.dof_upper = (const float*)(d + o_hi); md.dof_velocity = (const float*)(d + o_vel);
     md.pt_body = (const int*)(d + o_pb); md.pt_pos = (const float*)(d + o_pp); md.pt_radius = (const float*)(d + o_pr);
+    md.bsph = (const float*)(d + o_bs); md.chunk32 = (const unsigned*)(d + o_ch); md.nch32 = nch32;
     DevSim& sp = s->sp;
     sp.dt = p->dt; sp.gx = p->gravity[0]; sp.gy = p->gravity[1]; sp.gz = p->gravity[2];
     sp.iters = p->solver_iterations; sp.contact_offset = p->contact_offset; sp.rest_offset = p->rest_offset;
@@ -2303,10 +2484,14 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     sp.armature = p->armature; sp.clamp_qd = p->clamp_joint_velocity; sp.max_contacts = p->max_contacts;
     sp.max_rows = p->max_rows;
     sp.hf = nullptr; sp.hf_rows = sp.hf_cols = 0; sp.hf_inv_hs = sp.hf_vs = sp.hf_border = 0.f;
+    sp.hf_slope1 = 1.f; sp.hf_nmin = 1.f;
     sp.selfp = nullptr; sp.n_selfp = 0; sp.max_self = 0;
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->vsim, sizeof(float) * 2 * num_envs));
+    HIP_TRY(hipMalloc(&s->stats, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
+    HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
+    s->sp.stats = s->stats;
     HIP_TRY(hipMemset(s->added_mass, 0, sizeof(float) * num_envs));
     {
         float* ones = (float*)malloc(sizeof(float) * num_envs);
@@ -2325,6 +2510,7 @@ LGS_API int lgs_destroy_sim(lgs_sim* s) {
     (void)hipFree(s->friction);
     (void)hipFree(s->added_mass);
     (void)hipFree(s->vsim);
+    (void)hipFree(s->stats);
     (void)hipFree(s->task_dev);
     (void)hipFree(s->hf_mem);
     (void)hipFree(s->self_mem);
@@ -2351,6 +2537,22 @@ LGS_API int lgs_set_heightfield(lgs_sim* s, const int16_t* heights, int32_t rows
     s->sp.hf_inv_hs = 1.0f / horizontal_scale;
     s->sp.hf_vs = vertical_scale;
     s->sp.hf_border = border_size;
+    // slope bound of the map for the contact pre-filter: the largest gradient norm over the
+    // triangles terrain_sample() builds (both halves of every cell), rounded up
+    double g2 = 0.0;
+    const double is = 1.0 / horizontal_scale;
+    for (int i = 0; i + 1 < rows; ++i)
+        for (int j = 0; j + 1 < cols; ++j) {
+            const double h00 = heights[(size_t)i * cols + j] * (double)vertical_scale;
+            const double h01 = heights[(size_t)i * cols + j + 1] * (double)vertical_scale;
+            const double h10 = heights[(size_t)(i + 1) * cols + j] * (double)vertical_scale;
+            const double h11 = heights[(size_t)(i + 1) * cols + j + 1] * (double)vertical_scale;
+            const double a0 = (h10 - h00) * is, a1 = (h11 - h10) * is, b0 = (h11 - h01) * is, b1 = (h01 - h00) * is;
+            g2 = std::max(g2, std::max(a0 * a0 + a1 * a1, b0 * b0 + b1 * b1));
+        }
+    const double G = std::sqrt(g2) * (1.0 + 1e-6) + 1e-6;
+    s->sp.hf_slope1 = (float)(1.0 + G);
+    s->sp.hf_nmin = (float)(1.0 / std::sqrt(1.0 + G * G) * (1.0 - 1e-6));
     return LGS_OK;
 }
 
@@ -2564,6 +2766,23 @@ LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t*
     hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0,
                        (uint32_t)step_counter, (const float*)s->vsim);
     HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_get_contact_stats(lgs_sim* s, uint64_t* out, int32_t reset) {
+    if (!s || !out) return set_err(LGS_ERR_ARG, "lgs_get_contact_stats: null argument");
+    unsigned long long h[8 * LGS_NUM_CONTACT_STATS];
+    HIP_TRY(hipMemcpyAsync(h, s->stats, sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    for (int k = 0; k < LGS_NUM_CONTACT_STATS; ++k) {
+        uint64_t t = 0;
+        for (int x = 0; x < 8; ++x) t += h[LGS_NUM_CONTACT_STATS * x + k];
+        out[k] = t;
+    }
+    if (reset) {
+        HIP_TRY(hipMemsetAsync(s->stats, 0, sizeof(h), s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     return LGS_OK;
 }
 

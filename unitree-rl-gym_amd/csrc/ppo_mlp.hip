@@ -2022,16 +2022,10 @@ __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ re
     if (i == 0 && draw) *draw += 1;
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-
 // GEMM operand staging: 1 = LDS-DMA (GL) where the shapes allow it, 0 = register staging only
-// (PMLP_GLDS, or pmlp_set_gemm_staging for in-process A/B)
-static int g_glds = -1;
+// (pmlp_set_gemm_staging selects the others for in-process A/B)
+static int g_glds = 1;
 static int glds_on() {
-    if (g_glds < 0) g_glds = env_int("PMLP_GLDS", 1);
     return g_glds;
 }
 
@@ -2233,16 +2227,9 @@ static int reduce_pack(int32_t njobs, const pmlp_reduce_job* jobs, RedJobs& rj, 
         if (!J.slab || !J.out || J.nslabs <= 0 || J.n <= 0 || J.stride < J.n ||
             (J.bias_out && (J.cols_in <= J.cols_out || J.cols_out <= 0 || J.n % J.cols_in)))
             return fail(-1, "pmlp_reduce_slabs: bad job " + std::to_string(i));
-        static const bool split = [] {
-            const char* v = getenv("PMLP_REDUCE_GROUPS");  // 0: one thread per quad (A/B knob)
-            return !(v && v[0] == '0');
-        }();
-        static const int spt = [] {  // target slabs per thread (A/B knob)
-            const char* v = getenv("PMLP_REDUCE_SPT");
-            return v ? std::max(1, atoi(v)) : 8;
-        }();
+        constexpr int spt = 8;  // target slabs per thread (4 / 2 measured slower)
         int G = 1;  // <= spt slabs per thread, at most 32 groups
-        while (split && G < 32 && J.nslabs > spt * G) G *= 2;
+        while (G < 32 && J.nslabs > spt * G) G *= 2;
         rj.j[i] = RedJob{J.slab, J.out, J.bias_out, J.stride, J.n, J.nslabs, J.cols_in, J.cols_out, G};
         rj.start[i] = (int)nb;
         const int64_t eqb = 256 / G;  // element quads per block
@@ -2272,6 +2259,11 @@ PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, 
         return fail(-1, "pmlp_reduce_slabs_step: loss partials / stats / dstd / 0 < A <= 61");
     if (r->norm_partial && (!r->step || !r->lr))
         return fail(-1, "pmlp_reduce_slabs_step: norm_partial needs step and lr");
+    // every workgroup (+ the loss-finishing one) writes one norm partial: check the capacity
+    // before anything is launched
+    if (r->norm_partial && nb + 1 > (int64_t)r->nparts)
+        return fail(-1, "pmlp_reduce_slabs_step: " + std::to_string(nb + 1) + " norm partials > capacity " +
+                            std::to_string(r->nparts));
     const RedStep rs{r->loss_partial, r->loss_blocks, r->A, r->M, r->ecoef, r->stdv, r->stats, r->dstd,
                      r->norm_partial, r->step, r->lr, r->acc, r->desired_kl, r->adaptive};
     r->nparts = (int32_t)(nb + 1);  // + the loss-finishing workgroup
@@ -2403,11 +2395,8 @@ PMLP_API int pmlp_adam_mirror_n(float* param, const float* grad, float* exp_avg,
     }
     // grid cap 1024 blocks: for the Go2 parameters (1,486 blocks at one element per thread)
     // uncapped / 1024 / 512 / 256 measured 9.2-9.5 / 7.5-8.1 / 8.5-10.0 / 12.1-12.7 us
-    // (profiles/round2/update/adam_grid_ab.txt); PMLP_ADAM_BLOCKS overrides it (A/B knob)
-    static const int cap = [] {
-        const char* v = getenv("PMLP_ADAM_BLOCKS");
-        return v ? std::max(1, atoi(v)) : 1024;
-    }();
+    // (profiles/round2/update/adam_grid_ab.txt)
+    constexpr int cap = 1024;
     const int blocks = (int)std::min<int64_t>(cap, (n + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS);
     hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad, exp_avg,
                        exp_avg_sq, n, grad_scale, partial, nparts, step, lr, max_norm, beta1, beta2, eps, mj);
@@ -2512,8 +2501,7 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
     // rows per workgroup: 96 (one 150 KB workgroup per CU, every job in turn) for the update's
     // mini-batches; 32 with one job per workgroup for the rollout's num_envs rows
     hipStream_t st = (hipStream_t)stream;
-    static const int rows_ab = getenv("PMLP_FMLP_ROWS") ? atoi(getenv("PMLP_FMLP_ROWS")) : 0;  // (A/B knob)
-    if (rows_ab ? rows_ab == 96 : M >= 96 * 192)
+    if (M >= 96 * 192)
         hipLaunchKernelGGL(k_mlp_fwd<96>, dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0, st, fj, M);
     else
         hipLaunchKernelGGL(k_mlp_fwd<32>, dim3((M + 31) / 32, njobs), dim3(FMLP_THREADS), 0, st, fj, M);

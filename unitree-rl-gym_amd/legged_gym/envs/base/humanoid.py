@@ -10,13 +10,15 @@ from .legged_robot import LeggedRobot
 
 class HumanoidRobot(LeggedRobot):
     obs_layout = cabi.OBS_HUMANOID
-    # 8 contact slots (4 sole corners per planted foot: the feet's candidates are dealt
-    # round-robin, Model.reorder_points) + 8 joint-limit rows = the 32-row variant, which
-    # runs two envs per wave (H1 8192: 0.70 -> 0.38 ms per control step).  12 / 48 selects
-    # the one-env-per-wave 48-row kernels.
+    # 8 contact slots + 8 joint-limit rows = the 32-row variant, which runs two envs per
+    # wave (H1 8192: 0.70 -> 0.38 ms per control step).  Slot order (include/leggedsim.h):
+    # one slot per body on the ground first (a knee, hip or pelvis is never crowded out by
+    # the soles), then up to 4 self contacts, then further sole corners (the feet's
+    # candidates are dealt round-robin, Model.reorder_points: two planted soles share the
+    # rest evenly).  Limits beyond the 8 limit rows use the rows of unused contact slots.
     max_contacts = 8
     max_rows = 32
-    max_self_contacts = 2
+    max_self_contacts = 4
 
     def _init_buffers(self):
         super()._init_buffers()

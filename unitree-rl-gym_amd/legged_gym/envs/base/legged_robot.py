@@ -41,7 +41,7 @@ class LeggedRobot(BaseTask):
     hip_dof_indices = ()
     max_contacts = 8
     max_rows = 32
-    max_self_contacts = 2  # contact slots self contacts may take per substep (cfg.asset.self_collisions == 0)
+    max_self_contacts = 4  # contact slots self contacts may take per substep (cfg.asset.self_collisions == 0)
 
     def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
         self.cfg = cfg

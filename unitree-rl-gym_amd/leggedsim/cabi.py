@@ -19,6 +19,7 @@ MAX_OBS = 128
 MAX_REWARDS = 24
 MAX_SELF_PROXIES = 64
 MAX_SELF_PAIRS = 192
+NUM_CONTACT_STATS = 3  # lgs_get_contact_stats: bodies without a slot, self contacts without one, limits without a row
 
 OBS_QUADRUPED = 0
 OBS_HUMANOID = 1
@@ -236,4 +237,6 @@ def load_oracle(path=None):
     lib.orc_terrain_sample.restype = C.c_float
     lib.orc_set_self_collision.argtypes = [C.POINTER(SelfCollisionDesc)]
     lib.orc_set_self_collision.restype = None
+    lib.orc_contact_stats.argtypes = [vp, C.c_int]
+    lib.orc_contact_stats.restype = None
     return lib

@@ -70,6 +70,9 @@ def load():
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     lib.lgs_set_self_collision.argtypes = [vp, C.POINTER(cabi.SelfCollisionDesc)]
+    if hasattr(lib, "lgs_get_contact_stats"):  # (absent only from pre-round-4 builds used in A/B timing)
+        lib.lgs_get_contact_stats.argtypes = [vp, vp, C.c_int32]
+        lib.lgs_get_contact_stats.restype = C.c_int
     for name in ("lgs_get_body_name", "lgs_get_dof_name"):
         getattr(lib, name).argtypes = [vp, C.c_int32]
         getattr(lib, name).restype = C.c_char_p
@@ -99,6 +102,7 @@ EXPORTED_SYMBOLS = [
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
     "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
+    "lgs_get_contact_stats",
 ]
 
 
@@ -201,6 +205,16 @@ class Sim:
     def set_dof_indexed(self, src, ids_i32, n):
         check(self.lib, self.lib.lgs_set_dof_state_indexed(self.handle, src.data_ptr(), ids_i32.data_ptr(), n),
               "set_dof_state_indexed")
+
+    def contact_stats(self, reset=False):
+        """Capacity drops summed over envs and substeps (lgs_get_contact_stats): a dict of
+        touching bodies without a contact slot, self contacts without one, joint limits
+        without a row.  Synchronises the sim's stream."""
+        import numpy as np
+        out = np.zeros(cabi.NUM_CONTACT_STATS, dtype=np.uint64)
+        check(self.lib, self.lib.lgs_get_contact_stats(self.handle, out.ctypes.data, int(bool(reset))),
+              "lgs_get_contact_stats")
+        return {"bodies": int(out[0]), "self": int(out[1]), "limits": int(out[2])}
 
     # name queries (gym.get_asset_rigid_body_names / get_asset_dof_names /
     # find_actor_rigid_body_handle, legged_robot.py:342-343, 388-407)

@@ -21,7 +21,6 @@ Every parameter is a view of ONE flat fp32 buffer (each tensor starting on 16 by
 gradient a view of another (its 4-float tail: the loss statistics, all-reduced with it at
 world > 1), Adam's moments flat too -- as FusedPPOStep (fused_step.py).
 """
-import os
 
 import torch
 import torch.distributed as dist
@@ -37,17 +36,18 @@ def _pad4(n):
 
 def supported(ac, num_envs, num_mini_batches):
     """The policy shapes the fused recurrent step covers (else the autograd update runs)."""
-    if os.environ.get("PPO_FUSED_RECURRENT", "1") == "0":
-        return False
     if not getattr(ac, "is_recurrent", False) or not hasattr(ac, "memory_a") or num_envs % num_mini_batches:
         return False
     for seq in (ac.actor, ac.critic):
         if not isinstance(seq, nn.Sequential) or len(seq) != 3 or not isinstance(seq[0], nn.Linear) or \
                 not isinstance(seq[1], nn.ELU) or seq[1].alpha != 1.0 or not isinstance(seq[2], nn.Linear):
             return False
-        if seq[0].bias is None or seq[2].bias is None or seq[0].out_features > 32 or seq[0].out_features % 4 or \
+        # (pmlp_heads_forward / _backward take hidden widths N0 <= 32, a multiple of 8, and N1 <= 16)
+        if seq[0].bias is None or seq[2].bias is None or seq[0].out_features > 32 or seq[0].out_features % 8 or \
                 seq[2].out_features > 16:
             return False
+    if ac.memory_a.rnn.hidden_size != ac.memory_c.rnn.hidden_size:  # (one H per launch)
+        return False
     if ac.critic[2].out_features != 1:
         return False
     for m in (ac.memory_a, ac.memory_c):

@@ -24,7 +24,6 @@ state_dict keep their reference structure: the Parameters are the same objects
 of the flat moments.  With torch.distributed the gradient (and the statistics
 tail) is all-reduced as one bucket and averaged inside the kernels.
 """
-import os
 
 import torch
 import torch.distributed as dist
@@ -91,10 +90,6 @@ class FusedPPOStep:
         # the fp32 weights (construction, a checkpoint load, any update outside this path)
         # and are reconverted before their next use (ensure_weights)
         self.weights_changed = True
-        # weight gradients read the row-major activations through LDS-transposed MFMA
-        # operands (PARTIAL_TN), so no transposed copy is ever written; PMLP_TN=0 keeps
-        # the transposed copies and the k-contiguous PARTIAL GEMM (A/B comparisons)
-        self.tn = os.environ.get("PMLP_TN", "1") != "0"
         self.sync_optimizer_state(alg.optimizer)
         self._alloc()
 
@@ -104,15 +99,11 @@ class FusedPPOStep:
         L = len(self.lins[0])
         self.L = L
         self.k0p = [_ceil8(ls[0].in_features) for ls in self.lins]
-        tn = self.tn
-        # tn: row-major activations of exactly the layer's width (rows of 512 / 256 / 128
-        # features start on 128-byte lines); the weight-gradient GEMM forms the bias
-        # gradient as its A operand times ones (sum_col).  The transposed copies carry 8
-        # extra rows instead: a row of ones (then zeros) makes the GEMM's extra output
-        # column the bias gradient.
+        # row-major activations of exactly the layer's width (rows of 512 / 256 / 128 features
+        # start on 128-byte lines); the weight gradients read them through LDS-transposed MFMA
+        # operands (PARTIAL_TN: no transposed copy is ever written) and form the bias gradient
+        # as their A operand times ones (sum_col)
         self.xb = [torch.empty(M, k, dtype=bf, device=dev) for k in self.k0p]
-        self.xt = [None if tn else self._ones_row(torch.empty(k + 8, M, dtype=bf, device=dev), k)
-                   for k in self.k0p]
         # W[out, in] in bf16: the forward's B[N, K] and, unchanged, the input gradient's B[K, N]
         # (b_kn); the last layer's rows are padded to a multiple of 8 with zero rows (the input
         # gradient's K) -- no transposed copy
@@ -120,41 +111,32 @@ class FusedPPOStep:
                                 self.k0p[n] if l == 0 else lin.in_features, dtype=bf, device=dev)
                     for l, lin in enumerate(ls)] for n, ls in enumerate(self.lins)]
         # the whole forward of both nets in ONE launch (pmlp_mlp_forward: activations kept on
-        # chip between layers, bitwise the per-layer GEMMs); PMLP_FUSED_FWD=0: per-layer GEMMs
-        self.fused_fwd = os.environ.get("PMLP_FUSED_FWD", "1") != "0" and self.tn and \
-            all(mm.mlp_forward_supported(self.lins[n], self.k0p[n]) for n in range(2))
+        # chip between layers, bitwise the per-layer GEMMs) where its shapes allow; else per-layer GEMMs
+        self.fused_fwd = all(mm.mlp_forward_supported(self.lins[n], self.k0p[n]) for n in range(2))
         # its weight operands fragment-packed (include/ppo_mlp.h, pmlp_mirror_job.frag): one
-        # contiguous 1 KB per wave and k-step; PMLP_FRAG_W=0 reads the row-major wb instead
+        # contiguous 1 KB per wave and k-step
         self.wf = [[torch.zeros(-(-w.shape[0] // 32) * 32 * w.shape[1], dtype=bf, device=dev) for w in ws]
-                   for ws in self.wb] if self.fused_fwd and os.environ.get("PMLP_FRAG_W", "1") != "0" else None
+                   for ws in self.wb] if self.fused_fwd else None
         self.mirror = (mm.MirrorJob * (2 * len(self.lins[0])))(*[
             mm.MirrorJob(self._offset[id(lin.weight)], lin.out_features, lin.in_features, self.wb[n][l].shape[1],
                          self.wb[n][l].data_ptr(), self.wf[n][l].data_ptr() if self.wf else None)
             for n, ls in enumerate(self.lins) for l, lin in enumerate(ls)])
         self.y = [[torch.empty(M, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in self.lins]
-        self.yt = [[None if tn else
-                    self._ones_row(torch.empty(lin.out_features + 8, M, dtype=bf, device=dev), lin.out_features)
-                    for lin in ls[:-1]] for ls in self.lins]
         self.out = [torch.empty(M, ls[-1].out_features, device=dev) for ls in self.lins]
         A = self.lins[0][-1].out_features
         if self.lins[1][-1].out_features != 1:
             raise ValueError("fused PPO step: the critic must output one value")
         self.loss_partial = torch.empty(mm.load().pmlp_ppo_loss_step_parts(M, A), device=dev)
-        # output gradients (bf16, both layouts) and the hidden-layer input gradients
+        # output gradients (bf16) and the hidden-layer input gradients
         self.dz_out = [torch.empty(M, _ceil8(ls[-1].out_features), dtype=bf, device=dev) for ls in self.lins]
-        self.dzt_out = [None if tn else torch.empty(_ceil8(ls[-1].out_features), M, dtype=bf, device=dev)
-                        for ls in self.lins]
-        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 1 or (tn and l > 0) else None
+        self.dz = [[torch.empty(M, lin.in_features, dtype=bf, device=dev) if l > 0 else None
                     for l, lin in enumerate(ls)] for ls in self.lins]
-        self.dzt = [[torch.empty(lin.in_features, M, dtype=bf, device=dev) if l > 0 and not tn else None
-                     for l, lin in enumerate(ls)] for ls in self.lins]
         # split-K weight-gradient slabs; layers whose padded width differs from the
         # parameter's get a staging buffer (copied into the flat gradient)
         self.ks, self.slab, self.dw_stage = [], [], []
         for l in range(L):
             kps = [self.k0p[n] if l == 0 else self.lins[n][l].in_features for n in range(2)]
-            # (the bias column is the TN kernel's ones product, not an extra column tile;
-            # the transposed-copy path takes the same slabs, so the two agree bitwise)
+            # (the bias column is the TN kernel's ones product, not an extra column tile)
             ks = mm._ksplit(M, max(mm._tiles(self.lins[n][l].out_features, kps[n]) for n in range(2)),
                             slab_bytes=max(4 * self.lins[n][l].out_features * (kps[n] + 8) for n in range(2)))
             nsl = (M + ks - 1) // ks
@@ -168,16 +150,10 @@ class FusedPPOStep:
         # inside the slab-reduce launch (pmlp_reduce_slabs_step): two launches fewer per step.
         # The reduce jobs plus the std gradient must then be the whole gradient.
         covered = sum(lin.out_features * (lin.in_features + 1) for ls in self.lins for lin in ls) + A
-        self.fold_loss = 2 * L <= mm.MAX_JOBS and os.environ.get("PMLP_FOLD_OPT", "1") != "0"
+        self.fold_loss = 2 * L <= mm.MAX_JOBS
         self.fold_opt = self.fold_loss and covered == self.n and all(d is None for ds in self.dw_stage for d in ds)
         self.norm_partial = torch.empty(16384, device=dev) if self.fold_opt else None
         self.nparts = 0
-
-    @staticmethod
-    def _ones_row(t, k):
-        t[k:].zero_()
-        t[k].fill_(1.0)
-        return t
 
     # -------------------------------------------------------- optimizer state --
     def sync_optimizer_state(self, opt):
@@ -228,14 +204,7 @@ class FusedPPOStep:
         #    observations through `rows` and converts them on load, storing the bf16 rows
         #    (the first weight gradient's operand) on the way; the bf16 weights are current
         #    (the previous Adam step wrote them)
-        tn = self.tn
-        if not tn:
-            jobs = [(obs, self.k0p[0], None, self.xt[0], rows)]
-            if not shared:
-                jobs.append((cobs, self.k0p[1], None, self.xt[1], rows))
-            mm._convert(jobs)
         xb = [self.xb[0], self.xb[0] if shared else self.xb[1]]
-        xt = [self.xt[0], self.xt[0] if shared else self.xt[1]]
         fobs = [obs, cobs]
         # 2. forward
         if self.fused_fwd:
@@ -260,7 +229,7 @@ class FusedPPOStep:
                                    cf=self.out[n], **a))
                 else:
                     gj.append(dict(B=self.wb[n][l], M=M, N=lin.out_features, K=K, bias=lin.bias.detach(),
-                                   cb=self.y[n][l], ct=self.yt[n][l], **a))
+                                   cb=self.y[n][l], **a))
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
         # 3. loss forward + backward in one pass (rollout inputs read through `rows`); the
         #    output gradients land directly in the backward's bf16 operands
@@ -274,13 +243,12 @@ class FusedPPOStep:
                                       float(alg.entropy_coef), P(self.loss_partial),
                                       None if self.fold_loss else P(self.stats),
                                       None if self.fold_loss else P(self._gview[id(ac.std)]),
-                                      P(self.dz_out[0]), mm._p(self.dzt_out[0]),
-                                      self.dz_out[0].shape[1], P(self.dz_out[1]), mm._p(self.dzt_out[1]),
+                                      P(self.dz_out[0]), None, self.dz_out[0].shape[1], P(self.dz_out[1]), None,
                                       self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
         #    (dW_l beside dX_l on a second stream measured slower: the two latency-bound
         #    GEMMs contend)
-        dz, dzt = list(self.dz_out), list(self.dzt_out)
+        dz = list(self.dz_out)
         red, copies = [], []
         for l in range(L - 1, -1, -1):
             gj = []
@@ -288,28 +256,24 @@ class FusedPPOStep:
                 lin = self.lins[n][l]
                 kp = self.k0p[n] if l == 0 else lin.in_features
                 slab = self.slab[l][n]
-                if tn:  # A = dz [M, out], B = activations [M, kp + 8] (row-major)
-                    B = xb[n] if l == 0 else self.y[n][l - 1]
-                    gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab, sum_col=kp))
-                else:
-                    B = xt[n] if l == 0 else self.yt[n][l - 1]
-                    gj.append(dict(A=dzt[n], B=B, M=lin.out_features, N=kp + 8, K=M, cf=slab))
+                # A = dz [M, out], B = activations [M, kp] (row-major)
+                B = xb[n] if l == 0 else self.y[n][l - 1]
+                gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab, sum_col=kp))
                 dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
                 red.append((slab, dw, lin.out_features * (kp + 8), slab.shape[0], self._gview[id(lin.bias)],
                             kp + 8, kp))
                 if self.dw_stage[l][n] is not None:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
-            mm._gemm(mm.EPI_PARTIAL_TN if tn else mm.EPI_PARTIAL, gj, ksplit=self.ks[l])
+            mm._gemm(mm.EPI_PARTIAL_TN, gj, ksplit=self.ks[l])
             if l > 0:
                 gj = []
                 for n in range(2):
                     lin = self.lins[n][l]
                     # the input layer's gradient is only consumed transposed (its weight gradient)
                     gj.append(dict(A=dz[n], B=self.wb[n][l], b_kn=1, M=M, N=lin.in_features, K=dz[n].shape[1],
-                                   yprev=self.y[n][l - 1], cb=self.dz[n][l], ct=self.dzt[n][l]))
+                                   yprev=self.y[n][l - 1], cb=self.dz[n][l]))
                 mm._gemm(mm.EPI_BWD_DX, gj)
                 dz = [self.dz[n][l] for n in range(2)]
-                dzt = [self.dzt[n][l] for n in range(2)]
         adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
         dkl = float(alg.desired_kl if alg.desired_kl is not None else 0.0)
         fold_opt = self.fold_opt and alg.world_size == 1
@@ -317,10 +281,8 @@ class FusedPPOStep:
             rs = mm.ReduceStep(P(self.loss_partial), self.loss_partial.numel() // (3 + A), A, M,
                                float(alg.entropy_coef), P(std), P(self.stats), P(self._gview[id(ac.std)]),
                                P(self.norm_partial) if fold_opt else None, P(self.step_t), P(alg._lr), P(acc), dkl,
-                               adaptive, 0)
-            self.nparts = mm._reduce_step(red, rs)
-            if fold_opt and self.nparts > self.norm_partial.numel():
-                raise RuntimeError(f"fused PPO step: {self.nparts} norm partials > {self.norm_partial.numel()}")
+                               adaptive, self.norm_partial.numel() if fold_opt else 0)
+            self.nparts = mm._reduce_step(red, rs)  # (raises before launching if the partials do not fit)
         else:
             mm._reduce(red)
         for dst, srcv in copies:
@@ -452,10 +414,10 @@ class RecurrentRollout:
         from rsl_rl.algorithms import fused_recurrent
         # the memories' rollout step on the update's matrix-core kernel (pmlp_lstm_step_mfma)
         # when the update runs the fused recurrent step with it: the stored log-probabilities
-        # then come from the numbers the update recomputes (LSTM_MFMA_STEP=0: fp32 step kernel)
-        rnns = [getattr(getattr(ac, m, None), "rnn", None) for m in ("memory_a", "memory_c")]
-        self.mfma_step = os.environ.get("LSTM_MFMA_STEP", "1") != "0" and alg._rfused is not None and \
-            all(r is not None and lstm_seq.mfma_usable(r, torch.empty(1, r.input_size)) for r in rnns)
+        # then come from the numbers the update recomputes.  Gated on the update's own choice
+        # (FusedRecurrentStep.mfma, I + H + 1 <= 128), so both always use the same arithmetic.
+        rf = alg._rfused
+        self.mfma_step = rf is not None and all(rf.mfma)
         self.heads = None
         if fused_recurrent.supported(ac, self.N, 1) and ac.memory_a.rnn.hidden_size == ac.memory_c.rnn.hidden_size:
             dev = ac.std.device

@@ -129,7 +129,10 @@ class PPO:
         if self._fused_loss and self._dense_recurrent and self._rfused is None and \
                 fused_recurrent.supported(self.actor_critic, num_envs, self.num_mini_batches):
             # the recurrent optimizer step without autograd (algorithms/fused_recurrent.py)
-            self._rfused = fused_recurrent.FusedRecurrentStep(self, num_envs, num_transitions_per_env)
+            try:
+                self._rfused = fused_recurrent.FusedRecurrentStep(self, num_envs, num_transitions_per_env)
+            except ValueError:  # a shape the kernels do not take: the autograd update runs
+                self._rfused = None
         if self.actor_critic.is_recurrent and self._rollout is None and str(self.device).startswith("cuda") and \
                 hasattr(self.actor_critic, "rollout_capturable"):
             self._rollout = fused_step.RecurrentRollout(self, num_envs)

@@ -14,7 +14,6 @@ around pmlp_lstm_fwd / pmlp_lstm_bwd plus three GEMMs for the weight gradients);
 ``lstm_dense_reference`` is the same recurrence in plain torch ops (CPU, tests).
 """
 import ctypes as C
-import os
 
 import torch
 
@@ -61,13 +60,9 @@ def _ok(status, what):
 
 
 # The update's dense sequences on the matrix cores (pmlp_lstm_fwd_mfma / _bwd_mfma: bf16
-# products, fp32 state) for hidden 64 and inputs <= 64; LSTM_MFMA=0 keeps the fp32 kernels.
-# The rollout's step (lstm_step_) is always the fp32 kernel.
-MFMA = os.environ.get("LSTM_MFMA", "1") != "0"
-
-
+# products, fp32 state) for hidden 64 and inputs <= 64; other shapes take the fp32 kernels.
 def mfma_usable(rnn, x):
-    return MFMA and rnn.hidden_size == 64 and x.shape[-1] <= 64
+    return rnn.hidden_size == 64 and x.shape[-1] <= 64
 
 
 def usable(rnn, x):
@@ -81,7 +76,7 @@ def _gx(x, w_ih, b_ih, b_hh):
     return torch.addmm(b_ih + b_hh, x.reshape(T * B, I), w_ih.t()).view(T, B, w_ih.shape[0])
 
 
-_ROWS_CHUNK = int(os.environ.get("LSTM_ROWS_CHUNK", "1024"))  # (A/B knob)
+_ROWS_CHUNK = 1024
 
 
 def _rows_tn(g, x, chunk=None):

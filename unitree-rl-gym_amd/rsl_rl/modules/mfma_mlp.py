@@ -296,8 +296,8 @@ def _tiles(M, N):
 
 # ~128 workgroups per weight-gradient job: fewer slabs than 256 cut the slab combine
 # 16.8 -> 11.6 us per optimizer step at equal GEMM time
-_KS_TARGET = int(os.environ.get("PMLP_KSPLIT_TARGET", "128"))  # (A/B knobs of the split-K heuristic)
-_KS_BUDGET = int(os.environ.get("PMLP_KSPLIT_BUDGET_MB", "12")) << 20
+_KS_TARGET = 128
+_KS_BUDGET = 12 << 20  # slab bytes per job
 
 
 def _ksplit(batch, tiles, slab_bytes=0, target_blocks=None, min_rows=256, budget=None):

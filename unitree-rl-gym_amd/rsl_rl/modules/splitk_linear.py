@@ -6,14 +6,13 @@ dW = dY^T X puts the whole 24576-long reduction on a handful of output tiles
 batched GEMM with chunks x tiles workgroups plus a small reduction.  Same
 parameters and state_dict keys as nn.Linear (checkpoints interchange).
 """
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 SPLIT_MIN_ROWS = 8192
-CHUNK = int(os.environ.get("SPLITK_CHUNK", "512"))  # (A/B knob: 4096 -> 512 cut 1 ms off an H1 update)
+CHUNK = 512  # rows per split-K chunk (4096 -> 512 cut 1 ms off an H1 update)
 
 
 class _SplitKLinearFn(torch.autograd.Function):
