@@ -221,6 +221,10 @@ typedef struct lgs_task_params {
      * fills; they join the reset-time extras like the native sums. */
     int32_t defer_reward_total;
     int32_t num_extra_sums;
+    /* with write_body_states: the bodies whose rigid_body_states rows each step refreshes (bit b =
+     * body b; the humanoid tasks: their feet, the only rows h1_env.py:34-52 reads); 0 = every body.
+     * lgs_forward_kinematics (refresh_rigid_body_state_tensor) always refreshes every body. */
+    uint32_t body_state_mask;
 } lgs_task_params;
 
 /* ---- per-env buffers of the VecEnv (device pointers; torch owns them) ---- */

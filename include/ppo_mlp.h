@@ -285,6 +285,38 @@ typedef struct {
 } pmlp_mlp_fwd_job;
 PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream);
 
+/* One env step's policy work of the fused rollout in the forward launch (pmlp_mlp_forward
+ * of job 0 = the actor [N, A] means and job 1 = the critic [N, 1] values, N = M envs):
+ *  - PPO.act + RolloutStorage.add_transitions (pmlp_act's arithmetic): a ~ N(mu, std) with
+ *    Philox draw counter draw[parity], log-prob, and the storage rows (actions, log-prob, mu,
+ *    sigma, value, observations); then draw[parity ^ 1] = draw[parity] + 1 (the next step
+ *    reads that one: the counters alternate with the step parity, so no launch reads and
+ *    advances the same counter);
+ *  - optionally the PREVIOUS env step's PPO.process_env_step (pmlp_store_step without the
+ *    draw advance), deferred into this launch: st_rewards = rewards + gamma * (prev_value *
+ *    time_outs), st_dones = dones (rewards == NULL: none).  The caller issues the last step's
+ *    with pmlp_store_step (draw = NULL) before anything reads the storage.
+ * One launch per env step instead of three (forward, pmlp_act, pmlp_store_step).          */
+typedef struct {
+    const float* stdv;                  /* [A]                                              */
+    const float* obs;                   /* [N, O] (storage observations)                    */
+    const float* cobs;                  /* [N, CO] or NULL (no privileged storage)          */
+    int32_t O, CO, A;                   /* A <= 16                                          */
+    float *actions_out, *st_actions, *st_logp, *st_mu, *st_sigma, *st_value, *st_obs, *st_cobs;
+    int64_t* draw;                      /* [2]                                              */
+    int32_t parity;
+    uint64_t seed;
+    const float* rewards;               /* deferred store of the previous step, or NULL     */
+    const uint8_t* dones;
+    const uint8_t* time_outs;           /* or NULL: no bootstrap                            */
+    const float* prev_value;
+    float* st_rewards;
+    uint8_t* st_dones;
+    float gamma;
+} pmlp_rollout_step;
+PMLP_API int pmlp_rollout_forward(const pmlp_mlp_fwd_job* jobs, int32_t N, const pmlp_rollout_step* rs,
+                                  void* stream);
+
 /* ---- recurrent heads (the fused recurrent optimizer step, rsl_rl/algorithms/fused_recurrent.py):
  * the MLP heads of ActorCriticRecurrent on the LSTM output h [M, H] (rsl_rl
  * actor_critic_recurrent.py: the actor / critic Sequential(Linear(H, N0), ELU, Linear(N0, N1))),

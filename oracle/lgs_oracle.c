@@ -1223,6 +1223,15 @@ void orc_simulate(const lgs_model_desc* md, const lgs_sim_params* sp, int N, flo
     }
 }
 
+/* the step's rigid_body_states refresh: the bodies of T->body_state_mask (0: every body) */
+static void step_body_states(const lgs_model_desc* md, const lgs_task_params* T, const float* root13,
+                             const float* dofs, float* rbs) {
+    float tmp[LGS_MAX_BODIES * 13];
+    orc_body_states_env(md, root13, dofs, tmp);
+    for (int b = 0; b < md->num_bodies; ++b)
+        if (!T->body_state_mask || ((T->body_state_mask >> b) & 1u)) memcpy(rbs + 13 * b, tmp + 13 * b, 13 * sizeof(float));
+}
+
 /* the fused control step (LeggedRobot.step, legged_robot.py:615-647) for all envs */
 void orc_step(const lgs_model_desc* md, const lgs_sim_params* sp, const lgs_task_params* T, int N, float* root,
               float* dofs, float* cforce, float* rbs, const float* added_mass, const float* friction,
@@ -1237,7 +1246,7 @@ void orc_step(const lgs_model_desc* md, const lgs_sim_params* sp, const lgs_task
             orc_substep_env(md, sp, root + 13 * e, dofs + 2 * D * e, E->torques + D * e, cforce + 3 * B * e,
                             added_mass ? added_mass[e] : 0.f, friction ? friction[e] : 1.f);
         }
-        if (rbs && T->write_body_states) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
+        if (rbs && T->write_body_states) step_body_states(md, T, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
         ostate st = {root, dofs, cforce, T->write_body_states ? rbs : NULL};
         orc_post_physics_env(md, T, N, e, &st, E, step_counter);
     }
@@ -1258,7 +1267,7 @@ void orc_step_physics(const lgs_model_desc* md, const lgs_sim_params* sp, const 
             orc_substep_env(md, sp, root + 13 * e, dofs + 2 * D * e, E->torques + D * e, cforce + 3 * B * e,
                             added_mass ? added_mass[e] : 0.f, friction ? friction[e] : 1.f);
         }
-        if (rbs && T->write_body_states) orc_body_states_env(md, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
+        if (rbs && T->write_body_states) step_body_states(md, T, root + 13 * e, dofs + 2 * D * e, rbs + 13 * B * e);
     }
 }
 

@@ -179,7 +179,8 @@ def test_fused_rollout_act_and_store_match_reference_semantics():
     """PPO.act / process_env_step through FusedRollout: actions ~ N(mu, std) (sample
     moments), log-prob, mean, sigma, value and observations in the storage row exactly
     as the reference computes them from the same policy outputs; the time-out bootstrap
-    bitwise as the torch statement; fresh noise every step."""
+    bitwise as the torch statement (deferred into the next act's launch, the last one
+    flushed before the storage is read); fresh noise every step."""
     from torch.distributions import Normal
     torch.manual_seed(0)
     N, T, O, A = 4096, 4, 48, 12
@@ -214,11 +215,16 @@ def test_fused_rollout_act_and_store_match_reference_semantics():
             rew = torch.randn(N, device="cuda", generator=g)
             done = torch.rand(N, device="cuda", generator=g) < 0.1
             tout = done & (torch.rand(N, device="cuda", generator=g) < 0.5)
+            if t > 0:  # the previous step's store rode in this act's launch
+                assert torch.equal(st.rewards[t - 1].squeeze(1), refs[-1][0])
+                assert torch.equal(st.dones[t - 1].squeeze(1), refs[-1][1])
             alg.process_env_step(rew, done, {"time_outs": tout})
             ref = rew.clone()
-            ref += alg.gamma * torch.squeeze(value * tout.unsqueeze(1), 1)
-            assert torch.equal(st.rewards[t].squeeze(1), ref)
-            assert torch.equal(st.dones[t].squeeze(1), done)
+            ref += alg.gamma * torch.squeeze(value.clone() * tout.unsqueeze(1), 1)
+            refs = [(ref, done.clone())]
+    alg.flush_rollout()
+    assert torch.equal(st.rewards[T - 1].squeeze(1), refs[-1][0])
+    assert torch.equal(st.dones[T - 1].squeeze(1), refs[-1][1])
     assert st.step == T
     with pytest.raises(AssertionError):
         alg.act(obs, obs)

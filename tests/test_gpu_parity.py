@@ -427,3 +427,33 @@ def test_other_robot_shape_registers_and_matches_oracle_bitwise(n):
     assert env.num_dof == 23 and env.num_bodies == 24 and env.obs_buf.shape == (n, 80)
     assert env.sim.find_body("torso_link") == env.model.body_names.index("torso_link")
     fused_vs_oracle(env, g, 2, f"g1_23dof x{n}")
+
+
+@pytest.mark.parametrize("task", ["h1", "g1"])
+def test_step_refreshes_the_feet_rows_and_gym_refresh_every_body(task):
+    """The humanoid step refreshes the rigid_body_states rows its task reads (the feet,
+    h1_env.py:34-52: lgs_task_params.body_state_mask); the other rows stay as they were.
+    gym.refresh_rigid_body_state_tensor (lgs_forward_kinematics) then refreshes every row,
+    equal to the oracle's forward kinematics of the same state."""
+    import ctypes as C
+    env, g = warm(task, 64, steps=5)
+    B = env.num_bodies
+    feet = env.feet_indices.cpu().numpy()
+    other = np.setdiff1d(np.arange(B), feet)
+    env.rigid_body_states.fill_(7.0)
+    env.step(0.5 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
+    rbs = env.rigid_body_states.view(env.num_envs, B, 13).cpu().numpy()
+    assert (rbs[:, other] == 7.0).all() and not (rbs[:, feet] == 7.0).any()
+    feet_rows = rbs[:, feet].copy()
+    env.gym.refresh_rigid_body_state_tensor(env.sim)
+    rbs = env.rigid_body_states.view(env.num_envs, B, 13).cpu().numpy()
+    np.testing.assert_array_equal(rbs[:, feet], feet_rows)
+    lib = bridge.ensure_built()
+    mh = cabi.ModelHandle(env.model)
+    root = env.root_states.cpu().numpy()
+    dofs = env.dof_state.cpu().numpy().reshape(env.num_envs, -1)
+    want = np.zeros((env.num_envs, B, 13), np.float32)
+    for e in range(env.num_envs):
+        r, d = np.ascontiguousarray(root[e]), np.ascontiguousarray(dofs[e])
+        lib.orc_body_states_env(C.byref(mh.desc), r.ctypes.data, d.ctypes.data, want[e].ctypes.data)
+    np.testing.assert_array_equal(rbs, want)

@@ -1505,9 +1505,9 @@ __device__ __forceinline__ int xcd_env(int b, int nwg) {
 
 // rigid body states [B][13] of the block's env into global memory
 template <int D, int B, int ROWS, int EPW>
-__device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, float* rbs_out) {
+__device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, float* rbs_out, unsigned mask = 0u) {
     const int lane = hl<EPW>();
-    if (lane < B) {
+    if (lane < B && (!mask || ((mask >> lane) & 1u))) {  // mask: the rows the task reads (0: all)
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
         quat_to_mat(s.root + 3, R);
         p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
@@ -2057,7 +2057,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
         }
         STAMP(0);
         if (lane < D) E.torques[D * e + lane] = s.tau[lane];
-        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs);  // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only
+        // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only: the rows they read
+        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs, T.body_state_mask);
     } else {  // the physics half's outputs, as it stored them
         if (lane < A) s.act[lane] = E.actions[A * e + lane];
         if (lane < D) s.tau[lane] = E.torques[D * e + lane];
@@ -2254,7 +2255,8 @@ static int variant_chain(Variant v) {
 template <int D, int B>
 static void ex_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
                     lgs_env_buffers E, int N, uint32_t step, int mode) {
-    hipLaunchKernelGGL((k_step<D, B, 48, 0, 1, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, tp, E, N, step, mode);
+    // (2 waves/SIMD: the 29-row dense factorisation does not fit the 48-row default's 168 VGPRs)
+    hipLaunchKernelGGL((k_step<D, B, 48, 0, 1, 2>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, tp, E, N, step, mode);
 }
 template <int D, int B>
 static void ex_simulate(const lgs_sim* s, DevModel md, DevSim sp, DevState st, int N) {

@@ -1544,6 +1544,20 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
     }
 }
 
+// Philox4x32-10 (the rollout's policy noise: k_act, k_act4 and the rollout forward)
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)x + 0.5f) * 2.3283064365386963e-10f; }
+
 // ------------------------------------------------------------ fused MLP forward --
 // The whole forward of a 4-layer Linear/ELU MLP (rsl_rl's actor or critic: K0 -> H0 ->
 // H1 -> H2 -> N3) in ONE launch: a workgroup of 8 waves owns R mini-batch rows and keeps
@@ -1720,8 +1734,89 @@ extern "C" int pmlp_diag_fmlp_stamps(unsigned long long* host, int n) {
 #define FMLP_STAMP(k) ((void)(k))
 #endif
 
+// pmlp_rollout_step (include/ppo_mlp.h)
+struct RollStep {
+    const float* stdv;
+    const float* obs;
+    const float* cobs;
+    int O, CO, A;
+    float *actions_out, *st_actions, *st_logp, *st_mu, *st_sigma, *st_value, *st_obs, *st_cobs;
+    int64_t* draw;
+    int parity;
+    uint64_t seed;
+    const float* rew;
+    const uint8_t* dones;
+    const uint8_t* time_outs;
+    const float* prev_value;
+    float* st_rew;
+    uint8_t* st_dones;
+    float gamma;
+};
+
+// The rollout's work on the workgroup's R rows after job jj's forward (its outputs are in
+// J.out, written by this workgroup before the barrier that precedes this call).  Job 0 (the
+// actor): sampling and the storage rows, k_act4's Philox counters and arithmetic; the
+// deferred store of the previous step.  Job 1 (the critic): the value and privileged rows.
 template <int R>
-__global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) {
+__device__ void roll_epilogue(const FmlpJob& J, int jj, const RollStep& rs, int r0, int M, float* terms) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x;
+    if (jj == 0) {
+        const uint32_t draw = (uint32_t)rs.draw[rs.parity];
+        const uint2 key = make_uint2((uint32_t)rs.seed, (uint32_t)(rs.seed >> 32));
+        for (int q = tid; q < R * 4; q += FMLP_THREADS) {  // (row, action quad)
+            const int rl = q >> 2, c = q & 3, k0 = 4 * c, i = r0 + rl;
+            if (i >= M || k0 >= rs.A) continue;
+            const uint4 r = philox4x32(make_uint4(draw, (uint32_t)i, (uint32_t)c, 0x5050u), key);
+            const float rad0 = sqrtf(-2.f * logf(u01(r.x))), rad1 = sqrtf(-2.f * logf(u01(r.z)));
+            float z[4];
+            sincospif(2.f * u01(r.y), &z[1], &z[0]);
+            sincospif(2.f * u01(r.w), &z[3], &z[2]);
+            z[0] *= rad0; z[1] *= rad0; z[2] *= rad1; z[3] *= rad1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u;
+                if (k >= rs.A) break;
+                const size_t o = (size_t)i * rs.A + k;
+                const float sg = rs.stdv[k], mu = J.out[(size_t)i * J.ldo + k];
+                const float act = mu + sg * z[u];
+                const float d = act - mu;
+                terms[rl * 16 + k] = -(d * d) / (2.f * sg * sg) - logf(sg) - kHalfLog2Pi;
+                rs.actions_out[o] = act;
+                rs.st_actions[o] = act;
+                rs.st_mu[o] = mu;
+                rs.st_sigma[o] = sg;
+            }
+        }
+        __syncthreads();
+        if (tid < R && r0 + tid < M) {
+            const int i = r0 + tid;
+            float logp = 0.f;
+            for (int k = 0; k < rs.A; ++k) logp += terms[tid * 16 + k];
+            rs.st_logp[i] = logp;
+            if (rs.rew) {  // the previous step's process_env_step (k_store_step's arithmetic)
+                float rw = rs.rew[i];
+                if (rs.time_outs) rw = rw + rs.gamma * (rs.prev_value[i] * (rs.time_outs[i] ? 1.f : 0.f));
+                rs.st_rew[i] = rw;
+                rs.st_dones[i] = rs.dones[i] ? 1 : 0;
+            }
+        }
+        const int nrow = min(R, M - r0);
+        for (int q = tid; q < nrow * rs.O; q += FMLP_THREADS)
+            rs.st_obs[(size_t)r0 * rs.O + q] = rs.obs[(size_t)r0 * rs.O + q];
+        if (blockIdx.x == 0 && tid == 0) rs.draw[rs.parity ^ 1] = (int64_t)draw + 1;
+    } else {
+        if (tid < R && r0 + tid < M) rs.st_value[r0 + tid] = J.out[(size_t)(r0 + tid) * J.ldo];
+        if (rs.st_cobs) {
+            const int nrow = min(R, M - r0);
+            for (int q = tid; q < nrow * rs.CO; q += FMLP_THREADS)
+                rs.st_cobs[(size_t)r0 * rs.CO + q] = rs.cobs[(size_t)r0 * rs.CO + q];
+        }
+    }
+}
+
+template <int R, bool ROLL = false>
+__global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M, RollStep rs) {
     // y0 (then y2) and x (then y1); row strides 8 elements past the width: ds_read_b128
     // fragment reads of 32 consecutive rows hit 4-bank groups 4 apart (conflict-free)
     constexpr int LD0 = FMLP_MAX_H0 + 8, LD1 = FMLP_MAX_H1 + 8;
@@ -1785,6 +1880,7 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M) 
         fmlp_layer<R, true>(Y0, LD0, J.N[2], J.W[3], J.Wf[3], J.b[3], J.N[3], nullptr, 0, J.out, J.ldo, r0, M);
         __syncthreads();  // (the next job restages x over y1)
         FMLP_STAMP(sb + 8);
+        if constexpr (ROLL) roll_epilogue<R>(J, jj, rs, r0, M, (float*)Y1);  // (one job per workgroup)
     }
 }
 
@@ -1868,18 +1964,6 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adv_norm(float* __restrict
 // PPO.act tail + RolloutStorage.add_transitions (rsl_rl v1.0.2) for the
 // Gaussian MLP policy, and PPO.process_env_step's reward bootstrap + store.
 // Policy noise: Philox4x32-10 keyed (seed; draw, row, pair) -> Box-Muller.
-__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
-__device__ __forceinline__ float u01(uint32_t x) { return ((float)x + 0.5f) * 2.3283064365386963e-10f; }
 
 struct ActArgs {
     const float *mu, *stdv, *value, *obs, *cobs;
@@ -2468,9 +2552,10 @@ PMLP_API int pmlp_adv_normalize(float* advantages, int64_t n, const double* mome
     return 0;
 }
 
-PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream) {
+// the jobs' shape checks, then their kernel form
+static int fmlp_pack(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, FmlpJobs& fj) {
     if (njobs <= 0 || njobs > 2 || !jobs || M <= 0) return fail(-1, "pmlp_mlp_forward: 1..2 jobs, M > 0");
-    FmlpJobs fj{};
+    fj = FmlpJobs{};
     fj.njobs = njobs;
     for (int i = 0; i < njobs; ++i) {
         const pmlp_mlp_fwd_job& J = jobs[i];
@@ -2498,14 +2583,41 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
         for (int l = 0; l < 3; ++l) { f.y[l] = (bf16*)J.y[l]; f.ldy[l] = J.ldy[l]; }
         f.out = J.out; f.ldo = J.ldo;
     }
+    return 0;
+}
+
+PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32_t M, void* stream) {
+    FmlpJobs fj;
+    if (int e = fmlp_pack(njobs, jobs, M, fj)) return e;
     // rows per workgroup: 96 (one 150 KB workgroup per CU, every job in turn) for the update's
     // mini-batches; 32 with one job per workgroup for the rollout's num_envs rows
     hipStream_t st = (hipStream_t)stream;
+    const RollStep none{};
     if (M >= 96 * 192)
-        hipLaunchKernelGGL(k_mlp_fwd<96>, dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0, st, fj, M);
+        hipLaunchKernelGGL((k_mlp_fwd<96>), dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0, st, fj, M, none);
     else
-        hipLaunchKernelGGL(k_mlp_fwd<32>, dim3((M + 31) / 32, njobs), dim3(FMLP_THREADS), 0, st, fj, M);
+        hipLaunchKernelGGL((k_mlp_fwd<32>), dim3((M + 31) / 32, njobs), dim3(FMLP_THREADS), 0, st, fj, M, none);
     PMLP_CHECK_LAUNCH("pmlp_mlp_forward");
+    return 0;
+}
+
+PMLP_API int pmlp_rollout_forward(const pmlp_mlp_fwd_job* jobs, int32_t N, const pmlp_rollout_step* r, void* stream) {
+    if (!r || !r->stdv || !r->obs || r->O <= 0 || r->A <= 0 || r->A > 16 || (r->cobs && r->CO <= 0) || !r->draw ||
+        (r->parity & ~1) || !r->actions_out || !r->st_actions || !r->st_logp || !r->st_mu || !r->st_sigma ||
+        !r->st_value || !r->st_obs || (r->cobs && !r->st_cobs) ||
+        (r->rewards && (!r->dones || !r->prev_value || !r->st_rewards || !r->st_dones)))
+        return fail(-1, "pmlp_rollout_forward: bad rollout step arguments");
+    if (!jobs || N <= 0 || jobs[0].N[3] != r->A || jobs[1].N[3] != 1)
+        return fail(-1, "pmlp_rollout_forward: job 0 = actor [N, A], job 1 = critic [N, 1]");
+    // the forward's own checks; then the 32-row form, one job per workgroup (the epilogue's layout)
+    FmlpJobs fj;
+    if (int e = fmlp_pack(2, jobs, N, fj)) return e;
+    const RollStep rs{r->stdv, r->obs, r->cobs, r->O, r->CO, r->A, r->actions_out, r->st_actions, r->st_logp,
+                      r->st_mu, r->st_sigma, r->st_value, r->st_obs, r->st_cobs, r->draw, r->parity, r->seed,
+                      r->rewards, r->dones, r->time_outs, r->prev_value, r->st_rewards, r->st_dones, r->gamma};
+    hipLaunchKernelGGL((k_mlp_fwd<32, true>), dim3((N + 31) / 32, 2), dim3(FMLP_THREADS), 0, (hipStream_t)stream,
+                       fj, N, rs);
+    PMLP_CHECK_LAUNCH("pmlp_rollout_forward");
     return 0;
 }
 

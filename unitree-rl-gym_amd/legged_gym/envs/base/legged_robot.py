@@ -36,8 +36,35 @@ from .env_spec import derive_env_spec
 from .legged_robot_config import LeggedRobotCfg
 
 
+class _GymTensorAPI:
+    """The gym tensor refreshes a task's own methods call (legged_robot.py:639, 678-679;
+    h1_env.py:37, 49).  The step writes the bound tensors in place, so the refreshes are
+    no-ops, except the rigid body states: the step refreshes only the rows the task reads
+    (lgs_task_params.body_state_mask: the humanoids' feet), and
+    refresh_rigid_body_state_tensor refreshes every body (lgs_forward_kinematics)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    def refresh_dof_state_tensor(self, sim):
+        pass
+
+    def refresh_actor_root_state_tensor(self, sim):
+        pass
+
+    def refresh_net_contact_force_tensor(self, sim):
+        pass
+
+    def refresh_rigid_body_state_tensor(self, sim):
+        self._env._sync_stream()
+        self._env.sim.forward_kinematics()
+
+
 class LeggedRobot(BaseTask):
     obs_layout = cabi.OBS_QUADRUPED
+    # rigid_body_states rows each step refreshes when the task reads them: "feet" (all the
+    # reference's envs read) or "all"; self.gym.refresh_rigid_body_state_tensor refreshes all
+    rigid_body_state_bodies = "feet"
     hip_dof_indices = ()
     max_contacts = 8
     max_rows = 32
@@ -46,6 +73,7 @@ class LeggedRobot(BaseTask):
     def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
         self.cfg = cfg
         self.sim_params = sim_params
+        self.gym = _GymTensorAPI(self)
         self.height_samples = None
         self.debug_viz = False
         self.init_done = False

@@ -115,6 +115,7 @@ class TaskParams(C.Structure):
         ("write_body_states", C.c_int32),
         ("custom_origins", C.c_int32),
         ("defer_reward_total", C.c_int32), ("num_extra_sums", C.c_int32),
+        ("body_state_mask", C.c_uint32),
     ]
 
 

@@ -106,5 +106,11 @@ def build_task_params(env) -> cabi.TaskParams:
     rank = int(os.environ.get("RANK", "0"))
     T.seed = (seed & 0xFFFFFFFF) | (rank << 32)
     T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)))
+    # the rows the step refreshes: the feet (all the reference's humanoid envs read, h1_env.py:34-52)
+    # unless the task asks for every body (rigid_body_state_bodies = "all")
+    if getattr(env, "rigid_body_state_bodies", "feet") == "all":
+        T.body_state_mask = 0
+    else:
+        T.body_state_mask = sum(1 << b for b in fi) if fi else 0
     T.custom_origins = int(bool(getattr(env, "custom_origins", False)))
     return T

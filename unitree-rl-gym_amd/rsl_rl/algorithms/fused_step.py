@@ -325,8 +325,13 @@ class FusedRollout:
         self.y = [[torch.empty(N, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in lins]
         self.out = [torch.empty(N, ls[-1].out_features, device=dev) for ls in lins]
         self.actions = torch.empty(N, lins[0][-1].out_features, device=dev)
-        self.draw = torch.zeros((), dtype=torch.int64, device=dev)
+        # policy-noise draw counters: the act at storage step t samples with draw[t % 2] and
+        # sets draw[(t + 1) % 2] (pmlp_rollout_forward), so the forward launch both draws and
+        # advances without racing itself
+        self.draw = torch.zeros(2, dtype=torch.int64, device=dev)
         self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        # the last process_env_step's store, deferred into the next act's launch (or flush())
+        self.pending = None
 
     def usable(self, obs, cobs, storage):
         ok = lambda t, w: (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and  # noqa: E731
@@ -367,24 +372,61 @@ class FusedRollout:
         return self.out
 
     def act(self, obs, cobs, storage, t):
+        """PPO.act + add_transitions for storage step t, and the previous step's deferred
+        process_env_step, in the forward's launch (pmlp_rollout_forward): one launch per env
+        step where the forward, pmlp_act and pmlp_store_step were three."""
         f, N = self.f, self.N
-        self.forward(obs, cobs, t)
         A = self.actions.shape[1]
         priv = storage.privileged_observations
         P = mm._p
-        mm._ok(mm.load().pmlp_act(P(self.out[0]), P(f.ac.std.detach()), P(self.out[1]), P(obs),
-                                  P(cobs) if priv is not None else None, N, A, obs.shape[1],
-                                  cobs.shape[1] if priv is not None else 0, P(self.draw), self.seed, P(self.actions),
-                                  P(storage.actions[t]), P(storage.actions_log_prob[t]), P(storage.mu[t]),
-                                  P(storage.sigma[t]), P(storage.values[t]), P(storage.observations[t]),
-                                  P(priv[t]) if priv is not None else None, mm._stream()), "pmlp_act")
+        if not f.fused_fwd:  # per-layer GEMMs, then the separate sampling launch
+            self.flush(storage)
+            self.forward(obs, cobs, t)
+            mm._ok(mm.load().pmlp_act(P(self.out[0]), P(f.ac.std.detach()), P(self.out[1]), P(obs),
+                                      P(cobs) if priv is not None else None, N, A, obs.shape[1],
+                                      cobs.shape[1] if priv is not None else 0, P(self.draw[t % 2:]), self.seed,
+                                      P(self.actions), P(storage.actions[t]), P(storage.actions_log_prob[t]),
+                                      P(storage.mu[t]), P(storage.sigma[t]), P(storage.values[t]),
+                                      P(storage.observations[t]), P(priv[t]) if priv is not None else None,
+                                      mm._stream()), "pmlp_act")
+            self.draw[(t + 1) % 2].copy_(self.draw[t % 2] + 1)
+            return self.actions
+        f.ensure_weights()
+        pend = self.pending
+        self.pending = None
+        rs = mm.RolloutStep(P(f.ac.std.detach()), P(obs), P(cobs) if priv is not None else None, obs.shape[1],
+                            cobs.shape[1] if priv is not None else 0, A, P(self.actions), P(storage.actions[t]),
+                            P(storage.actions_log_prob[t]), P(storage.mu[t]), P(storage.sigma[t]),
+                            P(storage.values[t]), P(storage.observations[t]), P(priv[t]) if priv is not None else None,
+                            P(self.draw), t % 2, self.seed)
+        if pend is not None:
+            rew, dones, tout, tp, gamma = pend
+            rs.rewards, rs.dones, rs.time_outs = P(rew), P(dones), P(tout)
+            rs.prev_value, rs.st_rewards, rs.st_dones = P(storage.values[tp]), P(storage.rewards[tp]), P(storage.dones[tp])
+            rs.gamma = float(gamma)
+        xs = [obs, cobs]
+        mm.mlp_forward([dict(x=xs[n], kx=f.lins[n][0].in_features, K0=f.k0p[n], W=f.wb[n],
+                             Wf=f.wf[n] if f.wf else None, b=[lin.bias.detach() for lin in f.lins[n]],
+                             N=[lin.out_features for lin in f.lins[n]], out=self.out[n]) for n in range(2)], N,
+                       rollout=rs)
         return self.actions
 
     def store(self, rewards, dones, time_outs, storage, t, gamma):
+        """PPO.process_env_step: deferred into the next act's launch; flush() issues it alone
+        (the buffers are the env's: rewards is overwritten by the next env.step, which runs
+        after that launch)."""
+        self.pending = (rewards, dones, time_outs, t, gamma)
+
+    def flush(self, storage):
+        """Issue a deferred process_env_step on its own (before the storage is read)."""
+        if self.pending is None:
+            return
+        rewards, dones, time_outs, t, gamma = self.pending
+        self.pending = None
         P = mm._p
         mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
                                          P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
-                                         P(self.draw), mm._stream()), "pmlp_store_step")
+                                         None, mm._stream()), "pmlp_store_step")
 
     @staticmethod
     def storable(rewards, dones, time_outs, N):

@@ -203,7 +203,13 @@ class PPO:
         var = (s[1] - s[2] * mean * mean) / (s[2] - 1.0)
         return mean, torch.sqrt(var.clamp(min=0.0))
 
+    def flush_rollout(self):
+        """The fused rollout's deferred process_env_step, before anything reads the storage."""
+        if self._rollout is not None and hasattr(self._rollout, "flush"):
+            self._rollout.flush(self.storage)
+
     def compute_returns(self, last_critic_obs):
+        self.flush_rollout()
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         if self._fused is not None or (str(self.device).startswith("cuda") and last_values.is_cuda):
             # GAE + normalisation: two launches (+ a moments all-reduce across ranks)
@@ -393,6 +399,7 @@ class PPO:
         self.actor_critic.distribution = None
 
     def update(self):
+        self.flush_rollout()
         num_updates = self.num_learning_epochs * self.num_mini_batches
         self._graph_calls += 1
         if self._fused is not None:

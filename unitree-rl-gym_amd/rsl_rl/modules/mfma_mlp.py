@@ -75,6 +75,17 @@ class MlpFwdJob(C.Structure):
                 ("ldo", C.c_int32), ("Wf", C.c_void_p * 4)]
 
 
+class RolloutStep(C.Structure):
+    """include/ppo_mlp.h pmlp_rollout_step (pmlp_rollout_forward)."""
+    _fields_ = [("stdv", C.c_void_p), ("obs", C.c_void_p), ("cobs", C.c_void_p), ("O", C.c_int32),
+                ("CO", C.c_int32), ("A", C.c_int32)] + \
+        [(n, C.c_void_p) for n in ("actions_out", "st_actions", "st_logp", "st_mu", "st_sigma", "st_value",
+                                   "st_obs", "st_cobs", "draw")] + \
+        [("parity", C.c_int32), ("seed", C.c_uint64)] + \
+        [(n, C.c_void_p) for n in ("rewards", "dones", "time_outs", "prev_value", "st_rewards", "st_dones")] + \
+        [("gamma", C.c_float)]
+
+
 class HeadJob(C.Structure):
     _fields_ = [("h", C.c_void_p), ("W0", C.c_void_p), ("b0", C.c_void_p), ("W1", C.c_void_p), ("b1", C.c_void_p),
                 ("y0", C.c_void_p), ("out", C.c_void_p), ("dout", C.c_void_p), ("dh", C.c_void_p),
@@ -126,6 +137,7 @@ def load():
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
+        L.pmlp_rollout_forward.argtypes = [C.POINTER(MlpFwdJob), i32, C.POINTER(RolloutStep), vp]
         L.pmlp_ppo_loss_step_f32.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
         L.pmlp_heads_blocks.argtypes = [i32]
         L.pmlp_heads_blocks.restype = i32
@@ -188,11 +200,12 @@ def frag_pack(w, rows32):
     return p.view(rows32 // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).reshape(-1)
 
 
-def mlp_forward(nets, M):
+def mlp_forward(nets, M, rollout=None):
     """One launch of the whole forward of up to two 4-layer MLPs (pmlp_mlp_forward).  nets:
     dicts x (fp32 [*, ldx]), kx, rows (int64 [M] | None), xa (bf16 [M, K0] | None), K0,
     W (4 bf16 [N, K] tensors), Wf (None or 4 frag_pack copies of W), b (4 fp32 tensors),
-    N (4 ints), y (3 bf16 [M, N] tensors or None), out (fp32 [M, N3])."""
+    N (4 ints), y (3 bf16 [M, N] tensors or None), out (fp32 [M, N3]).  rollout: a
+    RolloutStep (actor and critic over the M envs: pmlp_rollout_forward)."""
     def mk(n):
         y = n.get("y") or (None, None, None)
         return MlpFwdJob(_p(n["x"]), _p(n.get("rows")), n["x"].stride(0), n["kx"], _p(n.get("xa")),
@@ -202,7 +215,10 @@ def mlp_forward(nets, M):
                          (C.c_int32 * 3)(*[0 if t is None else t.stride(0) for t in y]), _p(n["out"]),
                          n["out"].stride(0), (C.c_void_p * 4)(*[_p(w) for w in (n.get("Wf") or (None,) * 4)]))
     arr = (MlpFwdJob * len(nets))(*[mk(n) for n in nets])
-    _ok(load().pmlp_mlp_forward(len(nets), arr, int(M), _stream()), "pmlp_mlp_forward")
+    if rollout is not None:  # the rollout step's sampling, storage rows and deferred store ride along
+        _ok(load().pmlp_rollout_forward(arr, int(M), C.byref(rollout), _stream()), "pmlp_rollout_forward")
+    else:
+        _ok(load().pmlp_mlp_forward(len(nets), arr, int(M), _stream()), "pmlp_mlp_forward")
 
 
 def _convert(jobs):

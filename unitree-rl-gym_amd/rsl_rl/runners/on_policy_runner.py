@@ -87,6 +87,10 @@ class _RolloutGraph:
         env.common_step_counter = step0
         storage.step = storage0
         self.obs, self.critic_obs = obs, critic_obs
+        # the fused rollout's last process_env_step is deferred (FusedRollout.store): every
+        # replay leaves it pending exactly as the captured loop did
+        ro = runner.alg._rollout
+        self.pending = getattr(ro, "pending", None)
 
     def matches(self, obs, critic_obs):
         """The loop's inputs are the buffers it was captured on (same env-buffer parity)."""
@@ -97,6 +101,8 @@ class _RolloutGraph:
             self.graph.replay()
         self.runner.env.account_replayed_steps(self.T)
         self.runner.alg.storage.step = self.T
+        if self.pending is not None:
+            self.runner.alg._rollout.pending = self.pending
         return self.obs, self.critic_obs
 
     def finished_episodes(self, rewbuffer, lenbuffer):
