@@ -130,6 +130,21 @@ def load_sq_valu(kernel_ms):
             "valu_insts_per_launch": sq["valu_insts_per_launch"], "share_of_wave_time": sq.get("share_of_wave_time")}
 
 
+def _cpu_share():
+    """The CPUs this process may use: its affinity mask and the cgroup v2 cpu.max quota."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -234,6 +249,7 @@ def cpu_baseline(env, seconds):
         build = ("gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (oracle/Makefile; built in the container, "
                  "the native build failed on this host)")
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    share = _cpu_share()
     n = env.num_envs
     half = max(2.0, seconds / 4)
     rate_all, st_all, el_all = _oracle_rate(env, bridge, lib, n, half, threads)
@@ -257,7 +273,11 @@ def cpu_baseline(env, seconds):
             "go2_4_envs": {"env_only_env_steps_per_s": round(rate4_all, 1),
                            "env_only_env_steps_per_s_1_thread": round(rate4_one, 1),
                            "ppo_iter_ms": round(it4 * 1e3, 2)},
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "build": build}
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "cpu_share": share,
+            "cores_note": (f"{threads} threads = OMP_NUM_THREADS, the job's CPU share as the harness sets it; "
+                           f"the process may run on {share['affinity_cpus']} CPUs (sched_getaffinity), cgroup "
+                           f"cpu.max quota {share['cgroup_quota_cpus']} CPUs; nproc counts the whole machine"),
+            "build": build}
 
 
 def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
@@ -292,6 +312,15 @@ def ppo_iter_rate(task, n, dev, iters, warmup, get_args, task_registry):
     return out
 
 
+def capacity_drops(env, steps):
+    """What the fixed constraint capacity (8 contact slots + 8 limit rows per env) left out over
+    the last `steps` control steps (lgs_get_contact_stats), per env and substep: touching bodies
+    without a contact row, self contacts without one, violated joint limits without a row."""
+    st = env.sim.contact_stats(reset=True)
+    den = float(steps * env.num_envs * env.cfg.control.decimation)
+    return {k: v / den for k, v in st.items()}
+
+
 def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
     """Back-to-back fused env steps of another BASELINE config (env only, no policy),
     timed with HIP events on the env's stream: env-steps/s and ms per step."""
@@ -309,6 +338,7 @@ def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
     env.actions.copy_(acts[0])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
+    env.sim.contact_stats(reset=True)
     e0.record(stream)
     for i in range(steps):
         env._buf_idx ^= 1
@@ -319,7 +349,8 @@ def env_kernel_rate(task, n, dev, steps, get_args, task_registry):
     ms = e0.elapsed_time(e1) / steps
     out = {"num_envs": n, "decimation": env.cfg.control.decimation, "env_step_kernel_ms": round(ms, 4),
            "env_steps_per_s": round(n / (ms * 1e-3), 1),
-           "terrain": env.cfg.terrain.mesh_type}
+           "terrain": env.cfg.terrain.mesh_type,
+           "capacity_drops_per_env_substep": capacity_drops(env, steps)}
     env.close()
     return out
 
@@ -360,6 +391,7 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     env.actions.copy_(acts[0])
     torch.cuda.synchronize(dev)
+    env.sim.contact_stats(reset=True)
     e0.record(stream)
     for i in range(args.env_steps):
         env._buf_idx ^= 1
@@ -368,6 +400,7 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = e0.elapsed_time(e1) / args.env_steps
+    go2_drops = capacity_drops(env, args.env_steps)
     # (b) env.step() as the runner calls it (actions copy + launch + extras dict)
     t0 = time.time()
     for i in range(args.env_steps):
@@ -427,6 +460,7 @@ def main():
         "env_only_env_steps_per_s": round(env_only, 1),
         "rollout_env_steps_per_s": round(rollout, 1),
         "env_step_kernel_ms": round(kernel_ms, 4),
+        "capacity_drops_per_env_substep": go2_drops,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch"),
                      "traffic_read_write": [pmc.get("read_bytes_per_launch"), pmc.get("write_bytes_per_launch")],

@@ -93,6 +93,11 @@ static int set_err(int code, const std::string& msg) {
 // ------------------------------------------------------------ device math --
 struct DevModel {
     int B, D, P;
+    // the robot's own body / DOF counts.  B, D (and the kernel's template sizes) may be larger:
+    // lgs_create_sim pads a model to its kernel's shape with inert bodies and DOFs (no mass, no
+    // contact candidates, no torque; every product they enter is an exact zero), so the state,
+    // torques, observations and body rows in memory use Br / Dr
+    int Br, Dr;
     const int* parent;
     const int* dof;
     const int* subtree_end;
@@ -1505,9 +1510,10 @@ __device__ __forceinline__ int xcd_env(int b, int nwg) {
 
 // rigid body states [B][13] of the block's env into global memory
 template <int D, int B, int ROWS, int EPW>
-__device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, float* rbs_out, unsigned mask = 0u) {
+__device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, float* rbs_out, int Br,
+                            unsigned mask = 0u) {
     const int lane = hl<EPW>();
-    if (lane < B && (!mask || ((mask >> lane) & 1u))) {  // mask: the rows the task reads (0: all)
+    if (lane < Br && (!mask || ((mask >> lane) & 1u))) {  // mask: the rows the task reads (0: all)
         float R[9], p[3], aw[3] = {0.f, 0.f, 0.f};
         quat_to_mat(s.root + 3, R);
         p[0] = s.root[0]; p[1] = s.root[1]; p[2] = s.root[2];
@@ -1558,21 +1564,22 @@ __device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, flo
 }
 
 template <int D, int B, int ROWS, int EPW>
-__device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
+__device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& st, const DevModel& md, int e) {
     const int lane = hl<EPW>();
     if (lane < 13) s.root[lane] = st.root[13 * e + lane];
-    if (lane < 2 * D) {
-        const float v = st.dofs[(size_t)2 * D * e + lane];
+    if (lane < 2 * D) {  // (a padded model's inert DOFs rest at 0)
+        const float v = lane < 2 * md.Dr ? st.dofs[(size_t)2 * md.Dr * e + lane] : 0.f;
         if (lane & 1) s.qd[lane >> 1] = v; else s.q[lane >> 1] = v;
     }
 }
 template <int D, int B, int ROWS, int EPW>
-__device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, int e) {
+__device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, const DevModel& md, int e) {
     int lane = hl<EPW>();
     asm volatile("" : "+v"(lane));  // recompute the lane indices here (no value kept live from load_state)
     if (lane < 13) st.root[13 * e + lane] = s.root[lane];
-    if (lane < 2 * D) st.dofs[(size_t)2 * D * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
-    for (int i = lane; i < 3 * B; i += WAVE / EPW) st.cforce[(size_t)3 * B * e + i] = (&s.cf[0][0])[i];
+    const int Dr = md.Dr, Br = md.Br;
+    if (lane < 2 * Dr) st.dofs[(size_t)2 * Dr * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
+    for (int i = lane; i < 3 * Br; i += WAVE / EPW) st.cforce[(size_t)3 * Br * e + i] = (&s.cf[0][0])[i];
 }
 
 // ---------------------------------------------------------- kernels --------
@@ -1583,12 +1590,13 @@ __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevSt
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, e);
-    if (threadIdx.x < D) s.tau[threadIdx.x] = st.torques_in[(size_t)D * e + threadIdx.x];
+    load_state<D, B, ROWS, 1>(s, st, md, e);
+    if (threadIdx.x < D)
+        s.tau[threadIdx.x] = threadIdx.x < md.Dr ? st.torques_in[(size_t)md.Dr * e + threadIdx.x] : 0.f;
     __syncthreads();
     substep<D, B, ROWS, CH, 1>(&s, mc, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
-    store_state<D, B, ROWS, 1>(s, st, e);
-    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
+    store_state<D, B, ROWS, 1>(s, st, md, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
 }
 
 template <int D, int B, int ROWS, int CH>
@@ -1598,9 +1606,9 @@ __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, e);
+    load_state<D, B, ROWS, 1>(s, st, md, e);
     __syncthreads();
-    body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
+    body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
 }
 
 struct DevEnv {
@@ -1656,7 +1664,7 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
     const float* cmd = s.u.post.misc + 12;
     const float* act = s.act;
     const float* last_act = E.last_actions + A * e;
-    const float* last_qd = E.last_dof_vel + D * e;
+    const float* last_qd = E.last_dof_vel + A * e;
     float* air = E.feet_air_time + T.num_feet * e;
     uint8_t* lastc = E.last_contacts + T.num_feet * e;
     const float* tau = s.tau;
@@ -1909,11 +1917,11 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     const int reset = s.flags[0];
     float* act = s.act;
     if (reset) {  // reset_idx (legged_robot.py:723-768)
-        if (lane < D) {
+        if (lane < D) {  // (a padded model's inert DOFs: default 0)
             s.q[lane] = T.default_dof_pos[lane] *
                         rand_range(0.5f, 1.5f, philox_uniform(seed, e, step, LGS_STREAM_RESET_DOF, lane));
             s.qd[lane] = 0.f;
-            E.last_dof_vel[D * e + lane] = 0.f;
+            if (lane < A) E.last_dof_vel[A * e + lane] = 0.f;
         }
         if (lane < A) { act[lane] = 0.f; E.actions[A * e + lane] = 0.f; E.last_actions[A * e + lane] = 0.f; }
         if (lane < T.num_feet) E.feet_air_time[T.num_feet * e + lane] = 0.f;
@@ -1966,8 +1974,8 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[3 + i] * T.obs_scale_ang_vel;
         for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[6 + i];
         for (int i = 0; i < 3; ++i) tmp[k++] = cmd[i] * T.commands_scale[i];
-        for (int j = 0; j < D; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
-        for (int j = 0; j < D; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
+        for (int j = 0; j < A; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
+        for (int j = 0; j < A; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
         for (int j = 0; j < A; ++j) tmp[k++] = act[j];
         if (T.obs_layout == LGS_OBS_HUMANOID) {
             float ph = 2.0f * 3.14159265358979323846f * s.u.post.misc[9];
@@ -1990,7 +1998,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
             E.priv_obs[(size_t)P * e + i] = clipf(s.u.post.obs_tmp[i], -T.clip_observations, T.clip_observations);
     // bookkeeping (:707-709)
     if (lane < A) E.last_actions[A * e + lane] = act[lane];
-    if (lane < D) E.last_dof_vel[D * e + lane] = s.qd[lane];
+    if (lane < A) E.last_dof_vel[A * e + lane] = s.qd[lane];
     if (vsim && T.push_robots && lane < 2) {
         // last_root_vel[:, 0:2]: the all-env push draw whenever any env is pushed this step
         // (legged_robot.py:549-550, 709), which is nearly every step; the simulated values
@@ -2026,9 +2034,9 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     const lgs_task_params& T = *Tp;
     const int lane = hl<EPW>();
     load_model(mc, md);
-    load_state<D, B, ROWS, EPW>(s, st, e);
+    load_state<D, B, ROWS, EPW>(s, st, md, e);
     const int A = T.num_actions;
-    float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * B * e : nullptr;
+    float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * md.Br * e : nullptr;
     STAMP_INIT();
     if (mode == MODE_STEP || mode == MODE_PHYSICS) {
         float a = 0.f;
@@ -2038,7 +2046,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
             E.actions[A * e + lane] = a;
             s.act[lane] = a;
         }
-        const float lqd = (lane < D) ? E.last_dof_vel[D * e + lane] : 0.f;
+        const float lqd = (lane < A) ? E.last_dof_vel[A * e + lane] : 0.f;
         const float am = st.added_mass ? st.added_mass[e] : 0.f;
         const float mu = st.friction ? st.friction[e] : 1.f;
         __syncthreads();
@@ -2053,16 +2061,23 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
                 s.tau[lane] = clipf(t, -T.torque_limits[lane], T.torque_limits[lane]);
             }
             __syncthreads();
+#ifndef LGS_DIAG_IO_ONLY
             substep<D, B, ROWS, CH, EPW>(sm, mc, md, sp, am, mu);
+#else
+            // diagnostic build (never the shipped library): no physics, the step's global loads
+            // and stores unchanged -- a known-byte calibration of the traffic counters
+            if (lane < 3 * B) (&s.cf[0][0])[lane] = 0.f;
+#endif
         }
         STAMP(0);
-        if (lane < D) E.torques[D * e + lane] = s.tau[lane];
+        if (lane < A) E.torques[A * e + lane] = s.tau[lane];
         // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only: the rows they read
-        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs, T.body_state_mask);
+        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs, md.Br, T.body_state_mask);
     } else {  // the physics half's outputs, as it stored them
         if (lane < A) s.act[lane] = E.actions[A * e + lane];
-        if (lane < D) s.tau[lane] = E.torques[D * e + lane];
-        for (int i = lane; i < 3 * B; i += WAVE / EPW) (&s.cf[0][0])[i] = st.cforce[(size_t)3 * B * e + i];
+        if (lane < D) s.tau[lane] = lane < A ? E.torques[A * e + lane] : 0.f;
+        for (int i = lane; i < 3 * B; i += WAVE / EPW)
+            (&s.cf[0][0])[i] = i < 3 * md.Br ? st.cforce[(size_t)3 * md.Br * e + i] : 0.f;
     }
     __syncthreads();
     STAMP(15);
@@ -2072,7 +2087,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
                                       st.vsim);
     __syncthreads();
     STAMP(16);
-    store_state<D, B, ROWS, EPW>(s, st, e);
+    store_state<D, B, ROWS, EPW>(s, st, md, e);
     STAMP(17);
     STAMP_FLUSH(e);
 }
@@ -2088,13 +2103,14 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     if (mask && !mask[e]) return;
     if (E.step_counter) step = (uint32_t)*E.step_counter;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, e);
-    if (threadIdx.x < 3 * B) (&s.cf[0][0])[threadIdx.x] = st.cforce[(size_t)3 * B * e + threadIdx.x];
+    load_state<D, B, ROWS, 1>(s, st, md, e);
+    if (threadIdx.x < 3 * B)
+        (&s.cf[0][0])[threadIdx.x] = threadIdx.x < 3 * md.Br ? st.cforce[(size_t)3 * md.Br * e + threadIdx.x] : 0.f;
     __syncthreads();
     post_physics<D, B, ROWS, 1>(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
     __syncthreads();
-    store_state<D, B, ROWS, 1>(s, st, e);
-    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * B * e);
+    store_state<D, B, ROWS, 1>(s, st, md, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
 }
 
 // After k_step (one block): the extras of reset_idx (legged_robot.py:742-768) —
@@ -2471,7 +2487,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     free(host);
     char* d = (char*)s->model_mem;
     DevModel& md = s->md;
-    md.B = B; md.D = D; md.P = P;
+    md.B = B; md.D = D; md.P = P; md.Br = B; md.Dr = D;
     md.parent = (const int*)(d + o_parent); md.dof = (const int*)(d + o_dof); md.subtree_end = (const int*)(d + o_se);
     md.depth = (const int*)(d + o_depth); md.chain = (const int*)(d + o_chain);
     md.joint_rot = (const float*)(d + o_jr); md.joint_pos = (const float*)(d + o_jp); md.axis = (const float*)(d + o_ax);
