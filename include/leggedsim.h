@@ -371,6 +371,12 @@ LGS_API int32_t lgs_find_dof(lgs_sim* sim, const char* name);
 #define LGS_NUM_CONTACT_STATS 3
 LGS_API int lgs_get_contact_stats(lgs_sim* sim, uint64_t* out, int32_t reset);
 
+/* the compiled kernel shape the sim runs on: *dofs >= the model's DOFs, *bodies >= its bodies
+ * (a robot without an instantiation of its own is padded to the smallest generic one that
+ * fits -- inert DOFs and bodies, results bit-identical to the unpadded model), *rows the
+ * constraint-row capacity.  Any pointer may be NULL. */
+LGS_API int lgs_get_instantiation(lgs_sim* sim, int32_t* dofs, int32_t* bodies, int32_t* rows);
+
 /* diagnostics: per-phase s_memtime cycle sums [N][24] of the last lgs_step
  * (only in a library built with -DLGS_PHASE_STAMPS; otherwise LGS_ERR_STATE) */
 LGS_API int lgs_debug_set_phase_buffer(void* dev_ptr);

@@ -741,7 +741,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
             const float* F = s.u.dyn.Fj[jc];
             const float cn[3] = {F[0], F[1], F[2]}, cf[3] = {F[3], F[4], F[5]};
             float val = dot3(Sw, cn) + dot3(Sv, cf);
-            if (jc == jr) val += sp.armature;
+            if (jc == jr) val += jr < md.Dr ? sp.armature : 1.f;  // (a padded model's inert DOF: M_jj = 1)
             m[cp] = ((mc.anc[jc] >> jr) & 1u) ? val : 0.f;
         }
         float Fn[3] = {s.u.dyn.cpk[bj][10 + 0], s.u.dyn.cpk[bj][10 + 1], s.u.dyn.cpk[bj][10 + 2]};
@@ -2169,6 +2169,7 @@ __global__ void k_copy_rows(float* dst, const float* src, const int32_t* ids, in
 // ------------------------------------------------------------ host side ----
 struct lgs_sim {
     int N, B, D, P;
+    int Dt, Bt;  // the instantiation shape the model is padded to (>= D, B; see LGS_GENERIC_SHAPES)
     int device;
     hipStream_t stream = nullptr;
     DevModel md{};
@@ -2209,12 +2210,32 @@ enum Variant { V_12_19, V_12_13_32, V_10_11_32, V_12_13, V_10_11, V_12_19_48, V_
 #ifndef LGS_EXTRA_SHAPES
 #define LGS_EXTRA_SHAPES X(23, 24)
 #endif
+// Runtime generality: any other robot (D <= LGS_MAX_DOFS, B <= LGS_MAX_BODIES) runs on the
+// smallest of these padded instantiations it fits, X(Dt, Bt) with D <= Dt and
+// B + (Dt - D) <= Bt, with no rebuild: lgs_create_sim appends Dt - D inert DOFs (each on
+// a massless body hinged to the base, M_jj = 1, no gains, no limits, no candidates) and
+// then inert fixed bodies up to Bt.  An inert DOF's rows and columns of every matrix the
+// step factorises are zero off the diagonal, so the real DOFs' arithmetic -- and the
+// results, bit for bit -- are those of the unpadded model (tests/test_gpu_padded.py).
+#ifndef LGS_GENERIC_SHAPES
+#define LGS_GENERIC_SHAPES X(16, 24) X(26, 32)
+#endif
+#define LGS_ALL_48_SHAPES LGS_EXTRA_SHAPES LGS_GENERIC_SHAPES
 
-static bool extra_shape(const lgs_sim* s) {
-#define X(D_, B_) if (s->D == D_ && s->B <= B_) return true;
+// the instantiation shape (Dt, Bt) a model of D DOFs and B bodies is padded to among the
+// extra (exact D) and generic (padded D) shapes; false if none fits
+static bool extra_shape(int D, int B, int* Dt, int* Bt) {
+#define X(D_, B_) if (D == D_ && B <= B_) { *Dt = D_; *Bt = B_; return true; }
     LGS_EXTRA_SHAPES
 #undef X
+#define X(D_, B_) if (D <= D_ && B + (D_ - D) <= B_) { *Dt = D_; *Bt = B_; return true; }
+    LGS_GENERIC_SHAPES
+#undef X
     return false;
+}
+static bool extra_shape(const lgs_sim* s) {
+    int dt, bt;
+    return extra_shape(s->D, s->B, &dt, &bt);
 }
 
 static Variant pick(const lgs_sim* s) {
@@ -2227,6 +2248,14 @@ static Variant pick(const lgs_sim* s) {
     if (s->D == 10 && s->B <= 11) return V_10_11;
     if (extra_shape(s)) return V_EXTRA;
     return V_NONE;
+}
+static void variant_shape(const lgs_sim* s, Variant v, int* Dt, int* Bt) {
+    switch (v) {
+    case V_12_19: case V_12_19_48: *Dt = 12; *Bt = 19; break;
+    case V_12_13_32: case V_12_13: *Dt = 12; *Bt = 13; break;
+    case V_10_11_32: case V_10_11: *Dt = 10; *Bt = 11; break;
+    default: if (!extra_shape(s->D, s->B, Dt, Bt)) { *Dt = s->D; *Bt = s->B; }
+    }
 }
 static int variant_rows(Variant v) { return (v == V_12_19 || v == V_12_13_32 || v == V_10_11_32) ? 32 : 48; }  // (V_EXTRA: 48)
 static int variant_chain(Variant v) {
@@ -2289,27 +2318,27 @@ static void ex_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_task_
 }
 static int extra_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
                       lgs_env_buffers E, int N, uint32_t step, int mode) {
-#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_step<D_, B_>(s, md, sp, st, tp, E, N, step, mode); return LGS_OK; }
-    LGS_EXTRA_SHAPES
+#define X(D_, B_) if (s->Dt == D_ && s->Bt == B_) { ex_step<D_, B_>(s, md, sp, st, tp, E, N, step, mode); return LGS_OK; }
+    LGS_ALL_48_SHAPES
 #undef X
     return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
 }
 static int extra_simulate(const lgs_sim* s, DevModel md, DevSim sp, DevState st, int N) {
-#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_simulate<D_, B_>(s, md, sp, st, N); return LGS_OK; }
-    LGS_EXTRA_SHAPES
+#define X(D_, B_) if (s->Dt == D_ && s->Bt == B_) { ex_simulate<D_, B_>(s, md, sp, st, N); return LGS_OK; }
+    LGS_ALL_48_SHAPES
 #undef X
     return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
 }
 static int extra_fk(const lgs_sim* s, DevModel md, DevState st, int N) {
-#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_fk<D_, B_>(s, md, st, N); return LGS_OK; }
-    LGS_EXTRA_SHAPES
+#define X(D_, B_) if (s->Dt == D_ && s->Bt == B_) { ex_fk<D_, B_>(s, md, st, N); return LGS_OK; }
+    LGS_ALL_48_SHAPES
 #undef X
     return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
 }
 static int extra_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_task_params* tp, lgs_env_buffers E,
                        int N, uint32_t step, const uint8_t* mask) {
-#define X(D_, B_) if (s->D == D_ && s->B <= B_) { ex_reset<D_, B_>(s, md, st, tp, E, N, step, mask); return LGS_OK; }
-    LGS_EXTRA_SHAPES
+#define X(D_, B_) if (s->Dt == D_ && s->Bt == B_) { ex_reset<D_, B_>(s, md, st, tp, E, N, step, mask); return LGS_OK; }
+    LGS_ALL_48_SHAPES
 #undef X
     return set_err(LGS_ERR_ARG, "unsupported model size (D,B)");
 }
@@ -2425,6 +2454,7 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
         }
     }
     const int B = s->B, D = s->D, P = s->P;
+    variant_shape(s, pick(s), &s->Dt, &s->Bt);
     if (m->body_names)
         for (int b = 0; b < B; ++b) s->body_names.emplace_back(m->body_names[b] ? m->body_names[b] : "");
     if (m->dof_names)
@@ -2463,8 +2493,33 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
         o[4] = (float)(rmax * (1.0 + 1e-6) + 1e-6);
     }
     for (int k = 0; k < P; ++k) chunk32[k / 32] |= 1u << m->pt_body[k];
-    size_t ints = (size_t)B * (4 + LGS_MAX_DEPTH) + (size_t)P + chunk32.size();
-    size_t floats = (size_t)B * (9 + 3 + 3 + 1 + 3 + 6 + 5) + (size_t)D * 3 + (size_t)P * 4;
+    // the model padded to the instantiation shape (Dt, Bt): DOF D + k on body B + k, a
+    // massless body hinged to the base about z (M_jj = 1 in the kernel, no limits); then
+    // fixed massless bodies on the base; the base's subtree covers them all
+    const int Dt = s->Dt, Bt = s->Bt;
+    std::vector<int> parent(m->parent, m->parent + B), dofv(m->dof, m->dof + B), se(m->subtree_end, m->subtree_end + B);
+    std::vector<int> depth(m->depth, m->depth + B), chain(m->chain, m->chain + (size_t)B * LGS_MAX_DEPTH);
+    std::vector<float> jr(m->joint_rot, m->joint_rot + 9 * B), jp(m->joint_pos, m->joint_pos + 3 * B);
+    std::vector<float> ax(m->axis, m->axis + 3 * B), mass(m->mass, m->mass + B), com(m->com, m->com + 3 * B);
+    std::vector<float> inertia(m->inertia, m->inertia + 6 * B);
+    std::vector<float> dlo(m->dof_lower, m->dof_lower + D), dhi(m->dof_upper, m->dof_upper + D);
+    std::vector<float> dvel(m->dof_velocity, m->dof_velocity + D);
+    for (int b = B; b < Bt; ++b) {
+        const int j = D + (b - B) < Dt ? D + (b - B) : -1;
+        parent.push_back(0); dofv.push_back(j); se.push_back(b + 1); depth.push_back(1);
+        for (int k = 0; k < LGS_MAX_DEPTH; ++k) chain.push_back(k == 0 ? 0 : (k == 1 ? b : -1));
+        const float rot[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+        jr.insert(jr.end(), rot, rot + 9);
+        for (int k = 0; k < 3; ++k) { jp.push_back(0.f); ax.push_back(k == 2 ? 1.f : 0.f); com.push_back(0.f); }
+        mass.push_back(0.f);
+        for (int k = 0; k < 6; ++k) inertia.push_back(0.f);
+        if (j >= 0) { dlo.push_back(-1e30f); dhi.push_back(1e30f); dvel.push_back(0.f); }
+    }
+    se[0] = Bt;
+    bsph.resize((size_t)5 * Bt, 0.f);
+    for (int b = B; b < Bt; ++b) bsph[(size_t)5 * b + 3] = -1.f;
+    size_t ints = (size_t)Bt * (4 + LGS_MAX_DEPTH) + (size_t)P + chunk32.size();
+    size_t floats = (size_t)Bt * (9 + 3 + 3 + 1 + 3 + 6 + 5) + (size_t)Dt * 3 + (size_t)P * 4;
     size_t bytes = ints * 4 + floats * 4 + 512;
     HIP_TRY(hipMalloc(&s->model_mem, bytes));
     char* host = (char*)calloc(1, bytes);
@@ -2475,19 +2530,19 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
         off += (n + 15) & ~size_t(15);
         return o;
     };
-    size_t o_parent = put(m->parent, 4 * B), o_dof = put(m->dof, 4 * B), o_se = put(m->subtree_end, 4 * B);
-    size_t o_depth = put(m->depth, 4 * B), o_chain = put(m->chain, 4 * B * LGS_MAX_DEPTH);
-    size_t o_jr = put(m->joint_rot, 36 * B), o_jp = put(m->joint_pos, 12 * B), o_ax = put(m->axis, 12 * B);
-    size_t o_mass = put(m->mass, 4 * B), o_com = put(m->com, 12 * B), o_in = put(m->inertia, 24 * B);
-    size_t o_lo = put(m->dof_lower, 4 * D), o_hi = put(m->dof_upper, 4 * D), o_vel = put(m->dof_velocity, 4 * D);
+    size_t o_parent = put(parent.data(), 4 * Bt), o_dof = put(dofv.data(), 4 * Bt), o_se = put(se.data(), 4 * Bt);
+    size_t o_depth = put(depth.data(), 4 * Bt), o_chain = put(chain.data(), 4 * Bt * LGS_MAX_DEPTH);
+    size_t o_jr = put(jr.data(), 36 * Bt), o_jp = put(jp.data(), 12 * Bt), o_ax = put(ax.data(), 12 * Bt);
+    size_t o_mass = put(mass.data(), 4 * Bt), o_com = put(com.data(), 12 * Bt), o_in = put(inertia.data(), 24 * Bt);
+    size_t o_lo = put(dlo.data(), 4 * Dt), o_hi = put(dhi.data(), 4 * Dt), o_vel = put(dvel.data(), 4 * Dt);
     size_t o_pb = put(m->pt_body, 4 * P), o_pp = put(m->pt_pos, 12 * P), o_pr = put(m->pt_radius, 4 * P);
-    size_t o_bs = put(bsph.data(), 20 * B), o_ch = put(chunk32.data(), 4 * chunk32.size());
+    size_t o_bs = put(bsph.data(), 20 * Bt), o_ch = put(chunk32.data(), 4 * chunk32.size());
     if (off > bytes) { free(host); return set_err(LGS_ERR_STATE, "model packing overflow"); }
     HIP_TRY(hipMemcpy(s->model_mem, host, off, hipMemcpyHostToDevice));
     free(host);
     char* d = (char*)s->model_mem;
     DevModel& md = s->md;
-    md.B = B; md.D = D; md.P = P; md.Br = B; md.Dr = D;
+    md.B = Bt; md.D = Dt; md.P = P; md.Br = B; md.Dr = D;
     md.parent = (const int*)(d + o_parent); md.dof = (const int*)(d + o_dof); md.subtree_end = (const int*)(d + o_se);
     md.depth = (const int*)(d + o_depth); md.chain = (const int*)(d + o_chain);
     md.joint_rot = (const float*)(d + o_jr); md.joint_pos = (const float*)(d + o_jp); md.axis = (const float*)(d + o_ax);
@@ -2711,7 +2766,12 @@ LGS_API int lgs_set_task(lgs_sim* s, const lgs_task_params* t) {
         if (t->termination_idx[i] < 0 || t->termination_idx[i] >= s->B) return set_err(LGS_ERR_ARG, "termination index out of range");
     for (int i = 0; i < t->num_hip; ++i)
         if (t->hip_dofs[i] < 0 || t->hip_dofs[i] >= s->D) return set_err(LGS_ERR_ARG, "hip dof out of range");
-    HIP_TRY(hipMemcpy(s->task_dev, t, sizeof(lgs_task_params), hipMemcpyHostToDevice));
+    lgs_task_params tt = *t;  // a padded model's inert DOFs: no gains, no torque, no limits
+    for (int j = t->num_actions; j < LGS_MAX_DOFS; ++j) {
+        tt.p_gains[j] = tt.d_gains[j] = tt.default_dof_pos[j] = tt.torque_limits[j] = 0.f;
+        tt.soft_dof_pos_lower[j] = tt.soft_dof_pos_upper[j] = tt.dof_vel_limits[j] = 0.f;
+    }
+    HIP_TRY(hipMemcpy(s->task_dev, &tt, sizeof(lgs_task_params), hipMemcpyHostToDevice));
     s->has_task = 1;
     return LGS_OK;
 }
@@ -2834,6 +2894,14 @@ static int32_t find_name(const std::vector<std::string>& names, const char* name
 
 LGS_API int32_t lgs_find_body(lgs_sim* s, const char* name) { return s ? find_name(s->body_names, name) : -1; }
 LGS_API int32_t lgs_find_dof(lgs_sim* s, const char* name) { return s ? find_name(s->dof_names, name) : -1; }
+
+LGS_API int lgs_get_instantiation(lgs_sim* s, int32_t* dofs, int32_t* bodies, int32_t* rows) {
+    if (!s) return set_err(LGS_ERR_ARG, "null argument");
+    if (dofs) *dofs = s->Dt;
+    if (bodies) *bodies = s->Bt;
+    if (rows) *rows = variant_rows(pick(s));
+    return LGS_OK;
+}
 
 LGS_API int lgs_get_counts(lgs_sim* s, int32_t* n, int32_t* b, int32_t* d) {
     if (!s) return set_err(LGS_ERR_ARG, "null sim");

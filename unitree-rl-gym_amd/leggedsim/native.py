@@ -73,6 +73,8 @@ def load():
     if hasattr(lib, "lgs_get_contact_stats"):  # (absent only from pre-round-4 builds used in A/B timing)
         lib.lgs_get_contact_stats.argtypes = [vp, vp, C.c_int32]
         lib.lgs_get_contact_stats.restype = C.c_int
+    lib.lgs_get_instantiation.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.lgs_get_instantiation.restype = C.c_int
     for name in ("lgs_get_body_name", "lgs_get_dof_name"):
         getattr(lib, name).argtypes = [vp, C.c_int32]
         getattr(lib, name).restype = C.c_char_p
@@ -102,7 +104,7 @@ EXPORTED_SYMBOLS = [
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
     "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
-    "lgs_get_contact_stats",
+    "lgs_get_contact_stats", "lgs_get_instantiation",
 ]
 
 
@@ -215,6 +217,13 @@ class Sim:
         check(self.lib, self.lib.lgs_get_contact_stats(self.handle, out.ctypes.data, int(bool(reset))),
               "lgs_get_contact_stats")
         return {"bodies": int(out[0]), "self": int(out[1]), "limits": int(out[2])}
+
+    def padded_shape(self):
+        """(DOFs, bodies) of the compiled kernel the sim runs on (the model padded to it)."""
+        d, b = C.c_int32(), C.c_int32()
+        check(self.lib, self.lib.lgs_get_instantiation(self.handle, C.byref(d), C.byref(b), None),
+              "lgs_get_instantiation")
+        return d.value, b.value
 
     # name queries (gym.get_asset_rigid_body_names / get_asset_dof_names /
     # find_actor_rigid_body_handle, legged_robot.py:342-343, 388-407)
