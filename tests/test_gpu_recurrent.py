@@ -280,10 +280,16 @@ def test_recurrent_rollout_saves_the_pre_step_state_from_the_kernel():
         obs, cobs = torch.randn(N, O, device="cuda"), torch.randn(N, P, device="cuda")
         prev = [None if s is None else s.clone() for s in (ac.memory_a.hidden_states or (None, None))] + \
                [None if s is None else s.clone() for s in (ac.memory_c.hidden_states or (None, None))]
+        rew, done = torch.randn(N, device="cuda"), torch.rand(N, device="cuda") < 0.2
+        tout = torch.rand(N, device="cuda") < 0.5
         with torch.inference_mode():
             alg.act(obs, cobs)
-            alg.process_env_step(torch.randn(N, device="cuda"), torch.rand(N, device="cuda") < 0.2,
-                                 {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+            alg.process_env_step(rew, done, {"time_outs": tout})
+        alg.flush_rollout()
+        # process_env_step's storage rows (rsl_rl ppo.py: reward bootstrapped on time-outs)
+        want = rew + alg.gamma * st.values[t].squeeze(1) * tout.float()
+        torch.testing.assert_close(st.rewards[t].squeeze(1), want, rtol=1e-6, atol=1e-6)
+        assert torch.equal(st.dones[t].view(-1).bool(), done)
         got = [st.saved_hidden_states_a[0][t], st.saved_hidden_states_a[1][t], st.saved_hidden_states_c[0][t],
                st.saved_hidden_states_c[1][t]]
         for g, p in zip(got, prev):

@@ -311,11 +311,12 @@ class FusedPPOStep:
 
 class FusedRollout:
     """PPO.act + RolloutStorage.add_transitions and PPO.process_env_step for the
-    Gaussian MLP policy in 5 + 1 + 1 launches per env step: the bf16 forward of both
-    nets (one convert, L GEMMs), pmlp_act (sample, log-prob, storage row incl. the
-    observations) and pmlp_store_step (bootstrapped reward, dones).  The policy
-    noise is Philox keyed on a device draw counter, so a captured rollout draws
-    fresh noise on every replay; the seed comes from torch's (seeded) generator."""
+    Gaussian MLP policy in ONE launch per env step (pmlp_rollout_forward): the bf16
+    forward of both nets, the sampling / log-prob / storage rows (incl. the
+    observations) in the actor job's epilogue, and the previous step's deferred
+    process_env_step (bootstrapped reward, dones).  The policy noise is Philox keyed on
+    a device draw counter, so a captured rollout draws fresh noise on every replay; the
+    seed comes from torch's (seeded) generator."""
 
     def __init__(self, step: FusedPPOStep, num_envs):
         self.f = step
@@ -528,7 +529,13 @@ class RecurrentRollout:
                                   mm._stream()), "pmlp_act")
         return self.actions
 
-    store = FusedRollout.store
+    pending = None
+    flush = FusedRollout.flush
+
+    def store(self, rewards, dones, time_outs, storage, t, gamma):
+        """PPO.process_env_step: pmlp_store_step at once (no forward launch to ride in)."""
+        self.pending = (rewards, dones, time_outs, t, gamma)
+        self.flush(storage)
 
 
 def gae(storage, last_values, gamma, lam, world_size=1):
