@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 #include <string>
 
 #include "../../include/ppo_mlp.h"
@@ -161,6 +162,11 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     // gradients), staged k-major in LDS and fed to the MFMAs by transposed reads
     constexpr bool TNL = EPI == PMLP_EPI_PARTIAL_TN;
     constexpr bool PART = EPI == PMLP_EPI_PARTIAL || TNL;
+    // SW: the MFMAs take (B, A), so the accumulators hold C^T in the MFMA layout: a lane owns
+    // ONE row m of C and 4 consecutive columns n per register quad -- 16-byte slab stores and
+    // 8-byte LDS accesses in the epilogue instead of one per element (the same products, the
+    // same k order)
+    constexpr bool SW = PART || EPI == PMLP_EPI_BWD_DX;
     constexpr bool AF32 = (MODE & 1) != 0;
     constexpr bool BKN = TNL || (MODE & 2) != 0;  // B staged from [K][N]
     static_assert(!BKN || PMLP_NBUF == 1, "k-major B stages one k-tile");
@@ -391,14 +397,15 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         if constexpr (TNL) {
             if (dosum) {
                 bf16x8 ones;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) ones[u] = (bf16)1.f;
 #pragma unroll
-                for (int i = 0; i < FM; ++i) accs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accs[i], 0, 0, 0);
+                for (int i = 0; i < FM; ++i) accs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, af[i], accs[i], 0, 0, 0);
             }
         }
     };
@@ -432,12 +439,17 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         // form [R][64] or the k-major form [64][R]; NW waves share its wave-instructions
         auto gl_issue = [&](int st, int k0) {
             bf16* base = smem + st * GSTAGE;
-            auto op = [&](const bf16* X, int ld, int r0, int nrows, bool kmaj, int R, bf16* img) {
-                const int ninst = R * BK * 2 / 1024;  // 1 KiB per wave-instruction
-                for (int q = wid; q < ninst; q += WM * WN) {
+            auto op = [&](const bf16* X, int ld, int r0, int nrows, auto kmaj_c, auto R_c, bf16* img) {
+                constexpr bool kmaj = decltype(kmaj_c)::value;
+                constexpr int R = decltype(R_c)::value;
+                constexpr int ninst = R * BK * 2 / 1024, NW = WM * WN;  // 1 KiB per wave-instruction
+#pragma unroll
+                for (int qq = 0; qq < (ninst + NW - 1) / NW; ++qq) {  // (compile-time trip count)
+                    const int q = wid + qq * NW;
+                    if (ninst % NW != 0 && q >= ninst) break;
                     const int o = q * 1024 + 16 * lane;  // byte offset of this lane in the image
                     const bf16* src;
-                    if (kmaj) {
+                    if constexpr (kmaj) {
                         const int rb = 2 * R, kr = o / rb, w = o % rb, c = (w >> 6) ^ (R == 128 ? (kr & 3) : ((kr >> 1) & 1));
                         src = X + (size_t)(k0 + kr) * ld + r0 + c * 32 + ((w & 63) >> 1);
                     } else {
@@ -447,8 +459,9 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                     glds16(src, img + __builtin_amdgcn_readfirstlane(q) * 512);
                 }
             };
-            op(g.A, g.lda, m0, g.M, TNL, BM, base);
-            op(g.B, g.ldb, n0, g.N, BKN, BN, base + BM * BK);
+            op(g.A, g.lda, m0, g.M, std::integral_constant<bool, TNL>(), std::integral_constant<int, BM>(), base);
+            op(g.B, g.ldb, n0, g.N, std::integral_constant<bool, BKN>(), std::integral_constant<int, BN>(),
+               base + BM * BK);
         };
         if constexpr (GL == 1) {
             gl_issue(0, kb);
@@ -495,16 +508,12 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
 
     // ---- epilogue: lane owns column (lane&31), rows (t&3)+8(t>>2)+4(lane>>5)
     if constexpr (TNL) {
-        if (dosum && (lane & 31) == 0) {
+        if (dosum && lane < 32) {  // (C^T layout: every register of a lane holds its row's sum)
             float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int row = rbase + (t & 3) + 8 * (t >> 2);
-                    if (row < g.M) slab[(size_t)row * g.ldcf + g.sumc] = accs[i][t];
-                }
+                const int row = m0 + wm * TM + i * 32 + lane;
+                if (row < g.M) slab[(size_t)row * g.ldcf + g.sumc] = accs[i][0];
             }
         }
     }
@@ -515,6 +524,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         // layout (per-element global loads in that layout cost 2x the kernel's time)
         constexpr int YL = (RCH + NT - 1) / NT;
         uint4 yr[YL];
+        const bool yvec = (g.N % 8) == 0 && (g.ldyp % 8) == 0;  // (block-uniform: whole 16-B chunks)
 #pragma unroll
         for (int u = 0; u < YL; ++u) {
             const int c = tid + u * NT;
@@ -522,7 +532,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
             const int row = m0 + lr, col = n0 + lc;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (c < RCH && row < g.M && col < g.N) {
-                if (col + 8 <= g.N && (g.ldyp % 8) == 0) {
+                if (yvec) {
                     v = *(const uint4*)(g.yp + (size_t)row * g.ldyp + col);
                 } else {
                     bf16x8 t;
@@ -540,6 +550,110 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         }
         __syncthreads();
     }
+    // the tile's 16-byte output chunks: row-major C (cb) and transposed C^T (ct), from the
+    // bf16 tiles [BM][CS] / [BN][TS] in LDS
+    auto cb_out = [&]() {
+        for (int c = tid; c < RCH; c += NT) {
+            const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
+            const int row = m0 + lr, col = n0 + lc;
+            if (row >= g.M || col >= g.N || !PMLP_STORE_OK) continue;
+            const bf16* src = smem + lr * CS + lc;
+            if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
+                *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
+            } else {
+                for (int u = 0; u < 8 && col + u < g.N; ++u) g.cb[(size_t)row * g.ldcb + col + u] = src[u];
+            }
+        }
+    };
+    auto ct_out = [&]() {
+        for (int c = tid; c < RCH; c += NT) {
+            const int lc = c / (BM / 8), lr = (c % (BM / 8)) * 8;
+            const int col = n0 + lc, row = m0 + lr;
+            if (col >= g.N || row >= g.M || !PMLP_STORE_OK) continue;
+            const bf16* src = smem + lc * TS + lr;
+            if (row + 8 <= g.M && (g.ldct % 8) == 0) {
+                *(uint4*)(g.ct + (size_t)col * g.ldct + row) = *(const uint4*)src;
+            } else {
+                for (int u = 0; u < 8 && row + u < g.M; ++u) g.ct[(size_t)col * g.ldct + row + u] = src[u];
+            }
+        }
+    };
+    if constexpr (SW) {
+        // C^T accumulators: lane -> tile row lr0 + 32 i, columns lc0 + 32 j + 8 q + (0..3) in
+        // registers 4q..4q+3
+        const int lr0 = wm * TM + (lane & 31), lc0 = wn * TN + 4 * (lane >> 5);
+        if constexpr (PART) {
+            float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
+            const bool vec = (g.ldcf & 3) == 0;
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int row = m0 + lr0 + i * 32;
+                if (row >= g.M || !PMLP_STORE_OK) continue;
+                float* dst = slab + (size_t)row * g.ldcf;
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int col = n0 + lc0 + j * 32 + 8 * q;
+                        const float a[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                            acc[i][j][4 * q + 3]};
+                        if (vec && col + 4 <= g.N) {
+                            *(float4*)(dst + col) = make_float4(a[0], a[1], a[2], a[3]);
+                        } else {
+                            for (int u = 0; u < 4; ++u)
+                                if (col + u < g.N) dst[col + u] = a[u];
+                        }
+                    }
+            }
+        } else {  // BWD_DX: ELU' from the staged y tile, 4 columns per LDS read
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int lr = lr0 + i * 32, lc = lc0 + j * 32 + 8 * q;
+                        const bf16x4 yv = *(const bf16x4*)(smem + lr * CS + lc);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float y = (float)yv[u], v = acc[i][j][4 * q + u];
+                            acc[i][j][4 * q + u] = y > 0.f ? v : v * (y + 1.f);
+                        }
+                    }
+            __syncthreads();  // y tile consumed before the LDS is rewritten
+            if (g.cb) {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int lr = lr0 + i * 32, lc = lc0 + j * 32 + 8 * q;
+                            bf16x4 o;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) o[u] = (bf16)acc[i][j][4 * q + u];
+                            *(bf16x4*)(smem + lr * CS + lc) = o;
+                        }
+                __syncthreads();
+                cb_out();
+                if (g.ct) __syncthreads();
+            }
+            if (g.ct) {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                smem[(lc0 + j * 32 + 8 * q + u) * TS + lr0 + i * 32] = (bf16)acc[i][j][4 * q + u];
+                __syncthreads();
+                ct_out();
+            }
+        }
+        return;
+    }
     if (EPI == PMLP_EPI_FWD_HIDDEN) __syncthreads();  // LDS reuse
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -547,15 +661,8 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
         for (int j = 0; j < FN; ++j) {
             const int col = n0 + wn * TN + j * 32 + (lane & 31);
             const int rbase = m0 + wm * TM + i * 32 + 4 * (lane >> 5);
-            if (col >= g.N && (PART || EPI == PMLP_EPI_FWD_OUT)) continue;
-            if (PART) {
-                float* slab = g.cf + (size_t)slice * g.M * g.ldcf;
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int row = rbase + (t & 3) + 8 * (t >> 2);
-                    if (row < g.M && PMLP_STORE_OK) slab[(size_t)row * g.ldcf + col] = acc[i][j][t];
-                }
-            } else if (EPI == PMLP_EPI_FWD_OUT) {
+            if (col >= g.N && EPI == PMLP_EPI_FWD_OUT) continue;
+            if (EPI == PMLP_EPI_FWD_OUT) {
                 const float b = g.bias ? g.bias[col] : 0.f;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
@@ -563,26 +670,14 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                     if (row < g.M) g.cf[(size_t)row * g.ldcf + col] = acc[i][j][t] + b;
                 }
             } else {
-                // bias + ELU (forward) or ELU' (input gradient) in place; stored below
-                const float b = (EPI == PMLP_EPI_FWD_HIDDEN && g.bias && col < g.N) ? g.bias[col] : 0.f;
+                // bias + ELU in place; stored below
+                const float b = (g.bias && col < g.N) ? g.bias[col] : 0.f;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int row = rbase + (t & 3) + 8 * (t >> 2);
-                    float v = acc[i][j][t];
-                    if (EPI == PMLP_EPI_FWD_HIDDEN) {
-                        v = elu(v + b);
-                    } else {  // BWD_DX: d/dx ELU from its output y: 1 (y>0) or y+1
-                        const int lr = row - m0, lc = col - n0;
-                        const float y = (float)smem[lr * CS + lc];
-                        v = y > 0.f ? v : v * (y + 1.f);
-                    }
-                    acc[i][j][t] = v;
-                }
+                for (int t = 0; t < 16; ++t) acc[i][j][t] = elu(acc[i][j][t] + b);
             }
         }
     }
-    if (EPI == PMLP_EPI_FWD_HIDDEN || EPI == PMLP_EPI_BWD_DX) {
-        if (EPI == PMLP_EPI_BWD_DX) __syncthreads();  // y tile consumed before the LDS is rewritten
+    if (EPI == PMLP_EPI_FWD_HIDDEN) {
         if (g.cb) {
             // row-major: bf16 tile [BM][CS] in LDS, then 16-byte chunks along n
 #pragma unroll
@@ -597,17 +692,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                     }
                 }
             __syncthreads();
-            for (int c = tid; c < RCH; c += NT) {
-                const int lr = c / (BN / 8), lc = (c % (BN / 8)) * 8;
-                const int row = m0 + lr, col = n0 + lc;
-                if (row >= g.M || col >= g.N || !PMLP_STORE_OK) continue;
-                const bf16* src = smem + lr * CS + lc;
-                if (col + 8 <= g.N && (g.ldcb % 8) == 0) {
-                    *(uint4*)(g.cb + (size_t)row * g.ldcb + col) = *(const uint4*)src;
-                } else {
-                    for (int u = 0; u < 8 && col + u < g.N; ++u) g.cb[(size_t)row * g.ldcb + col + u] = src[u];
-                }
-            }
+            cb_out();
             if (g.ct) __syncthreads();  // the transposed tile reuses the LDS
         }
         if (g.ct) {
@@ -629,17 +714,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
                     }
                 }
             __syncthreads();
-            for (int c = tid; c < RCH; c += NT) {
-                const int lc = c / (BM / 8), lr = (c % (BM / 8)) * 8;
-                const int col = n0 + lc, row = m0 + lr;
-                if (col >= g.N || row >= g.M || !PMLP_STORE_OK) continue;
-                const bf16* src = smem + lc * TS + lr;
-                if (row + 8 <= g.M && (g.ldct % 8) == 0) {
-                    *(uint4*)(g.ct + (size_t)col * g.ldct + row) = *(const uint4*)src;
-                } else {
-                    for (int u = 0; u < 8 && row + u < g.M; ++u) g.ct[(size_t)col * g.ldct + row + u] = src[u];
-                }
-            }
+            ct_out();
         }
     }
 }
