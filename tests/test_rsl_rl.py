@@ -272,3 +272,14 @@ def test_fused_step_refuses_nets_deeper_than_the_adam_mirror():
     ppo = PPO(ActorCritic(6, 6, 3, hid, hid), device="cpu")
     with pytest.raises(ValueError, match="Linear layers"):
         fused_step.FusedPPOStep(ppo, 64)
+
+
+@pytest.mark.parametrize("hid,ok", [([32], True), ([16], True), ([12], False), ([20], False), ([28], False), ([40], False)])
+def test_fused_recurrent_covers_only_head_widths_the_kernels_take(hid, ok):
+    """pmlp_heads_forward / _backward take head hidden widths N0 <= 32 and a multiple of 8
+    (lstm_seq.hip heads_check): any other width must keep the autograd update (supported()
+    False) rather than build the fused step and fail at its first launch."""
+    from rsl_rl.algorithms import fused_recurrent
+    ac = ActorCriticRecurrent(47, 50, 12, actor_hidden_dims=hid, critic_hidden_dims=hid, rnn_type="lstm",
+                              rnn_hidden_size=64, rnn_num_layers=1)
+    assert fused_recurrent.supported(ac, 256, 4) is ok
