@@ -94,19 +94,34 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-# the committed rocprofv3 summaries of the current build (tools/gpu_round3_profile.sh)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "round3", "env_go2_4096")
+# the committed rocprofv3 summaries of the current build (tools/gpu_round4_profile.sh; the
+# round-3 set until the round-4 one is committed)
+PROFILE_DIR = next((d for d in (os.path.join(ROOT, "profiles", r, "env_go2_4096") for r in ("round4", "round3"))
+                    if os.path.exists(os.path.join(d, "pmc_k_step.json"))),
+                   os.path.join(ROOT, "profiles", "round3", "env_go2_4096"))
 
 
 def load_pmc():
     """HBM bytes per launch of the env-step kernel from the committed rocprofv3 PMC summary
-    (FETCH_SIZE / WRITE_SIZE in separate passes, each calibrated on a 1 GiB copy in the same
-    pass: tools/pmc_summary.py), or None."""
+    (FETCH_SIZE / WRITE_SIZE in separate passes: tools/pmc_summary.py), or None.  Where the
+    known-byte calibration of the I/O-only diagnostic build is committed
+    (traffic_calib.json, tools/traffic_calib.py: the counters' tally factor for this kernel's
+    own access pattern), its bytes are the traffic; else the 1 GiB-copy calibration's."""
     try:
         with open(os.path.join(PROFILE_DIR, "pmc_k_step.json")) as f:
-            return json.load(f)
+            d = json.load(f)
     except Exception:
         return None
+    try:
+        with open(os.path.join(PROFILE_DIR, "traffic_calib.json")) as f:
+            k = json.load(f)["k_step"]
+        d["copy_calibrated_bytes_per_launch"] = d.get("hbm_bytes_per_launch")
+        d["hbm_bytes_per_launch"] = k["hbm_bytes_per_launch"]
+        d["read_bytes_per_launch"], d["write_bytes_per_launch"] = k["read_bytes_per_launch"], k["write_bytes_per_launch"]
+        d["calibration"] = "known-byte I/O-only build (traffic_calib.json)"
+    except Exception:
+        d["calibration"] = "1 GiB copy in the same pass"
+    return d
 
 
 # VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per
@@ -464,7 +479,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc.get("hbm_bytes_per_launch"),
                      "traffic_read_write": [pmc.get("read_bytes_per_launch"), pmc.get("write_bytes_per_launch")],
-                     "traffic_profile_avg_ns": pmc.get("avg_ns"),
+                     "traffic_profile_avg_ns": pmc.get("avg_ns"), "traffic_calibration": pmc.get("calibration"),
+                     "traffic_profile": os.path.relpath(PROFILE_DIR, ROOT),
                      "kernel": pmc.get("kernel", "k_step (fused Go2 control step)"),
                      "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms)},
     }
