@@ -73,8 +73,9 @@ def load():
     if hasattr(lib, "lgs_get_contact_stats"):  # (absent only from pre-round-4 builds used in A/B timing)
         lib.lgs_get_contact_stats.argtypes = [vp, vp, C.c_int32]
         lib.lgs_get_contact_stats.restype = C.c_int
-    lib.lgs_get_instantiation.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
-    lib.lgs_get_instantiation.restype = C.c_int
+    if hasattr(lib, "lgs_get_instantiation"):  # (absent only from pre-round-4 builds used in A/B timing)
+        lib.lgs_get_instantiation.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.lgs_get_instantiation.restype = C.c_int
     for name in ("lgs_get_body_name", "lgs_get_dof_name"):
         getattr(lib, name).argtypes = [vp, C.c_int32]
         getattr(lib, name).restype = C.c_char_p
