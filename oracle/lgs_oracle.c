@@ -737,8 +737,11 @@ void orc_substep_env(const lgs_model_desc* md, const lgs_sim_params* sp, float* 
                 float lim = cmu[r / 3] * lam[r - 1];
                 float l1 = lam[r] - v[r] * inv[r];
                 float l2 = lam[r + 1] - v[r + 1] * inv[r + 1];
-                float nrm = sqrtf(l1 * l1 + l2 * l2);
-                if (nrm > lim) {
+                /* the cone test on squared norms: the square root (and the division) only when
+                   the friction impulse is projected back onto the cone (sliding) */
+                const float n2 = l1 * l1 + l2 * l2;
+                if (n2 > lim * lim) {
+                    const float nrm = sqrtf(n2);
                     float s = nrm > 0.f ? lim / nrm : 0.f;
                     l1 *= s; l2 *= s;
                 }

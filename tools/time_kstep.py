@@ -1,5 +1,7 @@
 """Time the fused env-step kernel (HIP events on its stream) for one or more builds.
-usage: python tools/time_kstep.py [task] [num_envs] [lib.so ...]   (default: the shipped build)"""
+usage: python tools/time_kstep.py [task] [num_envs] [lib.so ...]   (default: the shipped build)
+TIME_KSTEP_ACTIONS=zero: zero actions (the robots stand on their feet: the same contact set for
+every slot policy) instead of the default random flailing (0.5 N(0,1) actions, robots fall)"""
 import os
 import subprocess
 import sys
@@ -19,7 +21,8 @@ def run_one(task, n, lib):
     env, _ = task_registry.make_env(name=task, args=args)
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(0)
-    acts = [0.5 * torch.randn(n, env.num_actions, device="cuda", generator=g) for _ in range(8)]
+    scale = 0.0 if os.environ.get("TIME_KSTEP_ACTIONS") == "zero" else 0.5
+    acts = [scale * torch.randn(n, env.num_actions, device="cuda", generator=g) for _ in range(8)]
     for i in range(30):
         env.step(acts[i % 8])
     stream = torch.cuda.current_stream()
@@ -35,7 +38,7 @@ def run_one(task, n, lib):
         env.account_replayed_steps(1)
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in ev)
-    print(f"{task} n={n} lib={os.path.basename(lib or 'default')}: k_step median {ms[K // 2]:.4f} ms  "
+    print(f"{task} n={n} lib={os.path.basename(lib or 'default')} actions x{scale}: k_step median {ms[K // 2]:.4f} ms  "
           f"min {ms[0]:.4f}  -> {n / ms[K // 2] * 1e3:.3e} env-steps/s", flush=True)
 
 

@@ -528,7 +528,7 @@ __device__ __forceinline__ void uniform_solve(const float* b, const float (*L)[L
     }
 }
 
-template <int D, int B, int ROWS, int CH, int EPW>
+template <int D, int B, int ROWS, int CH, int EPW, bool PAD = false>
 __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const DevModel& md, const DevSim& sp,
                         float added_mass, float shape_mu) {
     constexpr int n = 6 + D;
@@ -741,7 +741,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
             const float* F = s.u.dyn.Fj[jc];
             const float cn[3] = {F[0], F[1], F[2]}, cf[3] = {F[3], F[4], F[5]};
             float val = dot3(Sw, cn) + dot3(Sv, cf);
-            if (jc == jr) val += jr < md.Dr ? sp.armature : 1.f;  // (a padded model's inert DOF: M_jj = 1)
+            if (jc == jr) val += (!PAD || jr < md.Dr) ? sp.armature : 1.f;  // (a padded model's inert DOF: M_jj = 1)
             m[cp] = ((mc.anc[jc] >> jr) & 1u) ? val : 0.f;
         }
         float Fn[3] = {s.u.dyn.cpk[bj][10 + 0], s.u.dyn.cpk[bj][10 + 1], s.u.dyn.cpk[bj][10 + 2]};
@@ -1275,9 +1275,13 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     pinv[r] = bc<EPW>(inv, r);
                 }
             for (int it = 0; it < sp.iters; ++it) {
+                // opaque row counts per sweep: the per-row guards are recomputed (one s_cmp
+                // each) instead of held across the sweeps as hoisted lane masks (SGPR spills)
+                int ncs = nc, ncgs = ncg, nls = nlimit, nos = nover;
+                asm volatile("" : "+v"(ncs), "+v"(ncgs), "+v"(nls), "+v"(nos));
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
-                    if (c < nc) {
+                    if (c < ncs) {
                         const int r = 3 * c;
                         const float lno = lamv[r], l1o = lamv[r + 1], l2o = lamv[r + 2];
                         const float vn = bc<EPW>(v, r), v1 = bc<EPW>(v, r + 1), v2 = bc<EPW>(v, r + 2);
@@ -1286,11 +1290,14 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                         v = fmaf(acol[r], dn, v);
                         const float v1n = fmaf(pa1[c], dn, v1);
                         const float v2n = fmaf(pa2[c], dn, v2);
-                        const float lim = (c < ncg ? mu : mus) * ln;
+                        const float lim = (c < ncgs ? mu : mus) * ln;
                         float l1 = l1o - v1n * pinv[r + 1];
                         float l2 = l2o - v2n * pinv[r + 2];
-                        const float nrm = sqrtf(l1 * l1 + l2 * l2);
-                        if (nrm > lim) {
+                        // cone test on squared norms (the oracle's): sqrt and division only
+                        // when the impulse is projected onto the cone
+                        const float n2 = l1 * l1 + l2 * l2;
+                        if (n2 > lim * lim) {
+                            const float nrm = sqrtf(n2);
                             const float sc = nrm > 0.f ? lim / nrm : 0.f;
                             l1 *= sc; l2 *= sc;
                         }
@@ -1301,7 +1308,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                 }
 #pragma unroll
                 for (int l = 0; l < LM; ++l) {
-                    if (l < nlimit) {
+                    if (l < nls) {
                         const int r = 3 * CM + l;
                         const float lo = lamv[r];
                         const float ln = fmaxf(0.f, lo + (ptg[r] - bc<EPW>(v, r)) * pinv[r]);
@@ -1309,13 +1316,16 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                         lamv[r] = ln;
                     }
                 }
-                if (nover > 0) {  // limits in the rows of unused contact slots (rare: their
-                                  // constants are broadcast per use, no registers held for them)
+                if (nos > 0) {  // limits in the rows of unused contact slots (rare: their
+                                  // constants are broadcast per use, no registers held for them;
+                                  // opaque copies keep LICM from hoisting the 2 x 3CM invariant
+                                  // broadcasts out of the sweep loop into live registers)
+                    const float tgo = tg, invo = inv;
 #pragma unroll
                     for (int r = 0; r < 3 * CM; ++r)
-                        if (r >= 3 * nc && r < 3 * nc + nover) {
+                        if (r >= 3 * ncs && r < 3 * ncs + nos) {
                             const float lo = lamv[r];
-                            const float ln = fmaxf(0.f, lo + (bc<EPW>(tg, r) - bc<EPW>(v, r)) * bc<EPW>(inv, r));
+                            const float ln = fmaxf(0.f, lo + (bc<EPW>(tgo, r) - bc<EPW>(v, r)) * bc<EPW>(invo, r));
                             v = fmaf(acol[r], ln - lo, v);
                             lamv[r] = ln;
                         }
@@ -1347,8 +1357,9 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     const float lim = (c < ncg ? mu : mus) * ln;
                     float l1 = l1o - v1n * bc<EPW>(inv, r + 1);
                     float l2 = l2o - v2n * bc<EPW>(inv, r + 2);
-                    const float nrm = sqrtf(l1 * l1 + l2 * l2);
-                    if (nrm > lim) {
+                    const float n2 = l1 * l1 + l2 * l2;
+                    if (n2 > lim * lim) {
+                        const float nrm = sqrtf(n2);
                         const float sc = nrm > 0.f ? lim / nrm : 0.f;
                         l1 *= sc; l2 *= sc;
                     }
@@ -1563,52 +1574,57 @@ __device__ void body_states(Smem<D, B, ROWS>& s, const ModelCache<D, B>& mc, flo
     }
 }
 
-template <int D, int B, int ROWS, int EPW>
+// PAD: the model may be padded to the kernel's shape (the generic instantiations); else its
+// sizes are the template's and every bound below is a compile-time constant
+template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ __forceinline__ void load_state(Smem<D, B, ROWS>& s, const DevState& st, const DevModel& md, int e) {
+    const int Dr = PAD ? md.Dr : D;
     const int lane = hl<EPW>();
     if (lane < 13) s.root[lane] = st.root[13 * e + lane];
     if (lane < 2 * D) {  // (a padded model's inert DOFs rest at 0)
-        const float v = lane < 2 * md.Dr ? st.dofs[(size_t)2 * md.Dr * e + lane] : 0.f;
+        const float v = lane < 2 * Dr ? st.dofs[(size_t)2 * Dr * e + lane] : 0.f;
         if (lane & 1) s.qd[lane >> 1] = v; else s.q[lane >> 1] = v;
     }
 }
-template <int D, int B, int ROWS, int EPW>
+template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ __forceinline__ void store_state(Smem<D, B, ROWS>& s, const DevState& st, const DevModel& md, int e) {
     int lane = hl<EPW>();
     asm volatile("" : "+v"(lane));  // recompute the lane indices here (no value kept live from load_state)
     if (lane < 13) st.root[13 * e + lane] = s.root[lane];
-    const int Dr = md.Dr, Br = md.Br;
+    const int Dr = PAD ? md.Dr : D, Br = PAD ? md.Br : B;
     if (lane < 2 * Dr) st.dofs[(size_t)2 * Dr * e + lane] = (lane & 1) ? s.qd[lane >> 1] : s.q[lane >> 1];
     for (int i = lane; i < 3 * Br; i += WAVE / EPW) st.cforce[(size_t)3 * Br * e + i] = (&s.cf[0][0])[i];
 }
 
 // ---------------------------------------------------------- kernels --------
-template <int D, int B, int ROWS, int CH>
+template <int D, int B, int ROWS, int CH, bool PAD = false>
 __global__ __launch_bounds__(WAVE) void k_simulate(DevModel md, DevSim sp, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
     __shared__ ModelCache<D, B> mc;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, md, e);
+    const int Dr = PAD ? md.Dr : D, Br = PAD ? md.Br : B;
+    load_state<D, B, ROWS, 1, PAD>(s, st, md, e);
     if (threadIdx.x < D)
-        s.tau[threadIdx.x] = threadIdx.x < md.Dr ? st.torques_in[(size_t)md.Dr * e + threadIdx.x] : 0.f;
+        s.tau[threadIdx.x] = threadIdx.x < Dr ? st.torques_in[(size_t)Dr * e + threadIdx.x] : 0.f;
     __syncthreads();
-    substep<D, B, ROWS, CH, 1>(&s, mc, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
-    store_state<D, B, ROWS, 1>(s, st, md, e);
-    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
+    substep<D, B, ROWS, CH, 1, PAD>(&s, mc, md, sp, st.added_mass ? st.added_mass[e] : 0.f, st.friction ? st.friction[e] : 1.f);
+    store_state<D, B, ROWS, 1, PAD>(s, st, md, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * Br * e, Br);
 }
 
-template <int D, int B, int ROWS, int CH>
+template <int D, int B, int ROWS, int CH, bool PAD = false>
 __global__ __launch_bounds__(WAVE) void k_fk(DevModel md, DevState st, int N) {
     __shared__ Smem<D, B, ROWS> s;
     __shared__ ModelCache<D, B> mc;
     const int e = xcd_env(blockIdx.x, gridDim.x);
     if (e >= N) return;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, md, e);
+    const int Br = PAD ? md.Br : B;
+    load_state<D, B, ROWS, 1, PAD>(s, st, md, e);
     __syncthreads();
-    body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
+    body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * Br * e, Br);
 }
 
 struct DevEnv {
@@ -1652,7 +1668,7 @@ __device__ __forceinline__ void resample_commands(const lgs_task_params& T, floa
 // lane 0 derives the base-frame state, commands and termination; then lane k
 // evaluates reward term k (all terms at once); lane 0 sums them in the reference's
 // (alphabetical) order, the same arithmetic as one lane summing term by term.
-template <int D, int B, int ROWS>
+template <int D, int B, int ROWS, bool PAD = false>
 __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                                              const float* rbs, int e, int id) {
     const int A = T.num_actions;
@@ -1664,7 +1680,7 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
     const float* cmd = s.u.post.misc + 12;
     const float* act = s.act;
     const float* last_act = E.last_actions + A * e;
-    const float* last_qd = E.last_dof_vel + A * e;
+    const float* last_qd = E.last_dof_vel + (PAD ? A : D) * e;
     float* air = E.feet_air_time + T.num_feet * e;
     uint8_t* lastc = E.last_contacts + T.num_feet * e;
     const float* tau = s.tau;
@@ -1775,7 +1791,7 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
     return r;
 }
 
-template <int D, int B, int ROWS, int EPW>
+template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                                     const float* rbs, int N, int e, uint32_t step) {
     const int lane = hl<EPW>();
@@ -1851,7 +1867,7 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
     __syncthreads();
     // rewards: lane k evaluates active term k (alphabetical order, legged_robot.py:770-787)
     if (lane < T.num_rewards) {
-        const float r = reward_term(s, T, E, rbs, e, T.reward_ids[lane]) * T.reward_scales[lane];
+        const float r = reward_term<D, B, ROWS, PAD>(s, T, E, rbs, e, T.reward_ids[lane]) * T.reward_scales[lane];
         s.u.post.terms[lane] = r;
         E.episode_sums[(size_t)lane * N + e] += r;
         if (E.rew_terms) E.rew_terms[(size_t)lane * N + e] = r;
@@ -1887,18 +1903,19 @@ enum { RESET_STEP = 0, RESET_ALL = 1, RESET_IDS = 2 };
 // the rest from the state the first part left in the env buffers (lgs_post_physics_finish)
 enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
 
-template <int D, int B, int ROWS, int EPW>
+template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                              const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL,
                              float* vsim = nullptr) {
     const int lane = hl<EPW>();
     const int A = T.num_actions;
+    const int Ad = PAD ? A : D;  // (unpadded: num_actions == D, a compile-time bound)
     const uint64_t seed = T.seed;
     const bool force_reset = reset_mode != RESET_STEP;
     if (force_reset) {
         if (lane == 0) s.flags[0] = 1;
     } else if (part != PART_FINISH) {
-        post_physics_scalar<D, B, ROWS, EPW>(s, T, E, rbs, N, e, step);
+        post_physics_scalar<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step);
         if (part == PART_REWARDS) return;
     } else if (lane == 0) {  // the first part's results: reset decision, base-frame state, commands
         s.flags[0] = E.reset[e];
@@ -1921,7 +1938,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
             s.q[lane] = T.default_dof_pos[lane] *
                         rand_range(0.5f, 1.5f, philox_uniform(seed, e, step, LGS_STREAM_RESET_DOF, lane));
             s.qd[lane] = 0.f;
-            if (lane < A) E.last_dof_vel[A * e + lane] = 0.f;
+            if (lane < Ad) E.last_dof_vel[Ad * e + lane] = 0.f;
         }
         if (lane < A) { act[lane] = 0.f; E.actions[A * e + lane] = 0.f; E.last_actions[A * e + lane] = 0.f; }
         if (lane < T.num_feet) E.feet_air_time[T.num_feet * e + lane] = 0.f;
@@ -1974,9 +1991,9 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
         for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[3 + i] * T.obs_scale_ang_vel;
         for (int i = 0; i < 3; ++i) tmp[k++] = s.u.post.misc[6 + i];
         for (int i = 0; i < 3; ++i) tmp[k++] = cmd[i] * T.commands_scale[i];
-        for (int j = 0; j < A; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
-        for (int j = 0; j < A; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
-        for (int j = 0; j < A; ++j) tmp[k++] = act[j];
+        for (int j = 0; j < Ad; ++j) tmp[k++] = (s.q[j] - T.default_dof_pos[j]) * T.obs_scale_dof_pos;
+        for (int j = 0; j < Ad; ++j) tmp[k++] = s.qd[j] * T.obs_scale_dof_vel;
+        for (int j = 0; j < Ad; ++j) tmp[k++] = act[j];
         if (T.obs_layout == LGS_OBS_HUMANOID) {
             float ph = 2.0f * 3.14159265358979323846f * s.u.post.misc[9];
             float sp_, cp_;
@@ -1998,7 +2015,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
             E.priv_obs[(size_t)P * e + i] = clipf(s.u.post.obs_tmp[i], -T.clip_observations, T.clip_observations);
     // bookkeeping (:707-709)
     if (lane < A) E.last_actions[A * e + lane] = act[lane];
-    if (lane < A) E.last_dof_vel[A * e + lane] = s.qd[lane];
+    if (lane < Ad) E.last_dof_vel[Ad * e + lane] = s.qd[lane];
     if (vsim && T.push_robots && lane < 2) {
         // last_root_vel[:, 0:2]: the all-env push draw whenever any env is pushed this step
         // (legged_robot.py:549-550, 709), which is nearly every step; the simulated values
@@ -2022,7 +2039,7 @@ enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MO
 // has N / 2 workgroups (N even) and every wave carries two envs.
 // WPE > 0: the waves/SIMD the build targets (the 48-row variant at <= 4096 envs takes 4:
 // one round of waves, worth its spills; 8192 envs run 3, fewer spills)
-template <int D, int B, int ROWS, int CH, int EPW, int WPE = 0>
+template <int D, int B, int ROWS, int CH, int EPW, int WPE = 0, bool PAD = false>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (EPW == 2 ? 2 : (ROWS <= 32 ? LGS_WAVES_PER_EU : LGS_WAVES_PER_EU_48))))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step, int mode) {
     __shared__ Smem<D, B, ROWS> sm[EPW];
@@ -2034,9 +2051,10 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     const lgs_task_params& T = *Tp;
     const int lane = hl<EPW>();
     load_model(mc, md);
-    load_state<D, B, ROWS, EPW>(s, st, md, e);
+    load_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
     const int A = T.num_actions;
-    float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * md.Br * e : nullptr;
+    const int Ad = PAD ? A : D, Br = PAD ? md.Br : B;  // (unpadded: compile-time bounds)
+    float* rbs = (T.write_body_states && st.rbs) ? st.rbs + (size_t)13 * Br * e : nullptr;
     STAMP_INIT();
     if (mode == MODE_STEP || mode == MODE_PHYSICS) {
         float a = 0.f;
@@ -2046,7 +2064,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
             E.actions[A * e + lane] = a;
             s.act[lane] = a;
         }
-        const float lqd = (lane < A) ? E.last_dof_vel[A * e + lane] : 0.f;
+        const float lqd = (lane < Ad) ? E.last_dof_vel[Ad * e + lane] : 0.f;
         const float am = st.added_mass ? st.added_mass[e] : 0.f;
         const float mu = st.friction ? st.friction[e] : 1.f;
         __syncthreads();
@@ -2062,7 +2080,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
             }
             __syncthreads();
 #ifndef LGS_DIAG_IO_ONLY
-            substep<D, B, ROWS, CH, EPW>(sm, mc, md, sp, am, mu);
+            substep<D, B, ROWS, CH, EPW, PAD>(sm, mc, md, sp, am, mu);
 #else
             // diagnostic build (never the shipped library): no physics, the step's global loads
             // and stores unchanged -- a known-byte calibration of the traffic counters
@@ -2070,30 +2088,30 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
 #endif
         }
         STAMP(0);
-        if (lane < A) E.torques[A * e + lane] = s.tau[lane];
+        if (lane < Ad) E.torques[Ad * e + lane] = s.tau[lane];
         // refresh_rigid_body_state (h1_env.py:49), humanoid tasks only: the rows they read
-        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs, md.Br, T.body_state_mask);
+        if (rbs) body_states<D, B, ROWS, EPW>(s, mc, rbs, Br, T.body_state_mask);
     } else {  // the physics half's outputs, as it stored them
         if (lane < A) s.act[lane] = E.actions[A * e + lane];
-        if (lane < D) s.tau[lane] = lane < A ? E.torques[A * e + lane] : 0.f;
+        if (lane < D) s.tau[lane] = lane < Ad ? E.torques[Ad * e + lane] : 0.f;
         for (int i = lane; i < 3 * B; i += WAVE / EPW)
-            (&s.cf[0][0])[i] = i < 3 * md.Br ? st.cforce[(size_t)3 * md.Br * e + i] : 0.f;
+            (&s.cf[0][0])[i] = i < 3 * Br ? st.cforce[(size_t)3 * Br * e + i] : 0.f;
     }
     __syncthreads();
     STAMP(15);
     if (mode != MODE_PHYSICS)
-        post_physics<D, B, ROWS, EPW>(s, T, E, rbs, N, e, step, RESET_STEP,
+        post_physics<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step, RESET_STEP,
                                       mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL),
                                       st.vsim);
     __syncthreads();
     STAMP(16);
-    store_state<D, B, ROWS, EPW>(s, st, md, e);
+    store_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
     STAMP(17);
     STAMP_FLUSH(e);
 }
 
 // reset_idx: every env (mask == NULL, BaseTask.reset) or the envs whose mask byte is set
-template <int D, int B, int ROWS, int CH>
+template <int D, int B, int ROWS, int CH, bool PAD = false>
 __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, const lgs_task_params* __restrict__ Tp,
                                                     lgs_env_buffers E, int N, uint32_t step, const uint8_t* mask) {
     __shared__ Smem<D, B, ROWS> s;
@@ -2103,14 +2121,15 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
     if (mask && !mask[e]) return;
     if (E.step_counter) step = (uint32_t)*E.step_counter;
     load_model(mc, md);
-    load_state<D, B, ROWS, 1>(s, st, md, e);
+    const int Br = PAD ? md.Br : B;
+    load_state<D, B, ROWS, 1, PAD>(s, st, md, e);
     if (threadIdx.x < 3 * B)
-        (&s.cf[0][0])[threadIdx.x] = threadIdx.x < 3 * md.Br ? st.cforce[(size_t)3 * md.Br * e + threadIdx.x] : 0.f;
+        (&s.cf[0][0])[threadIdx.x] = threadIdx.x < 3 * Br ? st.cforce[(size_t)3 * Br * e + threadIdx.x] : 0.f;
     __syncthreads();
-    post_physics<D, B, ROWS, 1>(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
+    post_physics<D, B, ROWS, 1, PAD>(s, *Tp, E, nullptr, N, e, step, mask ? RESET_IDS : RESET_ALL);
     __syncthreads();
-    store_state<D, B, ROWS, 1>(s, st, md, e);
-    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * md.Br * e, md.Br);
+    store_state<D, B, ROWS, 1, PAD>(s, st, md, e);
+    if (st.rbs) body_states<D, B, ROWS, 1>(s, mc, st.rbs + (size_t)13 * Br * e, Br);
 }
 
 // After k_step (one block): the extras of reset_idx (legged_robot.py:742-768) —
@@ -2240,12 +2259,13 @@ static bool extra_shape(const lgs_sim* s) {
 
 static Variant pick(const lgs_sim* s) {
     // 32-row humanoid variants (8 contacts): two envs per wave, as Go2
-    if (s->D == 12 && s->B <= 13 && s->rows <= 32) return V_12_13_32;
-    if (s->D == 10 && s->B <= 11 && s->rows <= 32) return V_10_11_32;
-    if (s->D == 12 && s->B <= 19 && s->rows <= 32) return V_12_19;
-    if (s->D == 12 && s->B <= 13) return V_12_13;
-    if (s->D == 12 && s->B <= 19) return V_12_19_48;
-    if (s->D == 10 && s->B <= 11) return V_10_11;
+    // (exact shapes only: these kernels take the model's sizes as compile-time bounds)
+    if (s->D == 12 && s->B == 13 && s->rows <= 32) return V_12_13_32;
+    if (s->D == 10 && s->B == 11 && s->rows <= 32) return V_10_11_32;
+    if (s->D == 12 && s->B == 19 && s->rows <= 32) return V_12_19;
+    if (s->D == 12 && s->B == 13) return V_12_13;
+    if (s->D == 12 && s->B == 19) return V_12_19_48;
+    if (s->D == 10 && s->B == 11) return V_10_11;
     if (extra_shape(s)) return V_EXTRA;
     return V_NONE;
 }
@@ -2301,20 +2321,20 @@ template <int D, int B>
 static void ex_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
                     lgs_env_buffers E, int N, uint32_t step, int mode) {
     // (2 waves/SIMD: the 29-row dense factorisation does not fit the 48-row default's 168 VGPRs)
-    hipLaunchKernelGGL((k_step<D, B, 48, 0, 1, 2>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, tp, E, N, step, mode);
+    hipLaunchKernelGGL((k_step<D, B, 48, 0, 1, 2, true>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, tp, E, N, step, mode);
 }
 template <int D, int B>
 static void ex_simulate(const lgs_sim* s, DevModel md, DevSim sp, DevState st, int N) {
-    hipLaunchKernelGGL((k_simulate<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, N);
+    hipLaunchKernelGGL((k_simulate<D, B, 48, 0, true>), dim3(N), dim3(WAVE), 0, s->stream, md, sp, st, N);
 }
 template <int D, int B>
 static void ex_fk(const lgs_sim* s, DevModel md, DevState st, int N) {
-    hipLaunchKernelGGL((k_fk<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, st, N);
+    hipLaunchKernelGGL((k_fk<D, B, 48, 0, true>), dim3(N), dim3(WAVE), 0, s->stream, md, st, N);
 }
 template <int D, int B>
 static void ex_reset(const lgs_sim* s, DevModel md, DevState st, const lgs_task_params* tp, lgs_env_buffers E, int N,
                      uint32_t step, const uint8_t* mask) {
-    hipLaunchKernelGGL((k_reset_all<D, B, 48, 0>), dim3(N), dim3(WAVE), 0, s->stream, md, st, tp, E, N, step, mask);
+    hipLaunchKernelGGL((k_reset_all<D, B, 48, 0, true>), dim3(N), dim3(WAVE), 0, s->stream, md, st, tp, E, N, step, mask);
 }
 static int extra_step(const lgs_sim* s, DevModel md, DevSim sp, DevState st, const lgs_task_params* tp,
                       lgs_env_buffers E, int N, uint32_t step, int mode) {
