@@ -2,12 +2,12 @@
 # A/B of two libppomlp.so builds on the captured Go2 PPO update, interleaved in separate
 # processes (A B A B), plus bitwise comparisons of the parameters after 3 updates: A vs A and
 # B vs B (run-to-run determinism), A vs B.
-# usage: tools/gpu_update_ab.sh libA.so libB.so   (log: gpurun_out/update_ab.log)
+# usage: [A_ENV='VAR=value ...'] tools/gpu_update_ab.sh libA.so libB.so   (log: gpurun_out/update_ab.log)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 A=$1; B=$2
 for rep in 1 2; do
-  PPOMLP_LIB=$A timeout -k 10 240 python tools/probes/update_time.py gpurun_out/upd_a$rep.npz >> gpurun_out/update_ab_full.log 2>&1 || exit 1
+  env $A_ENV PPOMLP_LIB=$A timeout -k 10 240 python tools/probes/update_time.py gpurun_out/upd_a$rep.npz >> gpurun_out/update_ab_full.log 2>&1 || exit 1
   PPOMLP_LIB=$B timeout -k 10 240 python tools/probes/update_time.py gpurun_out/upd_b$rep.npz >> gpurun_out/update_ab_full.log 2>&1 || exit 1
 done
 python - >> gpurun_out/update_ab.log 2>&1 <<'PY'

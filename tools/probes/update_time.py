@@ -1,7 +1,8 @@
 """Captured Go2 PPO update (4096 envs x 24 steps, 5 epochs x 4 mini-batches) with the
 libppomlp.so named by PPOMLP_LIB: median time of graph replays, and the parameters after
 3 updates from a fixed seed saved to argv[1] (for a bitwise comparison of two builds).
-Usage: PPOMLP_LIB=... python tools/probes/update_time.py out.npz"""
+Usage: PPOMLP_LIB=... python tools/probes/update_time.py out.npz
+(UPDATE_PER_LAYER_DW=1: one weight-gradient launch per layer, for builds limited to 4 GEMM jobs)"""
 import os
 import sys
 
@@ -25,6 +26,8 @@ for k in ("observations", "actions", "values", "returns", "advantages", "mu"):
     getattr(st, k).copy_(torch.randn(getattr(st, k).shape, device="cuda", generator=g))
 st.sigma.fill_(1.0)
 st.actions_log_prob.copy_(-12.0 + torch.randn(st.actions_log_prob.shape, device="cuda", generator=g))
+if os.environ.get("UPDATE_PER_LAYER_DW") == "1":  # a build from before the one-launch weight gradients
+    alg._fused.dw_one = False
 for _ in range(3):  # eager, then capture + replay
     st.step = T
     alg.update()
