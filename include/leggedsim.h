@@ -377,6 +377,13 @@ LGS_API int lgs_get_contact_stats(lgs_sim* sim, uint64_t* out, int32_t reset);
  * constraint-row capacity.  Any pointer may be NULL. */
 LGS_API int lgs_get_instantiation(lgs_sim* sim, int32_t* dofs, int32_t* bodies, int32_t* rows);
 
+/* the factorisation order of that instantiation: 0 = the joint-space Cholesky eliminates
+ * pivots in index order; CH > 0 = the model is D/CH equal chains of CH DOFs on the base and
+ * the chain-structured kernel eliminates the chains' pivots level by level (every base-row
+ * sum over the joint columns in level order; the CPU oracle takes it via
+ * orc_set_factor_chain to reproduce the step bit for bit). */
+LGS_API int lgs_get_factor_chain(lgs_sim* sim, int32_t* chain);
+
 /* diagnostics: per-phase s_memtime cycle sums [N][24] of the last lgs_step
  * (only in a library built with -DLGS_PHASE_STAMPS; otherwise LGS_ERR_STATE) */
 LGS_API int lgs_debug_set_phase_buffer(void* dev_ptr);

@@ -103,9 +103,10 @@ def set_self_collision(lib, sc=None):
 
 
 def set_env(lib, env):
-    """Ground and self-collision of a live env."""
+    """Ground, self-collision and Cholesky elimination order of a live env's sim."""
     set_ground(lib, getattr(env, "terrain", None), env.cfg.terrain)
     set_self_collision(lib, getattr(env, "self_collision", None))
+    lib.orc_set_factor_chain(env.sim.factor_chain())
 
 
 def step(env, snap, actions, step_counter, lib=None):

@@ -296,22 +296,49 @@ static void fk(const lgs_model_desc* md, const float* root13, const float* dofq,
     }
 }
 
+static int g_factor_chain;  /* 0: ascending reduction order; CH > 0: level order (below) */
+
+/* The factorisation order of the HIP instantiation that runs this model
+ * (lgs_get_factor_chain): its chain-structured variants eliminate the joint pivots level
+ * by level (k = t, CH+t, 2CH+t, .. for t = 0..CH-1, then the base), so every sum below
+ * runs over the earlier columns in that order.  Set per model by test infrastructure. */
+void orc_set_factor_chain(int ch) { g_factor_chain = ch; }
+
 /* dense Cholesky in place (lower), n <= NMAX.  The reciprocal of each pivot is taken
  * once (IEEE 1/d) and every division by L_kk -- here and in the triangular solves --
  * is a multiplication by it: the HIP kernel's arithmetic, operation for operation
  * (one division per pivot instead of five on its serial chain).  Every update is one
  * fused multiply-add (fmaf), as in the kernel (both build with -ffp-contract=off). */
 static void cholesky(float* M, float* invd, int n) {
+    /* reduction order: joint columns by level, then the base columns ascending (with the
+     * default 0: plain ascending).  Columns of other chains contribute exact zeros, so
+     * only the order of the base rows' sums differs between the two. */
+    int ord[NMAX];
+    const int D = n - 6, ch = g_factor_chain;
+    int q = 0;
+    if (ch > 0 && D % ch == 0) {
+        for (int t = 0; t < ch; ++t)
+            for (int c = 0; c < D / ch; ++c) ord[q++] = c * ch + t;
+        for (int s = D; s < n; ++s) ord[q++] = s;
+    } else {
+        for (int s = 0; s < n; ++s) ord[q++] = s;
+    }
     for (int k = 0; k < n; ++k) {
         float d = M[k * NMAX + k];
-        for (int s = 0; s < k; ++s) d = fmaf(-M[k * NMAX + s], M[k * NMAX + s], d);
+        for (int o = 0; o < n; ++o) {
+            const int s = ord[o];
+            if (s < k) d = fmaf(-M[k * NMAX + s], M[k * NMAX + s], d);
+        }
         d = sqrtf(fmaxf(d, 1e-12f));
         const float inv = 1.0f / d;
         M[k * NMAX + k] = d;
         invd[k] = inv;
         for (int i = k + 1; i < n; ++i) {
             float v = M[i * NMAX + k];
-            for (int s = 0; s < k; ++s) v = fmaf(-M[i * NMAX + s], M[k * NMAX + s], v);
+            for (int o = 0; o < n; ++o) {
+                const int s = ord[o];
+                if (s < k) v = fmaf(-M[i * NMAX + s], M[k * NMAX + s], v);
+            }
             M[i * NMAX + k] = v * inv;
         }
     }

@@ -757,8 +757,50 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
     // in the solves below is a multiplication by it (the oracle's arithmetic).  Lane k
     // keeps 1/L_kk in idg.
     float idg = 0.f;
+    // With CH > 0 the joint pivots run level by level: the NC chains' pivots at depth t
+    // (k = c*CH + t) are independent (column k is nonzero only on its own chain and the
+    // base rows), so each pivot lane takes the square root and reciprocal of its own
+    // diagonal and the NC reciprocals are broadcast together, one dependent
+    // sqrt -> rcp -> broadcast -> fma step per level instead of per pivot.  Every base
+    // row then receives the leg terms in LEVEL order (k = t, CH+t, 2CH+t, .. for
+    // t = 0..CH-1); the oracle's cholesky() sums in that order for these instantiations
+    // (orc_set_factor_chain).  The base pivots D..n-1 follow one by one.
+    constexpr int K0 = CH > 0 ? D : 0;
+    if constexpr (CH > 0) {
+        constexpr int NC = D / CH;
 #pragma unroll
-    for (int k = 0; k < n; ++k) {
+        for (int t = 0; t < CH; ++t) {
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            float dg = 1.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) dg = ln == c * CH + t ? m[c * CH + t] : dg;
+            const float dl = sqrtf(fmaxf(dg, 1e-12f));
+            const float il = 1.0f / dl;
+            float ic[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) ic[c] = bc<EPW>(il, c * CH + t);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int k = c * CH + t;
+                m[k] = ln == k ? dl : m[k] * ic[c];
+                idg = ln == k ? il : idg;
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int k = c * CH + t;
+#pragma unroll
+                for (int j = k + 1; j < n; ++j) {
+                    if (!l_nz<D, CH>(j, k)) continue;
+                    const float ljk = bc<EPW>(m[k], j);
+                    m[j] = fmaf(-m[k], ljk, m[j]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int k = K0; k < n; ++k) {
         // opaque per step: lane masks are recomputed here (one v_cmp each) instead of
         // being CSE'd across the factorisation and solves, where ~70 live mask SGPRs
         // spilled to VGPR lanes
@@ -2920,6 +2962,13 @@ LGS_API int lgs_get_instantiation(lgs_sim* s, int32_t* dofs, int32_t* bodies, in
     if (dofs) *dofs = s->Dt;
     if (bodies) *bodies = s->Bt;
     if (rows) *rows = variant_rows(pick(s));
+    return LGS_OK;
+}
+
+LGS_API int lgs_get_factor_chain(lgs_sim* s, int32_t* chain) {
+    if (!s || !chain) return set_err(LGS_ERR_ARG, "null argument");
+    const Variant v = pick(s);
+    *chain = (v != V_EXTRA && v != V_NONE && s->chain == variant_chain(v)) ? variant_chain(v) : 0;
     return LGS_OK;
 }
 

@@ -238,6 +238,8 @@ def load_oracle(path=None):
     lib.orc_terrain_sample.restype = C.c_float
     lib.orc_set_self_collision.argtypes = [C.POINTER(SelfCollisionDesc)]
     lib.orc_set_self_collision.restype = None
+    lib.orc_set_factor_chain.argtypes = [C.c_int]
+    lib.orc_set_factor_chain.restype = None
     lib.orc_contact_stats.argtypes = [vp, C.c_int]
     lib.orc_contact_stats.restype = None
     return lib

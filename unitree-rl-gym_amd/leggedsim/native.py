@@ -76,6 +76,9 @@ def load():
     if hasattr(lib, "lgs_get_instantiation"):  # (absent only from pre-round-4 builds used in A/B timing)
         lib.lgs_get_instantiation.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         lib.lgs_get_instantiation.restype = C.c_int
+    if hasattr(lib, "lgs_get_factor_chain"):
+        lib.lgs_get_factor_chain.argtypes = [vp, C.POINTER(C.c_int32)]
+        lib.lgs_get_factor_chain.restype = C.c_int
     for name in ("lgs_get_body_name", "lgs_get_dof_name"):
         getattr(lib, name).argtypes = [vp, C.c_int32]
         getattr(lib, name).restype = C.c_char_p
@@ -105,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
     "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
-    "lgs_get_contact_stats", "lgs_get_instantiation",
+    "lgs_get_contact_stats", "lgs_get_instantiation", "lgs_get_factor_chain",
 ]
 
 
@@ -225,6 +228,15 @@ class Sim:
         check(self.lib, self.lib.lgs_get_instantiation(self.handle, C.byref(d), C.byref(b), None),
               "lgs_get_instantiation")
         return d.value, b.value
+
+    def factor_chain(self):
+        """The chain length the kernel's Cholesky eliminates level by level (0: index order);
+        pre-level-order builds (A/B timing only) report 0."""
+        if not hasattr(self.lib, "lgs_get_factor_chain"):
+            return 0
+        ch = C.c_int32()
+        check(self.lib, self.lib.lgs_get_factor_chain(self.handle, C.byref(ch)), "lgs_get_factor_chain")
+        return ch.value
 
     # name queries (gym.get_asset_rigid_body_names / get_asset_dof_names /
     # find_actor_rigid_body_handle, legged_robot.py:342-343, 388-407)
