@@ -772,6 +772,15 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         for (int t = 0; t < CH; ++t) {
             int ln = lane;
             asm volatile("" : "+v"(ln));
+            // the level's column entries, broadcast UNSCALED ahead of the square roots (off
+            // the pivot chain); L_jk = raw * (1/L_kk) in the receiving lane is the product
+            // lane j would form, so the same bits
+            float raw[NC][n];
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int j = c * CH + t + 1; j < n; ++j)
+                    if (l_nz<D, CH>(j, c * CH + t)) raw[c][j] = bc<EPW>(m[c * CH + t], j);
             float dg = 1.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c) dg = ln == c * CH + t ? m[c * CH + t] : dg;
@@ -792,7 +801,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
                 for (int j = k + 1; j < n; ++j) {
                     if (!l_nz<D, CH>(j, k)) continue;
-                    const float ljk = bc<EPW>(m[k], j);
+                    const float ljk = raw[c][j] * ic[c];
                     m[j] = fmaf(-m[k], ljk, m[j]);
                 }
             }
@@ -806,6 +815,11 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         // spilled to VGPR lanes
         int ln = lane;
         asm volatile("" : "+v"(ln));
+        // the column's entries broadcast unscaled, in flight with the diagonal's (as above)
+        float raw[n];
+#pragma unroll
+        for (int j = k + 1; j < n; ++j)
+            if (l_nz<D, CH>(j, k)) raw[j] = bc<EPW>(m[k], j);
         const float d = sqrtf(fmaxf(bc<EPW>(m[k], k), 1e-12f));
         const float inv = 1.0f / d;
         // Lanes above the diagonal (i < k, i < j) update their upper-triangle registers
@@ -816,7 +830,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
 #pragma unroll
         for (int j = k + 1; j < n; ++j) {
             if (!l_nz<D, CH>(j, k)) continue;  // L_jk == 0: no update (compile-time after unrolling)
-            const float ljk = bc<EPW>(m[k], j);
+            const float ljk = raw[j] * inv;
             m[j] = fmaf(-m[k], ljk, m[j]);  // fused, as the oracle's cholesky()
         }
         __builtin_amdgcn_sched_barrier(0);
