@@ -49,6 +49,7 @@ def test_h1_ankles_locked_runs_padded_and_matches_oracle_bitwise(locked, n):
                   env__num_privileged_obs=14 + 3 * D)
     assert env.num_dof == D and env.num_bodies == 11
     assert env.sim.padded_shape() == (16, 24)
+    assert env.sim.factor_chain() == 0  # dense instantiation: index-order Cholesky (the oracle's default)
     fused_vs_oracle(env, g, 3, f"h1 ankles locked x{n}")
 
 

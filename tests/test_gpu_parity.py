@@ -292,6 +292,9 @@ def fused_vs_oracle(env, g, steps, what):
 @pytest.mark.parametrize("task", TASKS)
 def test_fused_step_matches_oracle_bitwise(task):
     env, g = warm(task, 512)
+    # the chain-structured instantiations eliminate the chains' joint pivots level by level;
+    # bridge.step hands that order to the oracle (orc_set_factor_chain)
+    assert env.sim.factor_chain() == {"go2": 3, "h1": 5, "g1": 6, "h1_2": 6}[task]
     fused_vs_oracle(env, g, 3, task)
 
 
