@@ -353,6 +353,24 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
                                 float clip, int32_t clipped_value, float vcoef, float ecoef, float* partial,
                                 float* stats, float* dstd, pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap,
                                 pmlp_bf16* dvalue, pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
+/* The update's forward and this loss step in ONE launch (rsl_rl PPO.update: evaluate + the
+ * loss + its backward to the output layer): pmlp_mlp_forward of job 0 = the actor (A outputs,
+ * ldo = A) and job 1 = the critic (1 output, ldo = 1), then, in the same workgroup on its 96
+ * rows, pmlp_ppo_loss_step's per-row arithmetic and outputs on mu = jobs[0].out, value =
+ * jobs[1].out, with the per-workgroup partials only (the folded form: pmlp_reduce_slabs_step
+ * finishes the loss over pmlp_mlp_forward_ppo_loss_parts(M, A) / (3 + A) partial rows; the
+ * partials sum 96-row groups, so the logged losses and the std gradient round differently
+ * from the 64-row groups of pmlp_ppo_loss_step).  Applies when
+ * pmlp_mlp_forward_ppo_loss_parts(M, A) > 0 (M >= 18432, A a multiple of 4 <= 16) and
+ * Ap <= 16, a multiple of 4; replaces PPO.update's separate forward and loss launches.   */
+PMLP_API int32_t pmlp_mlp_forward_ppo_loss_parts(int32_t M, int32_t A);
+PMLP_API int pmlp_mlp_forward_ppo_loss(const pmlp_mlp_fwd_job* jobs, int32_t M, const float* stdv,
+                                       const float* actions, const float* old_logp, const float* old_mu,
+                                       const float* old_sigma, const float* adv, const float* ret,
+                                       const float* target, const int64_t* rows, int32_t A, float clip,
+                                       int32_t clipped_value, float vcoef, float ecoef, float* partial,
+                                       pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap, pmlp_bf16* dvalue,
+                                       pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
 /* The same step with fp32 output gradients dmu [M, A] (16-byte aligned when A % 4 == 0) and
  * dvalue [M] (the recurrent heads' fp32 backward, pmlp_heads_backward).                */
 PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const float* value, const float* actions,

@@ -1366,9 +1366,20 @@ __global__ __launch_bounds__(64) void k_ppo_loss_step_reg(LossArgs a, LossStepOu
 // summed per wave (rows in xor order), then over the 4 waves in order (deterministic; the
 // same partials layout as k_ppo_loss_step_reg: one record of 3 + A per 64 rows).
 // Needs A % 4 == 0, A <= 16, Ap <= 16 and Ap % 4 == 0.
-__global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut o) {
-    __shared__ float c_h[16], c_i2[16], c_i3[16], c_i1[16], c_lg[16], c_sg[16];
-    __shared__ float wpart[4][3 + 16];
+// The quad-lane loss on rows i0 .. i0 + 16 NWV - 1: four lanes per row (each owning 4 actions),
+// 16 rows per wave, NWV waves (threads past 64 NWV join the barriers only); the per-wave sums
+// are added in a fixed order into partial row `part`.  sh: LDS scratch of >= 96 + 19 NWV floats.
+// k_ppo_loss_step_q (NWV = 4, 64 rows per workgroup) and the update forward's epilogue
+// (k_mlp_fwd<96, .., LOSS>: NWV = 6, the workgroup's 96 rows) run it.
+template <int NWV>
+__device__ __forceinline__ void loss_quad_rows(const LossArgs& a, const LossStepOut& o, int i0, int part, float* sh) {
+    float* const c_h = sh;
+    float* const c_i2 = sh + 16;
+    float* const c_i3 = sh + 32;
+    float* const c_i1 = sh + 48;
+    float* const c_lg = sh + 64;
+    float* const c_sg = sh + 80;
+    float(*const wpart)[3 + 16] = (float(*)[3 + 16])(sh + 96);
     const int A = a.A, W = 3 + A, tid = threadIdx.x, q = tid & 3, k0 = 4 * q;
     if (tid < A) {
         const float sg = a.stdv[tid];
@@ -1380,8 +1391,8 @@ __global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut
         c_lg[tid] = logf(sg);
     }
     __syncthreads();
-    const int i = blockIdx.x * 64 + (tid >> 2);
-    const bool valid = i < a.M;
+    const int i = i0 + (tid >> 2);
+    const bool valid = tid < 64 * NWV && i < a.M;
     const bool own = k0 < A;  // quad-uniform per lane, same for every row
     const size_t si = valid ? a.src(i) : 0;
     float d[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1474,17 +1485,27 @@ __global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut
         c[u] = rsum(valid && own ? dlogp * (d[u] * d[u] * c_i3[k] - c_i1[k]) : 0.f);
     }
     const int w = tid >> 6, lane = tid & 63;
-    if (lane == 0) {
+    if (lane == 0 && w < NWV) {
         wpart[w][0] = surr;
         wpart[w][1] = vl;
         wpart[w][2] = kl;
     }
-    if (lane < 4 && own) {
+    if (lane < 4 && own && w < NWV) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) wpart[w][3 + k0 + u] = c[u];
     }
     __syncthreads();
-    if (tid < W) o.partial[(size_t)blockIdx.x * W + tid] = (wpart[0][tid] + wpart[1][tid]) + (wpart[2][tid] + wpart[3][tid]);
+    if (tid < W) {
+        float x = (wpart[0][tid] + wpart[1][tid]) + (wpart[2][tid] + wpart[3][tid]);
+#pragma unroll
+        for (int v = 4; v < NWV; v += 2) x += wpart[v][tid] + wpart[v + 1][tid];
+        o.partial[(size_t)part * W + tid] = x;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ppo_loss_step_q(LossArgs a, LossStepOut o) {
+    __shared__ float sh[96 + 4 * 19];
+    loss_quad_rows<4>(a, o, blockIdx.x * 64, blockIdx.x, sh);
 }
 
 // stats = [surrogate_loss, value_loss, kl_mean, entropy_mean]; dstd[k] incl. the entropy term.
@@ -1890,8 +1911,11 @@ __device__ void roll_epilogue(const FmlpJob& J, int jj, const RollStep& rs, int 
     }
 }
 
-template <int R, bool ROLL = false>
-__global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M, RollStep rs) {
+// LOSS: the update's PPO loss on the workgroup's rows after both nets (loss_quad_rows; the
+// workgroup runs every job, gridDim.y == 1), its partial sums in row blockIdx.x
+template <int R, bool ROLL = false, bool LOSS = false>
+__global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M, RollStep rs, LossArgs la = {},
+                                                         LossStepOut lo = {}) {
     // y0 (then y2) and x (then y1); row strides 8 elements past the width: ds_read_b128
     // fragment reads of 32 consecutive rows hit 4-bank groups 4 apart (conflict-free)
     constexpr int LD0 = FMLP_MAX_H0 + 8, LD1 = FMLP_MAX_H1 + 8;
@@ -1957,6 +1981,9 @@ __global__ __launch_bounds__(FMLP_THREADS) void k_mlp_fwd(FmlpJobs jobs, int M, 
         FMLP_STAMP(sb + 8);
         if constexpr (ROLL) roll_epilogue<R>(J, jj, rs, r0, M, (float*)Y1);  // (one job per workgroup)
     }
+    // both nets' outputs of these rows are in global memory (written by this workgroup before
+    // the barrier that ended the last job); Y1 is dead
+    if constexpr (LOSS) loss_quad_rows<R / 16>(la, lo, r0, blockIdx.x, (float*)Y1);
 }
 
 // ----------------------------------------------------------------- GAE --
@@ -2799,6 +2826,37 @@ PMLP_API int pmlp_ppo_loss_step(const float* mu, const float* stdv, const float*
         return fail(-1, "pmlp_ppo_loss_step: null output or padded width too small");
     LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp, nullptr, nullptr};
     return loss_step_launch(a, o, M, A, Ap, partial, stats, dstd, stream);
+}
+
+PMLP_API int32_t pmlp_mlp_forward_ppo_loss_parts(int32_t M, int32_t A) {
+    return (M >= 96 * 192 && A > 0 && A % 4 == 0 && A <= 16) ? ((M + 95) / 96) * (3 + A) : 0;
+}
+
+PMLP_API int pmlp_mlp_forward_ppo_loss(const pmlp_mlp_fwd_job* jobs, int32_t M, const float* stdv,
+                                       const float* actions, const float* old_logp, const float* old_mu,
+                                       const float* old_sigma, const float* adv, const float* ret,
+                                       const float* target, const int64_t* rows, int32_t A, float clip,
+                                       int32_t clipped_value, float vcoef, float ecoef, float* partial,
+                                       pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap, pmlp_bf16* dvalue,
+                                       pmlp_bf16* dvalue_t, int32_t Vp, void* stream) {
+    FmlpJobs fj;
+    if (int e = fmlp_pack(2, jobs, M, fj)) return e;
+    if (pmlp_mlp_forward_ppo_loss_parts(M, A) <= 0 || Ap > 16 || Ap % 4)
+        return fail(-1, "pmlp_mlp_forward_ppo_loss: M >= 18432 rows, A a multiple of 4 <= 16, Ap <= 16");
+    if (jobs[0].N[3] != A || jobs[0].ldo != A || jobs[1].N[3] != 1 || jobs[1].ldo != 1)
+        return fail(-1, "pmlp_mlp_forward_ppo_loss: job 0 is the actor (A outputs), job 1 the critic (1), dense");
+    LossArgs a;
+    if (int e = loss_args(a, jobs[0].out, stdv, jobs[1].out, actions, old_logp, old_mu, old_sigma, adv, ret, target,
+                          rows, M, A, clip, clipped_value, vcoef, ecoef))
+        return e;
+    if (!partial || !dmu || !dvalue || Ap < A || Vp < 1)
+        return fail(-1, "pmlp_mlp_forward_ppo_loss: null output or padded width too small");
+    LossStepOut o{partial, (bf16*)dmu, (bf16*)dmu_t, (bf16*)dvalue, (bf16*)dvalue_t, Ap, Vp, nullptr, nullptr};
+    const RollStep none{};
+    hipLaunchKernelGGL((k_mlp_fwd<96, false, true>), dim3((M + 95) / 96, 1), dim3(FMLP_THREADS), 0,
+                       (hipStream_t)stream, fj, M, none, a, o);
+    PMLP_CHECK_LAUNCH("pmlp_mlp_forward_ppo_loss");
+    return 0;
 }
 
 PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const float* value, const float* actions,

@@ -25,6 +25,8 @@ of the flat moments.  With torch.distributed the gradient (and the statistics
 tail) is all-reduced as one bucket and averaged inside the kernels.
 """
 
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -154,6 +156,14 @@ class FusedPPOStep:
         self.fold_opt = self.fold_loss and covered == self.n and all(d is None for ds in self.dw_stage for d in ds)
         self.norm_partial = torch.empty(16384, device=dev) if self.fold_opt else None
         self.nparts = 0
+        # the loss in the forward's launch (pmlp_mlp_forward_ppo_loss: 96-row partials, fewer
+        # than pmlp_ppo_loss_step's 64-row ones, so loss_partial holds them) where it applies
+        lib = mm.load()
+        fl_parts = lib.pmlp_mlp_forward_ppo_loss_parts(M, A) if hasattr(lib, "pmlp_mlp_forward_ppo_loss") else 0
+        Ap = self.dz_out[0].shape[1]
+        self.fused_loss = bool(self.fused_fwd and self.fold_loss and 0 < fl_parts <= self.loss_partial.numel()
+                               and Ap <= 16 and Ap % 4 == 0 and os.environ.get("PMLP_FUSED_LOSS", "1") != "0")
+        self.loss_nb = (fl_parts if self.fused_loss else self.loss_partial.numel()) // (3 + A)
 
     # -------------------------------------------------------- optimizer state --
     def sync_optimizer_state(self, opt):
@@ -206,14 +216,22 @@ class FusedPPOStep:
         #    (the previous Adam step wrote them)
         xb = [self.xb[0], self.xb[0] if shared else self.xb[1]]
         fobs = [obs, cobs]
-        # 2. forward
+        # 2. forward (and, where it applies, 3. in the same launch)
+        A = self.out[0].shape[1]
+        std = ac.std.detach()
+        st = mm._stream()
+        P = mm._p
         if self.fused_fwd:
+            loss = (P(std), P(actions), P(logp), P(mu_old), P(sigma_old), P(adv), P(ret), P(values), P(rows), A,
+                    float(alg.clip_param), int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
+                    float(alg.entropy_coef), P(self.loss_partial), P(self.dz_out[0]), None, self.dz_out[0].shape[1],
+                    P(self.dz_out[1]), None, self.dz_out[1].shape[1], st) if self.fused_loss else None
             mm.mlp_forward([dict(x=fobs[n], kx=self.lins[n][0].in_features, rows=rows,
                                  xa=self.xb[n] if (n == 0 or not shared) else None, K0=self.k0p[n],
                                  W=self.wb[n], Wf=self.wf[n] if self.wf else None,
                                  b=[lin.bias.detach() for lin in self.lins[n]],
                                  N=[lin.out_features for lin in self.lins[n]], y=self.y[n], out=self.out[n])
-                            for n in range(2)], M)
+                            for n in range(2)], M, loss=loss)
         for l in range(L if not self.fused_fwd else 0):
             last = l == L - 1
             gj = []
@@ -233,18 +251,15 @@ class FusedPPOStep:
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
         # 3. loss forward + backward in one pass (rollout inputs read through `rows`); the
         #    output gradients land directly in the backward's bf16 operands
-        A = self.out[0].shape[1]
-        std = ac.std.detach()
-        st = mm._stream()
-        P = mm._p
-        mm._ok(lib.pmlp_ppo_loss_step(P(self.out[0]), P(std), P(self.out[1]), P(actions), P(logp), P(mu_old),
-                                      P(sigma_old), P(adv), P(ret), P(values), P(rows), M, A, float(alg.clip_param),
-                                      int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
-                                      float(alg.entropy_coef), P(self.loss_partial),
-                                      None if self.fold_loss else P(self.stats),
-                                      None if self.fold_loss else P(self._gview[id(ac.std)]),
-                                      P(self.dz_out[0]), None, self.dz_out[0].shape[1], P(self.dz_out[1]), None,
-                                      self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
+        if not self.fused_loss:
+            mm._ok(lib.pmlp_ppo_loss_step(P(self.out[0]), P(std), P(self.out[1]), P(actions), P(logp), P(mu_old),
+                                          P(sigma_old), P(adv), P(ret), P(values), P(rows), M, A, float(alg.clip_param),
+                                          int(bool(alg.use_clipped_value_loss)), float(alg.value_loss_coef),
+                                          float(alg.entropy_coef), P(self.loss_partial),
+                                          None if self.fold_loss else P(self.stats),
+                                          None if self.fold_loss else P(self._gview[id(ac.std)]),
+                                          P(self.dz_out[0]), None, self.dz_out[0].shape[1], P(self.dz_out[1]), None,
+                                          self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
         #    (dW_l beside dX_l on a second stream measured slower: the two latency-bound
         #    GEMMs contend)
@@ -278,7 +293,7 @@ class FusedPPOStep:
         dkl = float(alg.desired_kl if alg.desired_kl is not None else 0.0)
         fold_opt = self.fold_opt and alg.world_size == 1
         if self.fold_loss:
-            rs = mm.ReduceStep(P(self.loss_partial), self.loss_partial.numel() // (3 + A), A, M,
+            rs = mm.ReduceStep(P(self.loss_partial), self.loss_nb, A, M,
                                float(alg.entropy_coef), P(std), P(self.stats), P(self._gview[id(ac.std)]),
                                P(self.norm_partial) if fold_opt else None, P(self.step_t), P(alg._lr), P(acc), dkl,
                                adaptive, self.norm_partial.numel() if fold_opt else 0)

@@ -137,6 +137,11 @@ def load():
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
+        if hasattr(L, "pmlp_mlp_forward_ppo_loss"):  # (absent from builds before round 4's end)
+            L.pmlp_mlp_forward_ppo_loss_parts.argtypes = [i32, i32]
+            L.pmlp_mlp_forward_ppo_loss_parts.restype = i32
+            L.pmlp_mlp_forward_ppo_loss.argtypes = [C.POINTER(MlpFwdJob), i32] + [vp] * 9 + \
+                [i32, f32, i32, f32, f32, vp, vp, vp, i32, vp, vp, i32, vp]
         L.pmlp_rollout_forward.argtypes = [C.POINTER(MlpFwdJob), i32, C.POINTER(RolloutStep), vp]
         L.pmlp_ppo_loss_step_f32.argtypes = [vp] * 11 + [i32, i32, f32, i32, f32, f32, vp, vp, vp, vp, vp, vp]
         L.pmlp_heads_blocks.argtypes = [i32]
@@ -200,12 +205,13 @@ def frag_pack(w, rows32):
     return p.view(rows32 // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).reshape(-1)
 
 
-def mlp_forward(nets, M, rollout=None):
+def mlp_forward(nets, M, rollout=None, loss=None):
     """One launch of the whole forward of up to two 4-layer MLPs (pmlp_mlp_forward).  nets:
     dicts x (fp32 [*, ldx]), kx, rows (int64 [M] | None), xa (bf16 [M, K0] | None), K0,
     W (4 bf16 [N, K] tensors), Wf (None or 4 frag_pack copies of W), b (4 fp32 tensors),
     N (4 ints), y (3 bf16 [M, N] tensors or None), out (fp32 [M, N3]).  rollout: a
-    RolloutStep (actor and critic over the M envs: pmlp_rollout_forward)."""
+    RolloutStep (actor and critic over the M envs: pmlp_rollout_forward).  loss: the
+    arguments of pmlp_mlp_forward_ppo_loss after M (the update's loss in the same launch)."""
     def mk(n):
         y = n.get("y") or (None, None, None)
         return MlpFwdJob(_p(n["x"]), _p(n.get("rows")), n["x"].stride(0), n["kx"], _p(n.get("xa")),
@@ -217,6 +223,8 @@ def mlp_forward(nets, M, rollout=None):
     arr = (MlpFwdJob * len(nets))(*[mk(n) for n in nets])
     if rollout is not None:  # the rollout step's sampling, storage rows and deferred store ride along
         _ok(load().pmlp_rollout_forward(arr, int(M), C.byref(rollout), _stream()), "pmlp_rollout_forward")
+    elif loss is not None:  # the update's PPO loss on the workgroups' rows
+        _ok(load().pmlp_mlp_forward_ppo_loss(arr, int(M), *loss), "pmlp_mlp_forward_ppo_loss")
     else:
         _ok(load().pmlp_mlp_forward(len(nets), arr, int(M), _stream()), "pmlp_mlp_forward")
 
