@@ -72,6 +72,41 @@ def test_fused_step_matches_fp32_autograd_update(schedule):
         assert (da - db).abs().max() <= 4 * 3 * lr
 
 
+def test_loss_in_forward_launch_matches_the_separate_loss_kernel(monkeypatch):
+    """pmlp_mlp_forward_ppo_loss (the loss in the update forward's launch, mini-batches of at
+    least 18,432 rows) against the separate pmlp_ppo_loss_step launch (PMLP_FUSED_LOSS=0), one
+    optimizer step from identical weights and rollout: both nets' output gradients bitwise (the
+    same per-row arithmetic), the logged losses and every parameter to rounding (the partial
+    sums run over 96-row instead of 64-row groups)."""
+    torch.manual_seed(0)
+    N, T, O, A = 1024, 24, 48, 12  # one mini-batch of 24,576 rows
+    kw = dict(num_learning_epochs=1, num_mini_batches=1, learning_rate=1e-3, schedule="adaptive", device="cuda")
+    ac0 = ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda()
+    algs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("PMLP_FUSED_LOSS", fused)
+        alg = PPO(copy.deepcopy(ac0), **kw)
+        alg.init_storage(N, T, [O], [None], [A])
+        assert alg._fused is not None and alg._fused.fused_loss == (fused == "1")
+        algs.append(alg)
+    data = _fill_storage(algs[0], T, N, O, A, seed=3)
+    for alg in algs:
+        for k, v in data.items():
+            getattr(alg.storage, k).copy_(v)
+        alg.storage.step = T
+    losses = []
+    for alg in algs:
+        torch.manual_seed(7)
+        losses.append(alg.update())
+    sep, fus = algs
+    for n in range(2):
+        assert torch.equal(fus._fused.dz_out[n], sep._fused.dz_out[n])
+    np.testing.assert_allclose(losses[1], losses[0], rtol=1e-5, atol=1e-7)
+    assert fus.learning_rate == pytest.approx(sep.learning_rate, rel=1e-6)
+    for a, b in zip(sep.actor_critic.parameters(), fus.actor_critic.parameters()):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+
+
 def test_adam_kernel_matches_torch_adam_with_clipping():
     """pmlp_opt_prepare + pmlp_adam == nn.utils.clip_grad_norm_ + torch.optim.Adam (fp32)
     over several steps with changing gradients, on flat buffers."""
