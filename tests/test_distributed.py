@@ -124,3 +124,88 @@ def test_capture_fallback_is_decided_by_all_ranks():
     for p in procs:
         p.join(timeout=60)
     assert all(a is True and b is False for _, a, b in res), res
+
+
+# --- the drop-in launch: train.py under torch.distributed.run (legged_gym/utils/distributed.py)
+
+def _dist_mod():
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(here, "..", "unitree-rl-gym_amd")
+    if pkg not in sys.path:
+        sys.path.insert(0, pkg)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lg_distributed", os.path.join(pkg, "legged_gym", "utils",
+                                                                                 "distributed.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_rank_to_device_mapping_and_backend(monkeypatch):
+    m = _dist_mod()
+    # one rank per GPU on an 8-GPU node: rank r -> cuda:r, RCCL
+    assert [m.rank_device(r, 8) for r in range(8)] == list(range(8))
+    monkeypatch.delenv("LEGGED_GYM_DIST_BACKEND", raising=False)
+    assert m.choose_backend(8, 8) == "nccl"
+    # more local ranks than devices: ranks share devices round-robin, gloo (RCCL refuses
+    # two ranks on one device)
+    assert [m.rank_device(r, 1) for r in range(2)] == [0, 0]
+    assert [m.rank_device(r, 2) for r in range(4)] == [0, 1, 0, 1]
+    assert m.choose_backend(2, 1) == "gloo"
+    assert m.choose_backend(2, 0) == "gloo"
+    monkeypatch.setenv("LEGGED_GYM_DIST_BACKEND", "nccl")
+    assert m.choose_backend(2, 1) == "nccl"
+    import pytest
+    with pytest.raises(ValueError):
+        m.rank_device(0, 0)
+    # outside a launcher: nothing changes
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    assert m.world_from_env() == (1, 0, 0, 1)
+
+    class A:
+        sim_device = rl_device = "cuda:0"
+    a = A()
+    assert m.init_from_env(a) == 1 and a.sim_device == "cuda:0" and not dist.is_initialized()
+
+
+def _init_env_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    os.environ.pop("LEGGED_GYM_DIST_BACKEND", None)
+    m = _dist_mod()
+
+    class A:
+        sim_device = rl_device = "cuda:0"
+    a = A()
+    try:
+        w = m.init_from_env(a)
+        w2 = m.init_from_env(a)  # idempotent (make_env, then make_alg_runner)
+        t = torch.tensor([float(rank + 1)])
+        dist.all_reduce(t)
+        q.put((rank, w, w2, dist.get_backend(), float(t), m.is_main_process(), None))
+    except Exception:
+        import traceback
+        q.put((rank, None, None, None, None, None, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_init_from_env_joins_the_process_group_two_ranks():
+    """WORLD_SIZE/RANK/LOCAL_RANK as torch.distributed.run sets them: both ranks join one
+    gloo group (no GPU in this container) and only rank 0 is the main process."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_init_env_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[6] is None, r[6]
+    assert [r[1] for r in res] == [2, 2] and [r[2] for r in res] == [2, 2]
+    assert all(r[3] == "gloo" and r[4] == 3.0 for r in res)
+    assert [r[5] for r in res] == [True, False]

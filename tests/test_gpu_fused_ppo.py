@@ -577,3 +577,30 @@ def test_minibatch_permutation_kernel_is_a_permutation(n):
         assert not torch.equal(a, b)
         disp = (a - torch.arange(n, device="cuda")).abs().double().mean().item()
         assert abs(disp - n / 3) < 0.02 * n
+
+
+@pytest.mark.parametrize("T", [3, 4])
+def test_fused_rollout_noise_is_fresh_across_iterations(T):
+    """the draw-counter parity follows the acts, not the storage index, so
+    with an odd num_steps_per_env the next iteration's first step does not reuse the last
+    step's noise; every step of two iterations samples different noise."""
+    torch.manual_seed(0)
+    N, O, A = 1024, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    assert alg._rollout is not None
+    st = alg.storage
+    obs = torch.randn(N, O, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    zs = []
+    for it in range(2):
+        for t in range(T):
+            with torch.inference_mode():
+                a = alg.act(obs, obs).clone()
+                zs.append(((a - alg._rollout.out[0]) / st.sigma[t]).clone())
+                alg.process_env_step(torch.zeros(N, device="cuda"), torch.zeros(N, dtype=torch.bool, device="cuda"),
+                                     {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+        alg.flush_rollout()
+        st.clear()
+    for i in range(len(zs)):
+        for j in range(i):
+            assert (zs[i] == zs[j]).float().mean().item() < 0.01, (T, i, j)

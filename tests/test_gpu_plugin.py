@@ -128,3 +128,46 @@ def test_many_python_reward_terms_on_two_envs_per_wave():
         assert (env.episode_sums[k] == 0).all(), k
         if k.startswith("extra_"):  # positive terms: a row left out of the extras would read 0
             assert float(extras["episode"]["rew_" + k]) > float(before[k].mean()) / env.max_episode_length_s * 0.99, k
+
+
+from legged_gym.envs.h1.h1_env import H1Robot  # noqa: E402
+
+
+class H1WithKneeTerm(H1Robot):
+    """An H1 task with a Python reward that reads non-foot rigid-body rows (the knees and the
+    pelvis), as a reference-style task written against refreshed body states would."""
+
+    def _reward_knee_height(self):
+        self.seen_body_states = self.rigid_body_states_view.clone()
+        knees = [i for i, n in enumerate(self.body_names) if "knee" in n]
+        return self.rigid_body_states_view[:, knees, 2].mean(dim=1) - self.rigid_body_states_view[:, 0, 2]
+
+
+def test_python_reward_reads_every_body_row_equal_to_the_oracle():
+    """With a Python reward term the step refreshes EVERY rigid_body_states row (not only the
+    feet), on the pre-reset state the reference's compute_reward sees; the rows the term read
+    equal the CPU oracle's forward kinematics of that step, bit for bit."""
+    import bridge
+    env_cfg, train_cfg = task_registry.get_cfgs("h1")
+    cfg = copy.deepcopy(env_cfg)
+    cfg.rewards.scales.knee_height = 0.5
+    task_registry.register("h1_knee_term", H1WithKneeTerm, cfg, copy.deepcopy(train_cfg))
+    env, _ = task_registry.make_env(name="h1_knee_term", args=get_args(["--task", "h1_knee_term", "--num_envs", "64",
+                                                                        "--headless"]))
+    assert env.task_params.body_state_mask == 0 and env.task_params.write_body_states == 1
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(8):
+        env.step(0.4 * torch.randn(64, env.num_actions, device="cuda", generator=g))
+    snap = bridge.snapshot(env)
+    a = 0.4 * torch.randn(64, env.num_actions, device="cuda", generator=g)
+    ref = bridge.step(env, snap, a.cpu().numpy(), env.common_step_counter)
+    env.step(a)
+    torch.cuda.synchronize()
+    B = env.num_bodies
+    want = ref["rbs"].reshape(64, B, 13)
+    seen = env.seen_body_states.cpu().numpy()
+    np.testing.assert_array_equal(seen, want)
+    np.testing.assert_array_equal(env.rigid_body_states.view(64, B, 13).cpu().numpy(), want)
+    knees = [i for i, n in enumerate(env.body_names) if "knee" in n]
+    assert len(knees) == 2 and not (seen[:, knees, 2] == 0).all()

@@ -468,3 +468,35 @@ def test_lstm_rollout_step_mfma_in_place_matches_nn_lstm():
         assert torch.equal(hs, h_ref) and torch.equal(cs, c_ref)
         torch.testing.assert_close(h, h_new, rtol=2e-5, atol=2e-5)
         torch.testing.assert_close(c, c_new, rtol=2e-5, atol=2e-5)
+
+
+def test_recurrent_rollout_draws_fresh_noise_every_step_and_iteration():
+    """the recurrent rollout's Philox draw counter advances after every
+    pmlp_act (in pmlp_store_step), so the standardised noise (a - mu) / sigma differs between
+    consecutive steps and between iterations (storage cleared, same obs)."""
+    torch.manual_seed(4)
+    N, T, O, P, A, H = 256, 3, 47, 50, 12, 64
+    ac = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                              rnn_hidden_size=H, rnn_num_layers=1).cuda()
+    alg = PPO(ac, device="cuda")
+    alg.init_storage(N, T, [O], [P], [A])
+    assert alg._rollout is not None
+    st = alg.storage
+    g = torch.Generator(device="cuda").manual_seed(1)
+    obs, cobs = torch.randn(N, O, device="cuda", generator=g), torch.randn(N, P, device="cuda", generator=g)
+    zs = []
+    for it in range(2):
+        for t in range(T):
+            with torch.inference_mode():
+                alg.act(obs, cobs)
+                alg.process_env_step(torch.zeros(N, device="cuda"), torch.zeros(N, dtype=torch.bool, device="cuda"),
+                                     {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+            zs.append(((st.actions[t] - st.mu[t]) / st.sigma[t]).clone())
+        alg.flush_rollout()
+        st.clear()
+    for i in range(len(zs)):
+        for j in range(i):
+            same = (zs[i] == zs[j]).float().mean().item()
+            assert same < 0.01, (i, j, same)
+    z = torch.stack(zs)
+    assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1.0) < 0.02

@@ -18,6 +18,7 @@ time-outs) are double-buffered, because the reference returns fresh tensors
 each step and rsl_rl holds references to them across the next ``step()``.
 """
 import os
+import time
 
 import numpy as np
 import torch
@@ -62,15 +63,26 @@ class _GymTensorAPI:
 
 class LeggedRobot(BaseTask):
     obs_layout = cabi.OBS_QUADRUPED
-    # rigid_body_states rows each step refreshes when the task reads them: "feet" (all the
-    # reference's envs read) or "all"; self.gym.refresh_rigid_body_state_tensor refreshes all
-    rigid_body_state_bodies = "feet"
+    # rigid_body_states rows each step refreshes: "feet" (all the reference's humanoid envs
+    # read, h1_env.py:34-52) or "all"; None = "all" when the task has Python `_reward_*` terms
+    # (they may read any body row, as after the reference's per-step refresh, h1_env.py:48-56),
+    # else "feet".  self.gym.refresh_rigid_body_state_tensor always refreshes every body.
+    rigid_body_state_bodies = None
     hip_dof_indices = ()
     max_contacts = 8
     max_rows = 32
     max_self_contacts = 4  # contact slots self contacts may take per substep (cfg.asset.self_collisions == 0)
+    # The reference's per-step methods that the native step replaces (legged_robot.py:649-671,
+    # 488-555, 557-594, 711-721, 770-811, 188-219).  The kernel never calls a Python method, so a
+    # task subclass overriding one of them (the reference's G1Robot does, g1_env.py:56-141)
+    # would train as if it had not: construction refuses it instead.  Python `_reward_<name>`
+    # terms ARE supported (_prepare_reward_function).
+    NATIVE_STEP_METHODS = ("_compute_torques", "_post_physics_step_callback", "_resample_commands", "_push_robots",
+                           "check_termination", "compute_reward", "compute_observations", "_get_noise_scale_vec",
+                           "post_physics_step", "_reset_dofs", "_reset_root_states")
 
     def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
+        self._refuse_native_step_overrides()
         self.cfg = cfg
         self.sim_params = sim_params
         self.gym = _GymTensorAPI(self)
@@ -83,6 +95,23 @@ class LeggedRobot(BaseTask):
         self._prepare_reward_function()
         self._build_task()
         self.init_done = True
+
+    @classmethod
+    def _refuse_native_step_overrides(cls):
+        from .humanoid import HumanoidRobot
+        native = (BaseTask, LeggedRobot, HumanoidRobot)
+        bad = []
+        for name in cls.NATIVE_STEP_METHODS:
+            owner = next((k for k in cls.__mro__ if name in vars(k)), None)
+            if owner is not None and owner not in native:
+                bad.append(f"{owner.__module__}.{owner.__qualname__}.{name}")
+        if bad:
+            raise NotImplementedError(
+                f"{cls.__name__} overrides {', '.join(bad)}: the native step (one lgs_step launch) computes "
+                "torques, commands, pushes, termination, rewards, resets and observations in a HIP kernel and "
+                "never calls these methods, so the override would be silently ignored.  Supported plugin "
+                "points: cfg values, Python `_reward_<name>` terms (scaled like the reference's), and "
+                "reset_idx(env_ids); see INTEGRATION.md.")
 
     # ------------------------------------------------------------ config ----
     def _parse_cfg(self, cfg):
@@ -408,6 +437,8 @@ class LeggedRobot(BaseTask):
         else:
             self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
         self._step_mirror += 1
+        if self.cfg.env.test:
+            self._pace_to_real_time()
         self.obs_buf = self._obs_bufs[i]
         self.privileged_obs_buf = self._priv_bufs[i]
         self.reset_buf = self._reset_bufs[i]
@@ -416,6 +447,19 @@ class LeggedRobot(BaseTask):
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self._time_outs
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    def _pace_to_real_time(self):
+        """cfg.env.test (play.py): simulated time does not run ahead of the wall clock
+        (legged_robot.py:631-635: gym.get_sim_time vs gym.get_elapsed_time, both counted
+        from the sim's creation).  Never inside a captured graph (nothing would wait)."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        if getattr(self, "_wall_t0", None) is None:
+            self._wall_t0, self._sim_time = time.perf_counter(), 0.0
+        self._sim_time += self.dt
+        ahead = self._sim_time - (time.perf_counter() - self._wall_t0)
+        if ahead > 0:
+            time.sleep(ahead)
 
     def _python_rewards(self):
         """compute_reward (legged_robot.py:770-787) for the Python terms: the kernel left the

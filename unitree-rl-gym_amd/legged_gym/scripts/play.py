@@ -1,16 +1,16 @@
-"""Roll out / export a trained policy (reference scripts/play.py:15-51; same CLI)."""
+"""Roll out / export a trained policy (reference scripts/play.py:15-51; same CLI, same
+imports, same 10-episode roll-out)."""
 import os
 
 import isaacgym  # noqa: F401
 from legged_gym import LEGGED_GYM_ROOT_DIR
 from legged_gym.envs import *  # noqa: F401,F403
-from legged_gym.utils import export_policy_as_jit, get_args, task_registry
-
-EXPORT_POLICY = True
+from legged_gym.utils import get_args, export_policy_as_jit, task_registry, Logger  # noqa: F401
 
 
-def play(args, num_steps=None):
+def play(args):
     env_cfg, train_cfg = task_registry.get_cfgs(name=args.task)
+    # override some parameters for testing
     env_cfg.env.num_envs = min(env_cfg.env.num_envs, 100)
     env_cfg.terrain.num_rows = 5
     env_cfg.terrain.num_cols = 5
@@ -25,18 +25,20 @@ def play(args, num_steps=None):
     train_cfg.runner.resume = True
     ppo_runner, train_cfg = task_registry.make_alg_runner(env=env, name=args.task, args=args, train_cfg=train_cfg)
     policy = ppo_runner.get_inference_policy(device=env.device)
+
+    # export the policy as a TorchScript module (run from C++ / MuJoCo deploy)
     if EXPORT_POLICY:
         path = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name, "exported", "policies")
         export_policy_as_jit(ppo_runner.alg.actor_critic, path)
         print("Exported policy as jit script to: ", path)
-    steps = num_steps if num_steps is not None else 10 * int(env.max_episode_length)
-    for _ in range(steps):
+
+    for _ in range(10 * int(env.max_episode_length)):
         actions = policy(obs.detach())
         obs, _, rews, dones, infos = env.step(actions.detach())
-    return env
 
 
 if __name__ == "__main__":
-    # LEGGED_GYM_PLAY_STEPS bounds the roll-out (the reference plays 10 episodes' worth)
-    n = os.environ.get("LEGGED_GYM_PLAY_STEPS")
-    play(get_args(), num_steps=int(n) if n else None)
+    EXPORT_POLICY = True
+    RECORD_FRAMES = False
+    MOVE_CAMERA = False
+    play(get_args())

@@ -2,7 +2,9 @@
 
 ``register(name, task_class, env_cfg, train_cfg)`` is the plugin API new tasks
 hook into; ``make_env`` / ``make_alg_runner`` keep their signatures, return
-values and ValueError behaviour.
+values and ValueError behaviour.  Under ``torch.distributed.run`` both first bind
+the rank to its device and join the process group (``distributed.init_from_env``),
+so the unmodified ``train.py`` trains data-parallel.
 """
 import os
 from datetime import datetime
@@ -14,6 +16,7 @@ from rsl_rl.runners import OnPolicyRunner
 from legged_gym import LEGGED_GYM_ROOT_DIR
 from legged_gym.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO
 
+from .distributed import init_from_env
 from .helpers import class_to_dict, get_args, get_load_path, parse_sim_params, set_seed, update_cfg_from_args
 
 
@@ -41,6 +44,7 @@ class TaskRegistry:
             args = get_args()
         if name not in self.task_classes:
             raise ValueError(f"Task with name: {name} was not registered")
+        init_from_env(args)  # WORLD_SIZE > 1: this rank's device into args, process group
         task_class = self.get_task_class(name)
         if env_cfg is None:
             env_cfg, _ = self.get_cfgs(name)
@@ -62,6 +66,7 @@ class TaskRegistry:
         elif name is not None:
             print(f"'train_cfg' provided -> Ignoring 'name={name}'")
         _, train_cfg = update_cfg_from_args(None, train_cfg, args)
+        init_from_env(args)
         stamp = datetime.now().strftime("%b%d_%H-%M-%S") + "_" + train_cfg.runner.run_name
         if log_root == "default":
             log_root = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name)

@@ -105,10 +105,17 @@ def build_task_params(env) -> cabi.TaskParams:
     seed = int(getattr(cfg, "seed", 1))
     rank = int(os.environ.get("RANK", "0"))
     T.seed = (seed & 0xFFFFFFFF) | (rank << 32)
-    T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)))
     # the rows the step refreshes: the feet (all the reference's humanoid envs read, h1_env.py:34-52)
-    # unless the task asks for every body (rigid_body_state_bodies = "all")
-    if getattr(env, "rigid_body_state_bodies", "feet") == "all":
+    # unless the task asks for every body (rigid_body_state_bodies = "all"); by default every
+    # body when the task has Python reward terms, which may read any row
+    bodies = getattr(env, "rigid_body_state_bodies", None)
+    if bodies is None:
+        bodies = "all" if py else "feet"
+    if bodies not in ("all", "feet"):
+        raise ValueError(f"rigid_body_state_bodies must be 'all', 'feet' or None, not {bodies!r}")
+    T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)) or
+                              bool(py))
+    if bodies == "all":
         T.body_state_mask = 0
     else:
         T.body_state_mask = sum(1 << b for b in fi) if fi else 0

@@ -35,6 +35,16 @@ from rsl_rl.modules import lstm_seq
 from rsl_rl.modules import mfma_mlp as mm
 
 
+def noise_seed():
+    """The rollout's policy-noise Philox key: from torch's seeded generator, mixed with
+    the data-parallel rank so the ranks (which start from the same torch seed) explore
+    with independent noise, as their envs do (seed + rank)."""
+    s = int(torch.randint(0, 2 ** 62, (1,)).item())
+    if dist.is_available() and dist.is_initialized():
+        s ^= (dist.get_rank() * 0x9E3779B97F4A7C15) & (2 ** 62 - 1)
+    return s
+
+
 def _ceil8(n):
     return (n + 7) // 8 * 8
 
@@ -341,11 +351,15 @@ class FusedRollout:
         self.y = [[torch.empty(N, lin.out_features, dtype=bf, device=dev) for lin in ls[:-1]] for ls in lins]
         self.out = [torch.empty(N, ls[-1].out_features, device=dev) for ls in lins]
         self.actions = torch.empty(N, lins[0][-1].out_features, device=dev)
-        # policy-noise draw counters: the act at storage step t samples with draw[t % 2] and
-        # sets draw[(t + 1) % 2] (pmlp_rollout_forward), so the forward launch both draws and
-        # advances without racing itself
+        # policy-noise draw counters: the k-th act samples with draw[k % 2] and sets
+        # draw[(k + 1) % 2] (pmlp_rollout_forward), so the forward launch both draws and
+        # advances without racing itself.  k counts acts across iterations (not the storage
+        # index t): with an odd num_steps_per_env, keying on t would make the next
+        # iteration's first step reread the counter the last step read.  A captured rollout
+        # has an even T (_RolloutGraph), so its replays keep k's parity.
         self.draw = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.k = 0
+        self.seed = noise_seed()
         # the last process_env_step's store, deferred into the next act's launch (or flush())
         self.pending = None
 
@@ -395,17 +409,19 @@ class FusedRollout:
         A = self.actions.shape[1]
         priv = storage.privileged_observations
         P = mm._p
+        par = self.k % 2
+        self.k += 1
         if not f.fused_fwd:  # per-layer GEMMs, then the separate sampling launch
             self.flush(storage)
             self.forward(obs, cobs, t)
             mm._ok(mm.load().pmlp_act(P(self.out[0]), P(f.ac.std.detach()), P(self.out[1]), P(obs),
                                       P(cobs) if priv is not None else None, N, A, obs.shape[1],
-                                      cobs.shape[1] if priv is not None else 0, P(self.draw[t % 2:]), self.seed,
+                                      cobs.shape[1] if priv is not None else 0, P(self.draw[par:]), self.seed,
                                       P(self.actions), P(storage.actions[t]), P(storage.actions_log_prob[t]),
                                       P(storage.mu[t]), P(storage.sigma[t]), P(storage.values[t]),
                                       P(storage.observations[t]), P(priv[t]) if priv is not None else None,
                                       mm._stream()), "pmlp_act")
-            self.draw[(t + 1) % 2].copy_(self.draw[t % 2] + 1)
+            self.draw[par ^ 1].copy_(self.draw[par] + 1)
             return self.actions
         f.ensure_weights()
         pend = self.pending
@@ -414,7 +430,7 @@ class FusedRollout:
                             cobs.shape[1] if priv is not None else 0, A, P(self.actions), P(storage.actions[t]),
                             P(storage.actions_log_prob[t]), P(storage.mu[t]), P(storage.sigma[t]),
                             P(storage.values[t]), P(storage.observations[t]), P(priv[t]) if priv is not None else None,
-                            P(self.draw), t % 2, self.seed)
+                            P(self.draw), par, self.seed)
         if pend is not None:
             rew, dones, tout, tp, gamma = pend
             rs.rewards, rs.dones, rs.time_outs = P(rew), P(dones), P(tout)
@@ -466,7 +482,7 @@ class RecurrentRollout:
         ac = alg.actor_critic
         self.actions = torch.empty(self.N, ac.std.shape[0], device=ac.std.device)
         self.draw = torch.zeros((), dtype=torch.int64, device=ac.std.device)
-        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.seed = noise_seed()
         # both Linear/ELU/Linear heads in one launch (pmlp_heads_forward, fp32) where the
         # fused recurrent step covers the policy; else the torch modules
         from rsl_rl.algorithms import fused_recurrent
@@ -545,12 +561,18 @@ class RecurrentRollout:
         return self.actions
 
     pending = None
-    flush = FusedRollout.flush
+
+    def flush(self, storage):
+        pass  # nothing is deferred: store() issues its launch at once
 
     def store(self, rewards, dones, time_outs, storage, t, gamma):
-        """PPO.process_env_step: pmlp_store_step at once (no forward launch to ride in)."""
-        self.pending = (rewards, dones, time_outs, t, gamma)
-        self.flush(storage)
+        """PPO.process_env_step: pmlp_store_step at once (no forward launch to ride in).
+        The launch also advances the policy-noise draw counter pmlp_act read (one thread,
+        after the store), so every step and every iteration samples fresh noise."""
+        P = mm._p
+        mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+                                         P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
+                                         P(self.draw), mm._stream()), "pmlp_store_step")
 
 
 def gae(storage, last_values, gamma, lam, world_size=1):

@@ -158,6 +158,9 @@ class PPO:
             tr.hidden_states = None
             self._stored_t = t
             return actions
+        # a store deferred by an earlier fused act goes out now: it holds the env's reward /
+        # done buffers, which the next env.step overwrites
+        self.flush_rollout()
         if self.actor_critic.is_recurrent:
             # the state BEFORE this step, copied into the storage slot now: on the GPU the
             # memory updates its state buffers in place during act()
