@@ -29,6 +29,7 @@ def run(script, *argv, timeout=300):
     return r.stdout
 
 
+@pytest.mark.parametrize("task,n_obs,recurrent", [("go2", 48, False), ("h1", 41, True)])
 def test_train_then_play_export(task, n_obs, recurrent):
     exp = f"pytest_{task}"
     out = run("train.py", "--task", task, "--num_envs", "512", "--max_iterations", "2", "--headless",
