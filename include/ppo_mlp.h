@@ -98,6 +98,13 @@ typedef struct {
     int32_t ldaf, kaf, ldxa, b_kn, sum_col;
 } pmlp_gemm_job;
 PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream);
+/* A layer's backward in one launch: the PARTIAL_TN weight-gradient batch jobs_w (ksplit as
+ * pmlp_gemm) and the BWD_DX input-gradient batch jobs_x (B given [K,N]) read the same output
+ * gradient and nothing the other writes, so both run in one grid where their tile
+ * configurations share a block size (else as two pmlp_gemm launches).  Results are bitwise
+ * those of the two launches. */
+PMLP_API int pmlp_gemm_pair(int32_t njobs_w, const pmlp_gemm_job* jobs_w, int32_t ksplit, int32_t njobs_x,
+                            const pmlp_gemm_job* jobs_x, void* stream);
 /* operand staging of pmlp_gemm's k-loop: 1 (default; env PMLP_GLDS) = LDS-DMA into two LDS buffers,
  * one barrier per k-tile, wherever the shapes allow (whole 64-deep k-tiles); 0 = register staging.
  * Both compute the same MFMA chain (bitwise equal).  Returns the previous setting. */

@@ -604,3 +604,36 @@ def test_fused_rollout_noise_is_fresh_across_iterations(T):
     for i in range(len(zs)):
         for j in range(i):
             assert (zs[i] == zs[j]).float().mean().item() < 0.01, (T, i, j)
+
+
+@pytest.mark.parametrize("mlp", [[512, 256, 128], [256, 128, 64]])
+def test_paired_backward_launch_is_bitwise_the_two_launches(monkeypatch, mlp):
+    """pmlp_gemm_pair (a layer's weight gradient beside its input gradient in one grid)
+    against the two pmlp_gemm launches (PMLP_GEMM_PAIR=0): two captured updates of the Go2
+    shapes (24,576-row mini-batches, 4 optimizer steps each) from identical weights and rollout
+    end with bitwise-identical parameters, gradients and Adam moments; and an MLP whose tiles
+    do not pair falls back to the two launches."""
+    torch.manual_seed(0)
+    N, T, O, A = 4096, 24, 48, 12
+    kw = dict(num_learning_epochs=2, num_mini_batches=2, learning_rate=1e-3, schedule="adaptive", device="cuda")
+    ac0 = ActorCritic(O, O, A, mlp, mlp).cuda()
+    algs = []
+    for pair in ("0", "1"):
+        monkeypatch.setenv("PMLP_GEMM_PAIR", pair)
+        alg = PPO(copy.deepcopy(ac0), **kw)
+        alg.init_storage(N, T, [O], [None], [A])
+        assert alg._fused is not None and alg._fused.pair_backward == (pair == "1")
+        algs.append(alg)
+    data = _fill_storage(algs[0], T, N, O, A, seed=5)
+    for it in range(2):
+        for alg in algs:
+            for k, v in data.items():
+                getattr(alg.storage, k).copy_(v)
+            alg.storage.step = T
+            torch.manual_seed(11 + it)
+            alg.update()
+    two, one = algs
+    for a, b in zip(two.actor_critic.parameters(), one.actor_critic.parameters()):
+        assert torch.equal(a, b)
+    assert torch.equal(two._fused.grad, one._fused.grad)
+    assert torch.equal(two._fused.exp_avg, one._fused.exp_avg) and torch.equal(two._fused.exp_avg_sq, one._fused.exp_avg_sq)

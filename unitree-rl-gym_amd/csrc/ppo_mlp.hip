@@ -135,17 +135,34 @@ __device__ __forceinline__ int gl_swz(int r) { return R == 128 ? (r & 3) : ((r >
 // Needs whole 64-deep k-tiles (K, and the split-K slab, multiples of 64) and, for a k-major
 // operand, R a multiple of the tile (rows-form tiles past M / N read a clamped row instead;
 // those outputs are never stored).  Same MFMA order as GL = 0: bitwise the same results.
+// LDS elements (bf16) of one k_gemm_nt tile: the staging buffers, or the epilogue tiles
+template <int BM, int BN, int WM, int WN, int EPI, int NKS, int MODE, int GL>
+__host__ __device__ constexpr int gemm_smem() {
+    constexpr bool TNL = EPI == PMLP_EPI_PARTIAL_TN, PART = EPI == PMLP_EPI_PARTIAL || TNL;
+    constexpr bool BKN = TNL || (MODE & 2) != 0;
+    constexpr int BK = 64, LS = BK + 8;
+    constexpr int SA = TNL ? BM + 32 : LS, SB = BKN ? BN + 32 : LS;
+    constexpr int ATILE = TNL ? BK * SA : BM * LS, BTILE = BKN ? BK * SB : BN * LS;
+    constexpr int GSTAGE = (BM + BN) * BK, GNS = GL == 2 ? 4 : 2;
+    constexpr int STAGE = GL ? GNS * GSTAGE : (ATILE + BTILE) * PMLP_NBUF, CTILE = BM * (BN + 8), TTILE = BN * (BM + 8);
+    return PART ? STAGE : (STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE));
+}
+
+// One output tile of the batched GEMM: block b of a gx x gy x gz grid (b linear), smem the
+// gemm_smem<...>() bf16 elements of LDS.  k_gemm_nt runs it as a kernel of its own;
+// k_gemm_pair runs two of them (a weight gradient beside an input gradient) in one grid.
 template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0, int GL = 0>
-__global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
+__device__ __forceinline__ void gemm_tile(const GemmBatch& gb, bf16* smem, int b, int gx, int gy, int gz) {
     // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (b % 8), each
     // with its own L2; give every XCD a contiguous range of logical tiles, ordered so that
     // the tiles sharing an operand panel are neighbours -- the n-tiles of one row block
     // (forward / input gradient: they share the A rows), the tiles of one split-K slab
     // (weight gradient: they share its rows of both operands) -- and read it from one L2.
+    // (In a paired grid b is the block's index within its half: the halves' XCDs are
+    // rotated by the offset, each XCD still owns one contiguous range.)
     int bx, by, bz;
     {
-        const int gx = gridDim.x, gy = gridDim.y;
-        const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), nwg = gx * gy * gridDim.z;
+        const int nwg = gx * gy * gz;
         const int xcd = b % 8, q = nwg / 8, r = nwg % 8;
         const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
         if (EPI == PMLP_EPI_PARTIAL || EPI == PMLP_EPI_PARTIAL_TN) {
@@ -192,7 +209,7 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
     static_assert(!GL || ((TNL ? BM : 64) % 64 == 0 && (BKN ? BN : 64) % 64 == 0), "GL k-major tiles: 64 or 128");
     constexpr int SMEM = PART ? STAGE
                               : (STAGE > CTILE ? (STAGE > TTILE ? STAGE : TTILE) : (CTILE > TTILE ? CTILE : TTILE));
-    __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
+    static_assert(SMEM == gemm_smem<BM, BN, WM, WN, EPI, NKS, MODE, GL>(), "gemm_smem out of step");
     bf16* As = smem;
     bf16* Bs = smem + ATILE;
 
@@ -717,6 +734,38 @@ __global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
             ct_out();
         }
     }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int NKS = 4, int MODE = 0, int GL = 0>
+__global__ __launch_bounds__(64 * WM* WN) void k_gemm_nt(GemmBatch gb) {
+    __shared__ __attribute__((aligned(16))) bf16 smem[gemm_smem<BM, BN, WM, WN, EPI, NKS, MODE, GL>()];
+    gemm_tile<BM, BN, WM, WN, EPI, NKS, MODE, GL>(gb, smem, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                                                  gridDim.x, gridDim.y, gridDim.z);
+}
+
+// A k_gemm_nt instantiation as a type (k_gemm_pair's halves)
+template <int BM_, int BN_, int WM_, int WN_, int EPI_, int NKS_ = 4, int MODE_ = 0, int GL_ = 0>
+struct GemmCfg {
+    static constexpr int BM = BM_, BN = BN_, NT = 64 * WM_ * WN_;
+    static constexpr int SMEM = gemm_smem<BM_, BN_, WM_, WN_, EPI_, NKS_, MODE_, GL_>();
+    __device__ static void run(const GemmBatch& gb, bf16* smem, int b, int gx, int gy, int gz) {
+        gemm_tile<BM_, BN_, WM_, WN_, EPI_, NKS_, MODE_, GL_>(gb, smem, b, gx, gy, gz);
+    }
+};
+
+// Two independent GEMM batches in ONE grid (1-D, block-uniform split): blocks [0, nA) run
+// batch A's tiles on a dA grid, the rest batch B's on a dB grid.  The backward's weight
+// gradient and input gradient of a layer both read only that layer's output gradient, so they
+// share a launch: one kernel boundary fewer per layer, and the small weight-gradient grid runs
+// beside the input gradient's instead of alone.  Each tile computes exactly what it computes
+// in its own launch (bitwise the same results).
+template <class CA, class CB>
+__global__ __launch_bounds__(CA::NT) void k_gemm_pair(GemmBatch ga, GemmBatch gbb, int nA, int3 dA, int3 dB) {
+    static_assert(CA::NT == CB::NT, "paired halves need one block size");
+    __shared__ __attribute__((aligned(16))) bf16 smem[CA::SMEM > CB::SMEM ? CA::SMEM : CB::SMEM];
+    const int b = blockIdx.x;
+    if (b < nA) CA::run(ga, smem, b, dA.x, dA.y, dA.z);
+    else CB::run(gbb, smem, b - nA, dB.x, dB.y, dB.z);
 }
 
 // Batched fp32 -> bf16 conversion, 64x64 tiles through LDS (blockIdx.z = job):
@@ -2328,14 +2377,18 @@ PMLP_API int pmlp_convert(int32_t njobs, const pmlp_convert_job* jobs, void* str
     return 0;
 }
 
-PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream) {
+}  // extern "C"
+
+// pmlp_gemm's argument checks and packing: one batch of jobs -> GemmBatch (+ its extents)
+static int gemm_pack(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, GemmBatch& gb, int& maxm,
+                     int& maxn, int& maxk, int& mode) {
     if (epi < 0 || epi > 4) return fail(-1, "pmlp_gemm: unknown epilogue");
     const bool part = epi == PMLP_EPI_PARTIAL || epi == PMLP_EPI_PARTIAL_TN;
     if (njobs <= 0 || njobs > PMLP_MAX_GEMM_JOBS || !jobs) return fail(-1, "pmlp_gemm: 1..PMLP_MAX_GEMM_JOBS jobs");
-    GemmBatch gb{};
+    gb = GemmBatch{};
     gb.slabs = 1;
-    int maxm = 0, maxn = 0, maxk = 0;
-    const int mode = (jobs[0].af ? 1 : 0) | (jobs[0].b_kn ? 2 : 0);
+    maxm = maxn = maxk = 0;
+    mode = (jobs[0].af ? 1 : 0) | (jobs[0].b_kn ? 2 : 0);
     for (int i = 0; i < njobs; ++i) {
         const pmlp_gemm_job& J = jobs[i];
         const std::string w = "pmlp_gemm job " + std::to_string(i) + ": ";
@@ -2385,6 +2438,52 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
                 return fail(-1, "pmlp_gemm: PARTIAL jobs must have the same number of slabs");
         gb.slabs = (maxk + ksplit - 1) / ksplit;
     }
+    return 0;
+}
+
+// The k_gemm_nt instantiations of the backward that k_gemm_pair pairs: the plan code of the
+// kernel pmlp_gemm's selection below would launch for this batch, or 0 for any other.
+//   1: PARTIAL_TN on 32 x 128 tiles, register staging (a narrow layer's weight gradient)
+//   2: BWD_DX, B [K,N], one 16-deep k-tile, 64 x 64 tiles (the output layer's input gradient)
+//   3: PARTIAL_TN on 128 x 128 tiles, LDS-DMA staging
+//   4: BWD_DX, B [K,N], 128 x 128 tiles, LDS-DMA staging
+// Pairs (1, 2) and (3, 4) share a block size (256 / 512 threads).
+static int gemm_plan(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk) {
+    const bool part = epi == PMLP_EPI_PARTIAL || epi == PMLP_EPI_PARTIAL_TN;
+    if (epi == PMLP_EPI_PARTIAL_TN && mode == 0) {
+        if (maxm <= 32) return gl_fits<32, 128>(epi, mode, gb, njobs) ? 0 : 1;
+        if (maxn > 64) return gl_fits<128, 128>(epi, mode, gb, njobs) && glds_on() == 1 ? 3 : 0;
+        return 0;
+    }
+    if (epi == PMLP_EPI_BWD_DX && mode == 2 && maxm > 32 && maxn > 64) {
+        const bool small = (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512;
+        (void)part;
+        if (small) return !gl_fits<64, 64>(epi, mode, gb, njobs) && maxk <= 16 ? 2 : 0;
+        return gl_fits<128, 128>(epi, mode, gb, njobs) ? 4 : 0;
+    }
+    return 0;
+}
+
+static dim3 gemm_grid(int BM, int BN, const GemmBatch& gb, int njobs, int maxm, int maxn) {
+    return dim3((maxm + BM - 1) / BM, (maxn + BN - 1) / BN, njobs * gb.slabs);
+}
+
+template <class CA, class CB>
+static void launch_pair(const GemmBatch& ga, int nja, int mma, int mna, const GemmBatch& gb2, int njb, int mmb, int mnb,
+                        hipStream_t st) {
+    const dim3 da = gemm_grid(CA::BM, CA::BN, ga, nja, mma, mna), db = gemm_grid(CB::BM, CB::BN, gb2, njb, mmb, mnb);
+    const int na = (int)(da.x * da.y * da.z), nb = (int)(db.x * db.y * db.z);
+    hipLaunchKernelGGL((k_gemm_pair<CA, CB>), dim3(na + nb), dim3(CA::NT), 0, st, ga, gb2, na,
+                       make_int3((int)da.x, (int)da.y, (int)da.z), make_int3((int)db.x, (int)db.y, (int)db.z));
+}
+
+extern "C" {
+
+PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int32_t ksplit, void* stream) {
+    GemmBatch gb;
+    int maxm, maxn, maxk, mode;
+    if (const int rc = gemm_pack(epi, njobs, jobs, ksplit, gb, maxm, maxn, maxk, mode)) return rc;
+    const bool part = epi == PMLP_EPI_PARTIAL || epi == PMLP_EPI_PARTIAL_TN;
     hipStream_t st = (hipStream_t)stream;
     if (maxm <= 32) launch<32, 128, 1, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
     else if (maxn <= 32) launch<128, 32, 4, 1>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
@@ -2401,6 +2500,29 @@ PMLP_API int pmlp_gemm(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, in
         else launch<128, 128, 2, 4>(epi, mode, gb, njobs, maxm, maxn, maxk, st);
     }
     PMLP_CHECK_LAUNCH("pmlp_gemm");
+    return 0;
+}
+
+PMLP_API int pmlp_gemm_pair(int32_t njobs_w, const pmlp_gemm_job* jobs_w, int32_t ksplit, int32_t njobs_x,
+                            const pmlp_gemm_job* jobs_x, void* stream) {
+    GemmBatch gw, gx;
+    int mmw, mnw, mkw, modew, mmx, mnx, mkx, modex;
+    if (const int rc = gemm_pack(PMLP_EPI_PARTIAL_TN, njobs_w, jobs_w, ksplit, gw, mmw, mnw, mkw, modew)) return rc;
+    if (const int rc = gemm_pack(PMLP_EPI_BWD_DX, njobs_x, jobs_x, 0, gx, mmx, mnx, mkx, modex)) return rc;
+    const int pw = gemm_plan(PMLP_EPI_PARTIAL_TN, modew, gw, njobs_w, mmw, mnw, mkw);
+    const int px = gemm_plan(PMLP_EPI_BWD_DX, modex, gx, njobs_x, mmx, mnx, mkx);
+    hipStream_t st = (hipStream_t)stream;
+    if (pw == 1 && px == 2) {
+        launch_pair<GemmCfg<32, 128, 1, 4, PMLP_EPI_PARTIAL_TN>, GemmCfg<64, 64, 2, 2, PMLP_EPI_BWD_DX, 1, 2>>(
+            gw, njobs_w, mmw, mnw, gx, njobs_x, mmx, mnx, st);
+    } else if (pw == 3 && px == 4) {
+        launch_pair<GemmCfg<128, 128, 2, 4, PMLP_EPI_PARTIAL_TN, 4, 0, 1>, GemmCfg<128, 128, 2, 4, PMLP_EPI_BWD_DX, 4, 2, 1>>(
+            gw, njobs_w, mmw, mnw, gx, njobs_x, mmx, mnx, st);
+    } else {  // no paired instantiation for these shapes: the two launches
+        if (const int rc = pmlp_gemm(PMLP_EPI_PARTIAL_TN, njobs_w, jobs_w, ksplit, stream)) return rc;
+        return pmlp_gemm(PMLP_EPI_BWD_DX, njobs_x, jobs_x, 0, stream);
+    }
+    PMLP_CHECK_LAUNCH("pmlp_gemm_pair");
     return 0;
 }
 

@@ -174,6 +174,8 @@ class FusedPPOStep:
         self.fused_loss = bool(self.fused_fwd and self.fold_loss and 0 < fl_parts <= self.loss_partial.numel()
                                and Ap <= 16 and Ap % 4 == 0 and os.environ.get("PMLP_FUSED_LOSS", "1") != "0")
         self.loss_nb = (fl_parts if self.fused_loss else self.loss_partial.numel()) // (3 + A)
+        # a layer's weight and input gradients in one launch (PMLP_GEMM_PAIR=0: two launches)
+        self.pair_backward = os.environ.get("PMLP_GEMM_PAIR", "1") != "0"
 
     # -------------------------------------------------------- optimizer state --
     def sync_optimizer_state(self, opt):
@@ -271,8 +273,9 @@ class FusedPPOStep:
                                           P(self.dz_out[0]), None, self.dz_out[0].shape[1], P(self.dz_out[1]), None,
                                           self.dz_out[1].shape[1], st), "pmlp_ppo_loss_step")
         # 4. backward through both MLPs; the weight-gradient slabs carry the bias column.
-        #    (dW_l beside dX_l on a second stream measured slower: the two latency-bound
-        #    GEMMs contend)
+        #    A layer's weight gradient and input gradient read only its output gradient: one
+        #    launch for both (pmlp_gemm_pair) where their tiles pair.  (dW_l beside dX_l on a
+        #    second stream measured slower)
         dz = list(self.dz_out)
         red, copies = [], []
         for l in range(L - 1, -1, -1):
@@ -289,15 +292,20 @@ class FusedPPOStep:
                             kp + 8, kp))
                 if self.dw_stage[l][n] is not None:
                     copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
-            mm._gemm(mm.EPI_PARTIAL_TN, gj, ksplit=self.ks[l])
-            if l > 0:
-                gj = []
+            if l == 0:
+                mm._gemm(mm.EPI_PARTIAL_TN, gj, ksplit=self.ks[l])
+            else:
+                gx = []
                 for n in range(2):
                     lin = self.lins[n][l]
                     # the input layer's gradient is only consumed transposed (its weight gradient)
-                    gj.append(dict(A=dz[n], B=self.wb[n][l], b_kn=1, M=M, N=lin.in_features, K=dz[n].shape[1],
+                    gx.append(dict(A=dz[n], B=self.wb[n][l], b_kn=1, M=M, N=lin.in_features, K=dz[n].shape[1],
                                    yprev=self.y[n][l - 1], cb=self.dz[n][l]))
-                mm._gemm(mm.EPI_BWD_DX, gj)
+                if self.pair_backward:
+                    mm._gemm_pair(gj, self.ks[l], gx)
+                else:
+                    mm._gemm(mm.EPI_PARTIAL_TN, gj, ksplit=self.ks[l])
+                    mm._gemm(mm.EPI_BWD_DX, gx)
                 dz = [self.dz[n][l] for n in range(2)]
         adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
         dkl = float(alg.desired_kl if alg.desired_kl is not None else 0.0)

@@ -107,6 +107,7 @@ def load():
         L.pmlp_last_error.restype = C.c_char_p
         L.pmlp_convert.argtypes = [i32, C.POINTER(ConvertJob), vp]
         L.pmlp_gemm.argtypes = [i32, i32, C.POINTER(GemmJob), i32, vp]
+        L.pmlp_gemm_pair.argtypes = [i32, C.POINTER(GemmJob), i32, i32, C.POINTER(GemmJob), vp]
         L.pmlp_reduce_slabs.argtypes = [i32, C.POINTER(ReduceJob), vp]
         L.pmlp_reduce_slabs_step.argtypes = [i32, C.POINTER(ReduceJob), C.POINTER(ReduceStep), vp]
         L.pmlp_permutation.argtypes = [vp, C.c_int64, C.c_uint64, vp]
@@ -246,22 +247,33 @@ def _convert(jobs):
         _ok(load().pmlp_convert(len(chunk), arr, _stream()), "pmlp_convert")
 
 
+def _gemm_job(j):
+    g = lambda k: j.get(k)  # noqa: E731
+    ld = lambda t: 0 if t is None else t.stride(0)  # noqa: E731
+    af = g("af")
+    return GemmJob(_p(g("A")), _p(j["B"]), _p(g("bias")), _p(g("yprev")), _p(g("cf")), _p(g("cb")), _p(g("ct")),
+                   ld(g("A")), j["B"].stride(0), ld(g("yprev")),
+                   0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"],
+                   _p(af), _p(g("rows")), _p(g("xa")), ld(af), 0 if af is None else af.shape[1], ld(g("xa")),
+                   int(bool(g("b_kn"))), int(g("sum_col") or 0))
+
+
+def _gemm_pair(jobs_w, ksplit, jobs_x):
+    """A layer's weight gradient (PARTIAL_TN jobs_w) and input gradient (BWD_DX jobs_x, B
+    given [K,N]) in one launch where their tile configurations pair (pmlp_gemm_pair; else the
+    two launches): bitwise the results of two _gemm calls."""
+    aw = (GemmJob * len(jobs_w))(*[_gemm_job(j) for j in jobs_w])
+    ax = (GemmJob * len(jobs_x))(*[_gemm_job(j) for j in jobs_x])
+    _ok(load().pmlp_gemm_pair(len(jobs_w), aw, ksplit, len(jobs_x), ax, _stream()), "pmlp_gemm_pair")
+
+
 def _gemm(epi, jobs, ksplit=0):
     """jobs: dicts with A, B, M, N, K and optional bias, yprev, cf, cb, ct (tensors); the
     first forward may give af (fp32 rows, A unused) with rows (int64 gather) and xa (bf16
     copy of the converted rows); the input gradient may give b_kn=1 (B = W[out, in]); a
     PARTIAL_TN weight gradient may give sum_col (slab column receiving sum_k A = the bias
     gradient)."""
-    def mk(j):
-        g = lambda k: j.get(k)  # noqa: E731
-        ld = lambda t: 0 if t is None else t.stride(0)  # noqa: E731
-        af = g("af")
-        return GemmJob(_p(g("A")), _p(j["B"]), _p(g("bias")), _p(g("yprev")), _p(g("cf")), _p(g("cb")), _p(g("ct")),
-                       ld(g("A")), j["B"].stride(0), ld(g("yprev")),
-                       0 if g("cf") is None else g("cf").shape[-1], ld(g("cb")), ld(g("ct")), j["M"], j["N"], j["K"],
-                       _p(af), _p(g("rows")), _p(g("xa")), ld(af), 0 if af is None else af.shape[1], ld(g("xa")),
-                       int(bool(g("b_kn"))), int(g("sum_col") or 0))
-    arr = (GemmJob * len(jobs))(*[mk(j) for j in jobs])
+    arr = (GemmJob * len(jobs))(*[_gemm_job(j) for j in jobs])
     _ok(load().pmlp_gemm(epi, len(jobs), arr, ksplit, _stream()), "pmlp_gemm")
 
 
