@@ -94,9 +94,9 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-# the committed rocprofv3 summaries of the current build (tools/gpu_round4_profile.sh; the
-# round-3 set until the round-4 one is committed)
-PROFILE_DIR = next((d for d in (os.path.join(ROOT, "profiles", r, "env_go2_4096") for r in ("round4", "round3"))
+# the committed rocprofv3 summaries of the current build (tools/gpu_round5_profile.sh; the
+# newest round that has them)
+PROFILE_DIR = next((d for d in (os.path.join(ROOT, "profiles", r, "env_go2_4096") for r in ("round5", "round4", "round3"))
                     if os.path.exists(os.path.join(d, "pmc_k_step.json"))),
                    os.path.join(ROOT, "profiles", "round3", "env_go2_4096"))
 

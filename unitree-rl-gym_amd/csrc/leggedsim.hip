@@ -417,6 +417,15 @@ struct Smem {
     float tgt[ROWS];
     int c_body[ROWS / 3];
     int c_body2[ROWS / 3];    // self contact: the second body (its force enters with a minus sign)
+    // PGS (two envs per wave): coupling block of contact c+1's rows with contact c's,
+    // cpl[c][3k + j] = A[3(c+1)+k][3c+j] (16-byte rows), for the speculative v below
+    __attribute__((aligned(16))) float cpl[ROWS / 4][12];
+    // PGS (two envs per wave): the sweep-invariant constants, read per update (uniform LDS
+    // reads issued with the v broadcasts) instead of held in ~64 VGPRs per lane:
+    // pkc[c] = {target, 1/A_rr of the normal row, 1/A of friction rows 1 and 2, A[r+1][r],
+    // A[r+2][r], -, -}; pkl[l] = {target, 1/A_rr} of limit row l
+    __attribute__((aligned(16))) float pkc[ROWS / 4][8];
+    __attribute__((aligned(8))) float pkl[ROWS - 3 * (ROWS / 4)][2];
     float c_pt[ROWS / 3][3];
     float c_fr[ROWS / 3][9];  // contact frame: normal, tangent 1, tangent 2
     float c_sep[ROWS / 3];
@@ -921,7 +930,12 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                 may = gap - sp.rest_offset < sp.contact_offset + LGS_PREFILTER_MARGIN;
             }
         }
-        touch = (uint32_t)hballot<EPW>(may);
+        // WAVE-uniform (two envs per wave: either env's bodies): the candidate loop below has a
+        // barrier in it, so its trip through the chunks must not differ between the halves.  A
+        // chunk run for the other env's bodies finds nothing the pre-filter ruled out (it only
+        // skips candidates that cannot be active): the same contacts, bit for bit.
+        const uint64_t mw = __ballot(may);
+        touch = (uint32_t)mw | (uint32_t)(mw >> 32);
     }
     __syncthreads();
     STAMP(7);
@@ -1000,7 +1014,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         int np = 0, nsec = 0;
         const int nch = (md.P + WAVE / EPW - 1) / (WAVE / EPW);
         for (int ch = 0; ch < nch; ++ch) {
-            if (!(chunk_bodies<EPW>(mc, ch) & touch)) continue;  // (env-uniform)
+            if (!(chunk_bodies<EPW>(mc, ch) & touch)) continue;  // (wave-uniform: touch above)
             const int k = ch * (WAVE / EPW) + lane;
             bool act = false;
             float c[3] = {0.f, 0.f, 0.f}, sep = 0.f, rad = 0.f, nrm[3] = {0.f, 0.f, 1.f};
@@ -1307,48 +1321,72 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         // acol (32 lane masks, which spilled SGPRs into VGPR lanes)
         float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
         if constexpr (EPW == 2) {
-            // the sweep-invariant per-row constants broadcast once (256 VGPRs at 2 waves/SIMD
-            // hold them): targets, 1/A_rr, a contact's normal-friction couplings.  The
-            // dependency chain of a contact update then carries 3 broadcasts (v) instead of 12.
-            float ptg[ROWS], pinv[ROWS], pa1[CM], pa2[CM];
+            // the sweep-invariant per-row constants into LDS (each row's lane writes its own;
+            // a friction row also its coupling with the contact's normal row)
+            if (used) {
+                if (lane < 3 * CM) {
+                    const int d3 = lane % 3;
+                    float* q = s.pkc[lane / 3];
+                    if (d3 == 0) { q[0] = tg; q[1] = inv; }
+                    else q[1 + d3] = inv;
 #pragma unroll
-            for (int r = 0; r < ROWS; ++r) { ptg[r] = 0.f; pinv[r] = 0.f; }
-#pragma unroll
-            for (int c = 0; c < CM; ++c) {
-                pa1[c] = 0.f; pa2[c] = 0.f;
-                if (c < nc) {
-                    const int r = 3 * c;
-                    ptg[r] = bc<EPW>(tg, r);
-                    pinv[r] = bc<EPW>(inv, r); pinv[r + 1] = bc<EPW>(inv, r + 1); pinv[r + 2] = bc<EPW>(inv, r + 2);
-                    pa1[c] = bc<EPW>(acol[r], r + 1); pa2[c] = bc<EPW>(acol[r], r + 2);
+                    for (int c = 0; c < CM; ++c)
+                        if (lane == 3 * c + 1 || lane == 3 * c + 2) q[3 + d3] = acol[3 * c];
+                } else {
+                    s.pkl[lane - 3 * CM][0] = tg; s.pkl[lane - 3 * CM][1] = inv;
                 }
             }
+            // Speculative v: the rows of contact c+1 take their v from a broadcast issued at the
+            // START of contact c (before its update), then apply contact c's impulse changes with
+            // the fma chain their owner lanes apply (coupling A[3(c+1)+k][3c+j] from s.cpl): the
+            // owner's bits, with the broadcast round trip off the contact-to-contact chain.  The
+            // rows of contact c+1 write its coupling block from their own columns of A.
+            if (nc > 1) {
 #pragma unroll
-            for (int l = 0; l < LM; ++l)
-                if (l < nlimit) {
-                    const int r = 3 * CM + l;
-                    ptg[r] = bc<EPW>(tg, r);
-                    pinv[r] = bc<EPW>(inv, r);
-                }
+                for (int c = 0; c + 1 < CM; ++c)
+                    if (c + 1 < nc && lane >= 3 * (c + 1) && lane < 3 * (c + 2)) {
+                        float* kp = s.cpl[c] + 3 * (lane - 3 * (c + 1));
+                        kp[0] = acol[3 * c]; kp[1] = acol[3 * c + 1]; kp[2] = acol[3 * c + 2];
+                    }
+            }
+            __syncthreads();
             for (int it = 0; it < sp.iters; ++it) {
                 // opaque row counts per sweep: the per-row guards are recomputed (one s_cmp
                 // each) instead of held across the sweeps as hoisted lane masks (SGPR spills)
                 int ncs = nc, ncgs = ncg, nls = nlimit, nos = nover;
                 asm volatile("" : "+v"(ncs), "+v"(ncgs), "+v"(nls), "+v"(nos));
+                // opaque per sweep: the constant and coupling loads stay in the sweep (not hoisted
+                // into live VGPRs)
+                int ko = 0;
+                asm volatile("" : "+v"(ko));
+                // v at the rows of the contact being updated (the first: a plain broadcast)
+                float sn = 0.f, s1 = 0.f, s2 = 0.f;
+                if (ncs > 0) { sn = bc<EPW>(v, 0); s1 = bc<EPW>(v, 1); s2 = bc<EPW>(v, 2); }
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < ncs) {
                         const int r = 3 * c;
+                        // the next contact's v before this update, and its coupling block: both issued
+                        // here, ahead of this contact's chain
+                        float nn = 0.f, n1 = 0.f, n2s = 0.f;
+                        float4 ka = make_float4(0.f, 0.f, 0.f, 0.f), kb = ka, kc = ka;
+                        const float4 pq = *(const float4*)(s.pkc[c] + ko);
+                        const float2 pa = *(const float2*)(s.pkc[c] + 4 + ko);
+                        if (c + 1 < CM && c + 1 < ncs) {
+                            nn = bc<EPW>(v, r + 3); n1 = bc<EPW>(v, r + 4); n2s = bc<EPW>(v, r + 5);
+                            const float4* kq = (const float4*)(s.cpl[c] + ko);
+                            ka = kq[0]; kb = kq[1]; kc = kq[2];
+                        }
                         const float lno = lamv[r], l1o = lamv[r + 1], l2o = lamv[r + 2];
-                        const float vn = bc<EPW>(v, r), v1 = bc<EPW>(v, r + 1), v2 = bc<EPW>(v, r + 2);
-                        const float ln = fmaxf(0.f, lno + (ptg[r] - vn) * pinv[r]);
+                        const float vn = sn, v1 = s1, v2 = s2;
+                        const float ln = fmaxf(0.f, lno + (pq.x - vn) * pq.y);
                         const float dn = ln - lno;
                         v = fmaf(acol[r], dn, v);
-                        const float v1n = fmaf(pa1[c], dn, v1);
-                        const float v2n = fmaf(pa2[c], dn, v2);
+                        const float v1n = fmaf(pa.x, dn, v1);
+                        const float v2n = fmaf(pa.y, dn, v2);
                         const float lim = (c < ncgs ? mu : mus) * ln;
-                        float l1 = l1o - v1n * pinv[r + 1];
-                        float l2 = l2o - v2n * pinv[r + 2];
+                        float l1 = l1o - v1n * pq.z;
+                        float l2 = l2o - v2n * pq.w;
                         // cone test on squared norms (the oracle's): sqrt and division only
                         // when the impulse is projected onto the cone
                         const float n2 = l1 * l1 + l2 * l2;
@@ -1360,6 +1398,11 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                         const float d1 = l1 - l1o, d2 = l2 - l2o;
                         v = fmaf(acol[r + 2], d2, fmaf(acol[r + 1], d1, v));
                         lamv[r] = ln; lamv[r + 1] = l1; lamv[r + 2] = l2;
+                        if (c + 1 < CM && c + 1 < ncs) {
+                            sn = fmaf(ka.z, d2, fmaf(ka.y, d1, fmaf(ka.x, dn, nn)));
+                            s1 = fmaf(kb.y, d2, fmaf(kb.x, d1, fmaf(ka.w, dn, n1)));
+                            s2 = fmaf(kc.x, d2, fmaf(kb.w, d1, fmaf(kb.z, dn, n2s)));
+                        }
                     }
                 }
 #pragma unroll
@@ -1367,7 +1410,8 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     if (l < nls) {
                         const int r = 3 * CM + l;
                         const float lo = lamv[r];
-                        const float ln = fmaxf(0.f, lo + (ptg[r] - bc<EPW>(v, r)) * pinv[r]);
+                        const float2 pl = *(const float2*)(s.pkl[l] + ko);
+                        const float ln = fmaxf(0.f, lo + (pl.x - bc<EPW>(v, r)) * pl.y);
                         v = fmaf(acol[r], ln - lo, v);
                         lamv[r] = ln;
                     }
