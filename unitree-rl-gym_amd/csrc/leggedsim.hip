@@ -158,6 +158,7 @@ struct DevState {
     const float* added_mass;  // [N]
     const float* torques_in;  // [N,D] (lgs_simulate)
     float* vsim;              // [N,2] the step's base xy velocity before the all-env push draw (k_step_extras)
+    unsigned* pushed;         // [2] "some env was pushed" per step parity (k_step sets, k_step_extras reads)
 };
 
 __device__ __forceinline__ float rl(float x, int l) {
@@ -417,15 +418,6 @@ struct Smem {
     float tgt[ROWS];
     int c_body[ROWS / 3];
     int c_body2[ROWS / 3];    // self contact: the second body (its force enters with a minus sign)
-    // PGS (two envs per wave): coupling block of contact c+1's rows with contact c's,
-    // cpl[c][3k + j] = A[3(c+1)+k][3c+j] (16-byte rows), for the speculative v below
-    __attribute__((aligned(16))) float cpl[ROWS / 4][12];
-    // PGS (two envs per wave): the sweep-invariant constants, read per update (uniform LDS
-    // reads issued with the v broadcasts) instead of held in ~64 VGPRs per lane:
-    // pkc[c] = {target, 1/A_rr of the normal row, 1/A of friction rows 1 and 2, A[r+1][r],
-    // A[r+2][r], -, -}; pkl[l] = {target, 1/A_rr} of limit row l
-    __attribute__((aligned(16))) float pkc[ROWS / 4][8];
-    __attribute__((aligned(8))) float pkl[ROWS - 3 * (ROWS / 4)][2];
     float c_pt[ROWS / 3][3];
     float c_fr[ROWS / 3][9];  // contact frame: normal, tangent 1, tangent 2
     float c_sep[ROWS / 3];
@@ -1321,72 +1313,48 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
         // acol (32 lane masks, which spilled SGPRs into VGPR lanes)
         float inv = used ? 1.f / (dg + 1e-9f) : 0.f;
         if constexpr (EPW == 2) {
-            // the sweep-invariant per-row constants into LDS (each row's lane writes its own;
-            // a friction row also its coupling with the contact's normal row)
-            if (used) {
-                if (lane < 3 * CM) {
-                    const int d3 = lane % 3;
-                    float* q = s.pkc[lane / 3];
-                    if (d3 == 0) { q[0] = tg; q[1] = inv; }
-                    else q[1 + d3] = inv;
+            // the sweep-invariant per-row constants broadcast once (256 VGPRs at 2 waves/SIMD
+            // hold them): targets, 1/A_rr, a contact's normal-friction couplings.  The
+            // dependency chain of a contact update then carries 3 broadcasts (v) instead of 12.
+            float ptg[ROWS], pinv[ROWS], pa1[CM], pa2[CM];
 #pragma unroll
-                    for (int c = 0; c < CM; ++c)
-                        if (lane == 3 * c + 1 || lane == 3 * c + 2) q[3 + d3] = acol[3 * c];
-                } else {
-                    s.pkl[lane - 3 * CM][0] = tg; s.pkl[lane - 3 * CM][1] = inv;
+            for (int r = 0; r < ROWS; ++r) { ptg[r] = 0.f; pinv[r] = 0.f; }
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+                pa1[c] = 0.f; pa2[c] = 0.f;
+                if (c < nc) {
+                    const int r = 3 * c;
+                    ptg[r] = bc<EPW>(tg, r);
+                    pinv[r] = bc<EPW>(inv, r); pinv[r + 1] = bc<EPW>(inv, r + 1); pinv[r + 2] = bc<EPW>(inv, r + 2);
+                    pa1[c] = bc<EPW>(acol[r], r + 1); pa2[c] = bc<EPW>(acol[r], r + 2);
                 }
             }
-            // Speculative v: the rows of contact c+1 take their v from a broadcast issued at the
-            // START of contact c (before its update), then apply contact c's impulse changes with
-            // the fma chain their owner lanes apply (coupling A[3(c+1)+k][3c+j] from s.cpl): the
-            // owner's bits, with the broadcast round trip off the contact-to-contact chain.  The
-            // rows of contact c+1 write its coupling block from their own columns of A.
-            if (nc > 1) {
 #pragma unroll
-                for (int c = 0; c + 1 < CM; ++c)
-                    if (c + 1 < nc && lane >= 3 * (c + 1) && lane < 3 * (c + 2)) {
-                        float* kp = s.cpl[c] + 3 * (lane - 3 * (c + 1));
-                        kp[0] = acol[3 * c]; kp[1] = acol[3 * c + 1]; kp[2] = acol[3 * c + 2];
-                    }
-            }
-            __syncthreads();
+            for (int l = 0; l < LM; ++l)
+                if (l < nlimit) {
+                    const int r = 3 * CM + l;
+                    ptg[r] = bc<EPW>(tg, r);
+                    pinv[r] = bc<EPW>(inv, r);
+                }
             for (int it = 0; it < sp.iters; ++it) {
                 // opaque row counts per sweep: the per-row guards are recomputed (one s_cmp
                 // each) instead of held across the sweeps as hoisted lane masks (SGPR spills)
                 int ncs = nc, ncgs = ncg, nls = nlimit, nos = nover;
                 asm volatile("" : "+v"(ncs), "+v"(ncgs), "+v"(nls), "+v"(nos));
-                // opaque per sweep: the constant and coupling loads stay in the sweep (not hoisted
-                // into live VGPRs)
-                int ko = 0;
-                asm volatile("" : "+v"(ko));
-                // v at the rows of the contact being updated (the first: a plain broadcast)
-                float sn = 0.f, s1 = 0.f, s2 = 0.f;
-                if (ncs > 0) { sn = bc<EPW>(v, 0); s1 = bc<EPW>(v, 1); s2 = bc<EPW>(v, 2); }
 #pragma unroll
                 for (int c = 0; c < CM; ++c) {
                     if (c < ncs) {
                         const int r = 3 * c;
-                        // the next contact's v before this update, and its coupling block: both issued
-                        // here, ahead of this contact's chain
-                        float nn = 0.f, n1 = 0.f, n2s = 0.f;
-                        float4 ka = make_float4(0.f, 0.f, 0.f, 0.f), kb = ka, kc = ka;
-                        const float4 pq = *(const float4*)(s.pkc[c] + ko);
-                        const float2 pa = *(const float2*)(s.pkc[c] + 4 + ko);
-                        if (c + 1 < CM && c + 1 < ncs) {
-                            nn = bc<EPW>(v, r + 3); n1 = bc<EPW>(v, r + 4); n2s = bc<EPW>(v, r + 5);
-                            const float4* kq = (const float4*)(s.cpl[c] + ko);
-                            ka = kq[0]; kb = kq[1]; kc = kq[2];
-                        }
                         const float lno = lamv[r], l1o = lamv[r + 1], l2o = lamv[r + 2];
-                        const float vn = sn, v1 = s1, v2 = s2;
-                        const float ln = fmaxf(0.f, lno + (pq.x - vn) * pq.y);
+                        const float vn = bc<EPW>(v, r), v1 = bc<EPW>(v, r + 1), v2 = bc<EPW>(v, r + 2);
+                        const float ln = fmaxf(0.f, lno + (ptg[r] - vn) * pinv[r]);
                         const float dn = ln - lno;
                         v = fmaf(acol[r], dn, v);
-                        const float v1n = fmaf(pa.x, dn, v1);
-                        const float v2n = fmaf(pa.y, dn, v2);
+                        const float v1n = fmaf(pa1[c], dn, v1);
+                        const float v2n = fmaf(pa2[c], dn, v2);
                         const float lim = (c < ncgs ? mu : mus) * ln;
-                        float l1 = l1o - v1n * pq.z;
-                        float l2 = l2o - v2n * pq.w;
+                        float l1 = l1o - v1n * pinv[r + 1];
+                        float l2 = l2o - v2n * pinv[r + 2];
                         // cone test on squared norms (the oracle's): sqrt and division only
                         // when the impulse is projected onto the cone
                         const float n2 = l1 * l1 + l2 * l2;
@@ -1398,11 +1366,6 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                         const float d1 = l1 - l1o, d2 = l2 - l2o;
                         v = fmaf(acol[r + 2], d2, fmaf(acol[r + 1], d1, v));
                         lamv[r] = ln; lamv[r + 1] = l1; lamv[r + 2] = l2;
-                        if (c + 1 < CM && c + 1 < ncs) {
-                            sn = fmaf(ka.z, d2, fmaf(ka.y, d1, fmaf(ka.x, dn, nn)));
-                            s1 = fmaf(kb.y, d2, fmaf(kb.x, d1, fmaf(ka.w, dn, n1)));
-                            s2 = fmaf(kc.x, d2, fmaf(kb.w, d1, fmaf(kb.z, dn, n2s)));
-                        }
                     }
                 }
 #pragma unroll
@@ -1410,8 +1373,7 @@ __device__ void substep(Smem<D, B, ROWS>* sm, const ModelCache<D, B>& mc, const 
                     if (l < nls) {
                         const int r = 3 * CM + l;
                         const float lo = lamv[r];
-                        const float2 pl = *(const float2*)(s.pkl[l] + ko);
-                        const float ln = fmaxf(0.f, lo + (pl.x - bc<EPW>(v, r)) * pl.y);
+                        const float ln = fmaxf(0.f, lo + (ptg[r] - bc<EPW>(v, r)) * pinv[r]);
                         v = fmaf(acol[r], ln - lo, v);
                         lamv[r] = ln;
                     }
@@ -2006,7 +1968,7 @@ enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
 template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                              const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL,
-                             float* vsim = nullptr) {
+                             float* vsim = nullptr, unsigned* pushed = nullptr) {
     const int lane = hl<EPW>();
     const int A = T.num_actions;
     const int Ad = PAD ? A : D;  // (unpadded: num_actions == D, a compile-time bound)
@@ -2078,6 +2040,7 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     if (lane == 0 && T.push_robots && E.episode_length[e] % T.push_interval == 0) {
         s.root[7] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy, philox_uniform(seed, e, step, LGS_STREAM_PUSH, 0));
         s.root[8] = rand_range(-T.max_push_vel_xy, T.max_push_vel_xy, philox_uniform(seed, e, step, LGS_STREAM_PUSH, 1));
+        if (pushed) atomicOr(pushed + (step & 1u), 1u);  // (few envs per step: the pushed and the reset ones)
     }
     // compute_observations
     if (lane == 0) {
@@ -2202,7 +2165,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     if (mode != MODE_PHYSICS)
         post_physics<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step, RESET_STEP,
                                       mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL),
-                                      st.vsim);
+                                      st.vsim, st.pushed);
     __syncthreads();
     STAMP(16);
     store_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
@@ -2246,7 +2209,8 @@ __global__ __launch_bounds__(WAVE) void k_reset_all(DevModel md, DevState st, co
 // simulated xy velocity to vsim): this one-workgroup kernel only restores vsim on the
 // rare steps where no env was pushed (it drew 2 Philox per env itself before: 4.6 -> 9.5 us).
 __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const lgs_task_params* __restrict__ Tp,
-                                                      int N, int advance, uint32_t step, const float* vsim) {
+                                                      int N, int advance, uint32_t step, const float* vsim,
+                                                      unsigned* pushed_flag) {
     const lgs_task_params& T = *Tp;
     const int nsum = num_sums(T);
     const float cnt = E.episode_acc[nsum];
@@ -2256,9 +2220,8 @@ __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const l
     if (advance && T.push_robots && E.last_root_vel && vsim) {
         // k_step wrote every env's draw; no env pushed (episode_length % push_interval == 0
         // after this step, reset ones at 0): the simulated velocities go back
-        int pushed = 0;
-        for (int e = t; e < N && !pushed; e += blockDim.x) pushed = (E.episode_length[e] % T.push_interval) == 0;
-        if (!__syncthreads_or(pushed))
+        // (k_step raised this step's flag for every env it pushed: no scan over the envs)
+        if (!pushed_flag[step & 1u])
             for (int e = t; e < N; e += blockDim.x) {
                 E.last_root_vel[6 * e] = vsim[2 * e];
                 E.last_root_vel[6 * e + 1] = vsim[2 * e + 1];
@@ -2274,6 +2237,7 @@ __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const l
         for (int e = t; e < N; e += blockDim.x) E.time_outs_carry[e] = E.time_out[e];
     __syncthreads();
     if (t <= nsum) E.episode_acc[t] = 0.f;
+    if (t == 0 && advance) pushed_flag[(step + 1u) & 1u] = 0u;  // the next step's flag
     if (t == 0 && E.step_counter && advance) *E.step_counter += 1;
 }
 
@@ -2297,6 +2261,7 @@ struct lgs_sim {
     float* friction = nullptr;
     float* added_mass = nullptr;
     float* vsim = nullptr;  // [N,2] scratch of the all-env push bookkeeping (DevState::vsim)
+    unsigned* pushed = nullptr;  // [2] the push flags (DevState::pushed)
     unsigned long long* stats = nullptr;  // [8][LGS_NUM_CONTACT_STATS] capacity-drop counters (DevState::stats)
     float* root = nullptr;
     float* dofs = nullptr;
@@ -2520,6 +2485,7 @@ static DevState state_of(lgs_sim* s) {
     DevState st;
     st.root = s->root; st.dofs = s->dofs; st.cforce = s->cforce; st.rbs = s->rbs;
     st.friction = s->friction; st.added_mass = s->added_mass; st.torques_in = s->torques; st.vsim = s->vsim;
+    st.pushed = s->pushed;
     return st;
 }
 
@@ -2682,6 +2648,8 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->vsim, sizeof(float) * 2 * num_envs));
+    HIP_TRY(hipMalloc(&s->pushed, sizeof(unsigned) * 2));
+    HIP_TRY(hipMemset(s->pushed, 0, sizeof(unsigned) * 2));
     HIP_TRY(hipMalloc(&s->stats, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
     HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
     s->sp.stats = s->stats;
@@ -2703,6 +2671,7 @@ LGS_API int lgs_destroy_sim(lgs_sim* s) {
     (void)hipFree(s->friction);
     (void)hipFree(s->added_mass);
     (void)hipFree(s->vsim);
+    (void)hipFree(s->pushed);
     (void)hipFree(s->stats);
     (void)hipFree(s->task_dev);
     (void)hipFree(s->hf_mem);
@@ -2909,7 +2878,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
     HIP_TRY(hipGetLastError());
     if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
-                           (uint32_t)step_counter, (const float*)s->vsim);
+                           (uint32_t)step_counter, (const float*)s->vsim, s->pushed);
         HIP_TRY(hipGetLastError());
     }
     return LGS_OK;
@@ -2962,7 +2931,7 @@ LGS_API int lgs_reset_idx(lgs_sim* s, const lgs_env_buffers* env, const uint8_t*
     HIP_TRY(hipGetLastError());
     // extras["episode"] over the reset envs and extras["time_outs"]; no step-counter advance
     hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 0,
-                       (uint32_t)step_counter, (const float*)s->vsim);
+                       (uint32_t)step_counter, (const float*)s->vsim, s->pushed);
     HIP_TRY(hipGetLastError());
     return LGS_OK;
 }

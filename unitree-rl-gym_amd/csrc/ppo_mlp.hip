@@ -2449,7 +2449,6 @@ static int gemm_pack(int32_t epi, int32_t njobs, const pmlp_gemm_job* jobs, int3
 //   4: BWD_DX, B [K,N], 128 x 128 tiles, LDS-DMA staging
 // Pairs (1, 2) and (3, 4) share a block size (256 / 512 threads).
 static int gemm_plan(int epi, int mode, const GemmBatch& gb, int njobs, int maxm, int maxn, int maxk) {
-    const bool part = epi == PMLP_EPI_PARTIAL || epi == PMLP_EPI_PARTIAL_TN;
     if (epi == PMLP_EPI_PARTIAL_TN && mode == 0) {
         if (maxm <= 32) return gl_fits<32, 128>(epi, mode, gb, njobs) ? 0 : 1;
         if (maxn > 64) return gl_fits<128, 128>(epi, mode, gb, njobs) && glds_on() == 1 ? 3 : 0;
@@ -2457,7 +2456,6 @@ static int gemm_plan(int epi, int mode, const GemmBatch& gb, int njobs, int maxm
     }
     if (epi == PMLP_EPI_BWD_DX && mode == 2 && maxm > 32 && maxn > 64) {
         const bool small = (long)((maxm + 127) / 128) * ((maxn + 127) / 128) * njobs < 512;
-        (void)part;
         if (small) return !gl_fits<64, 64>(epi, mode, gb, njobs) && maxk <= 16 ? 2 : 0;
         return gl_fits<128, 128>(epi, mode, gb, njobs) ? 4 : 0;
     }
