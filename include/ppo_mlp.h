@@ -260,7 +260,8 @@ PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const u
                              int64_t* draw, void* stream);
 /* The update's mini-batch permutation (RolloutStorage.mini_batch_generator's
  * torch.randperm(num_mini_batches * mini_batch_size)): out[i], i < n, a keyed pseudo-random
- * permutation of [0, n) (4-round Feistel, Philox round function, cycle walking), no sort. */
+ * permutation of [0, n) (4-round alternating Feistel on the ceil(log2 n)-bit domain, Philox
+ * round function, cycle walking), no sort. */
 PMLP_API int pmlp_permutation(int64_t* out, int64_t n, uint64_t seed, void* stream);
 
 /* The whole forward of 4-layer Linear/ELU MLPs (rsl_rl's actor and critic) in ONE launch

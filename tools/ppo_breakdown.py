@@ -18,6 +18,7 @@ args = get_args(["--task", task, "--num_envs", str(n), "--headless"])
 env, _ = task_registry.make_env(name=task, args=args)
 _, tc = task_registry.get_cfgs(task)
 runner = OnPolicyRunner(env, class_to_dict(tc), log_dir=None, device="cuda:0")
+runner.sync_phase_times = True  # device-exact phase times
 runner.learn(2)
 cs, ls = [], []
 for _ in range(iters):

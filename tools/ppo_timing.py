@@ -17,6 +17,7 @@ args = get_args(["--task", "go2", "--num_envs", "4096", "--headless"])
 env, _ = task_registry.make_env(name="go2", args=args)
 _, tc = task_registry.get_cfgs("go2")
 runner = OnPolicyRunner(env, class_to_dict(tc), log_dir=None, device="cuda:0")
+runner.sync_phase_times = True  # device-exact phase times
 runner.learn(3)
 cs, ls = [], []
 for _ in range(5):

@@ -15,6 +15,7 @@ args = get_args(["--task", "go2", "--num_envs", "4096", "--headless"])
 env, _ = task_registry.make_env(name="go2", args=args)
 _, tc = task_registry.get_cfgs("go2")
 runner = OnPolicyRunner(env, class_to_dict(tc), log_dir=None, device="cuda:0")
+runner.sync_phase_times = True  # device-exact phase times
 runner.learn(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
 torch.cuda.synchronize()
 print("done", runner.last_iteration_times)

@@ -54,8 +54,29 @@ __device__ unsigned long long* g_phase_buf;
 #define STAMP_INIT()                                                                             \
     do {                                                                                         \
         if (threadIdx.x < LGS_NPHASE) s.stamps[threadIdx.x] = 0;                                 \
+        if (threadIdx.x == 0) {                                                                  \
+            s.stamps[18] = _wt0; s.stamps[20] = _wr0;                                            \
+            s.stamps[22] = _whw; s.stamps[23] = _wxcc;                                           \
+        }                                                                                        \
+    } while (0)
+// the wave's timeline: shader-clock and 100 MHz real-time stamps at kernel entry and exit,
+// and where it ran (HW_ID: SIMD / CU / SH / SE; XCC_ID), for tools/wave_timeline.py
+#define STAMP_BEGIN()                                                                            \
+    unsigned long long _wt0, _wr0;                                                               \
+    unsigned _whw, _wxcc;                                                                        \
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_getreg_b32 %2, hwreg(HW_REG_HW_ID)\n\t"   \
+                 "s_getreg_b32 %3, hwreg(HW_REG_XCC_ID)\n\ts_waitcnt lgkmcnt(0)"                    \
+                 : "=s"(_wt0), "=s"(_wr0), "=s"(_whw), "=s"(_wxcc)::"memory")
+#define STAMP_END()                                                                              \
+    do {                                                                                         \
+        unsigned long long _t, _r;                                                               \
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"                    \
+                     : "=s"(_t), "=s"(_r)::"memory");                                            \
+        if (threadIdx.x == 0) { s.stamps[19] = _t; s.stamps[21] = _r; }                          \
     } while (0)
 #else
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END() do {} while (0)
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(e) do {} while (0)
 #define STAMP_INIT() do {} while (0)
@@ -2105,6 +2126,7 @@ enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MO
 template <int D, int B, int ROWS, int CH, int EPW, int WPE = 0, bool PAD = false>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (EPW == 2 ? 2 : (ROWS <= 32 ? LGS_WAVES_PER_EU : LGS_WAVES_PER_EU_48))))) void k_step(DevModel md, DevSim sp, DevState st, const lgs_task_params* __restrict__ Tp,
                                                lgs_env_buffers E, int N, uint32_t step, int mode) {
+    STAMP_BEGIN();
     __shared__ Smem<D, B, ROWS> sm[EPW];
     __shared__ ModelCache<D, B> mc;
     const int e = EPW * xcd_env(blockIdx.x, gridDim.x) + hh<EPW>();
@@ -2170,6 +2192,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     STAMP(16);
     store_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
     STAMP(17);
+    STAMP_END();
     STAMP_FLUSH(e);
 }
 
