@@ -49,6 +49,8 @@ def main(task="go2", n=4096, scale=0.5):
           f"p90 {np.percentile(dur, 90):.1f} max {dur.max():.1f}")
     print(f"  wave start us after the first: p50 {np.median(start):.2f} p99 {np.percentile(start, 99):.2f} "
           f"max {start.max():.2f}")
+    print("  waves started by (us): " + ", ".join(f"{q:.0f}: {int((start <= q).sum())}" for q in
+                                                 (1, 10, 50, 100, 150, 200, 250, 300, 400)))
     simd = collections.Counter()
     per_simd_end = collections.defaultdict(float)
     for k in range(len(b)):

@@ -401,7 +401,11 @@ class PPO:
         # stream and the captured update is no longer self-contained (replays race).
         self.actor_critic.distribution = None
 
-    def update(self):
+    def update(self, host_means=True):
+        """The PPO update; returns (mean value loss, mean surrogate loss) as Python floats (a
+        device read-back, as the reference's per-mini-batch .item()), or with host_means=False
+        the device tensor of the two means, so a caller that does not read them (the runner
+        without logging) keeps the host ahead of the device."""
         self.flush_rollout()
         num_updates = self.num_learning_epochs * self.num_mini_batches
         self._graph_calls += 1
@@ -421,8 +425,11 @@ class PPO:
                 gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
             for batch in gen:
                 self._minibatch_step(*batch, acc)
-        means = (acc / num_updates).tolist()
+        means = acc / num_updates
         self.storage.clear()
+        if not host_means:
+            return means
+        means = means.tolist()
         return means[0], means[1]
 
     def _update_fused(self):

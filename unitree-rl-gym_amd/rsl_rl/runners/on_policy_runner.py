@@ -209,7 +209,10 @@ class OnPolicyRunner:
                 collection_time = stop - start
                 start = stop
                 self.alg.compute_returns(critic_obs)
-            mean_value_loss, mean_surrogate_loss = self.alg.update()
+            if self.log_dir is not None or exact:
+                mean_value_loss, mean_surrogate_loss = self.alg.update()
+            else:  # nothing reads the losses: no read-back, the host stays ahead of the device
+                mean_value_loss, mean_surrogate_loss = self.alg.update(host_means=False)
             sync()
             stop = time.time()
             learn_time = stop - start
