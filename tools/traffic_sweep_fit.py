@@ -1,4 +1,4 @@
-"""Linear fit of the Go2 k_step traffic counters against the env count (tools/gpu_traffic_sweep.sh).
+"""Linear fit of the k_step traffic counters against the env count (tools/gpu_traffic_sweep.sh).
 
 Per build (shipped, I/O-only) and counter (FETCH_SIZE, WRITE_SIZE): counted bytes per launch =
 intercept + slope * envs, least squares over 512 / 1024 / 2048 / 4096 envs.  The intercept is
@@ -6,8 +6,10 @@ per-launch traffic that does not scale with envs (instruction fetch, the model b
 parameter structs); the slope is per-env traffic.  The I/O-only build moves a known byte count
 per env (tools/traffic_calib.py go2_io_bytes), so its slopes are the counters' tally factors
 for this access pattern; the shipped slopes divided by them are the shipped kernel's HBM
-bytes per env, compared with its own I/O bytes (<= 1.15x).
-usage: python tools/traffic_sweep_fit.py <sweep_dir> [out.json]"""
+bytes per env, compared with its own I/O bytes (<= 1.15x).  For the other
+robots (no hand-counted I/O list) the comparison is tally-free: the shipped slope over the
+I/O-only slope, per counter (the same access pattern, so the tally factor cancels).
+usage: python tools/traffic_sweep_fit.py <sweep_dir> [out.json] [task]"""
 import glob
 import json
 import os
@@ -27,16 +29,18 @@ def fit(ns, ys):
     return float(a), float(b), r2
 
 
-def main(d, out=None):
+def main(d, out=None, task="go2"):
     data = {}
     for f in glob.glob(os.path.join(d, "*_*", "pmc_k_step.json")):
         lib, n = os.path.basename(os.path.dirname(f)).rsplit("_", 1)
         j = json.load(open(f))
         data.setdefault(lib, []).append((int(n), j["fetch_size_kib"] * 1024.0, j["write_size_kib"] * 1024.0,
                                          j.get("avg_ns")))
-    rd, wr = go2_io_bytes()
-    known_r, known_w = sum(rd.values()), sum(wr.values())
-    res = {"known_io_bytes_per_env": {"read": known_r, "write": known_w}}
+    res = {"task": task}
+    if task == "go2":
+        rd, wr = go2_io_bytes()
+        known_r, known_w = sum(rd.values()), sum(wr.values())
+        res["known_io_bytes_per_env"] = {"read": known_r, "write": known_w}
     for lib, rows in data.items():
         rows.sort()
         ns = [r[0] for r in rows]
@@ -46,6 +50,10 @@ def main(d, out=None):
                     "fetch_fit": {"intercept": fr[0], "slope_per_env": fr[1], "r2": fr[2]},
                     "write_fit": {"intercept": fw[0], "slope_per_env": fw[1], "r2": fw[2]}}
     if "io" in res and "shipped" in res:
+        res["shipped_over_io_per_env"] = {
+            k: res["shipped"][f"{k}_fit"]["slope_per_env"] / res["io"][f"{k}_fit"]["slope_per_env"]
+            for k in ("fetch", "write")}
+    if "io" in res and "shipped" in res and task == "go2":
         tr = res["io"]["fetch_fit"]["slope_per_env"] / known_r  # counted bytes per true byte
         tw = res["io"]["write_fit"]["slope_per_env"] / known_w
         sr = res["shipped"]["fetch_fit"]["slope_per_env"] / tr
@@ -67,4 +75,4 @@ def main(d, out=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    main(*sys.argv[1:4])
