@@ -265,6 +265,36 @@ def test_fused_rollout_act_and_store_match_reference_semantics():
         alg.act(obs, obs)
 
 
+def test_compute_returns_last_values_are_bitwise_evaluate():
+    """compute_returns takes the last values from one launch of the critic's fused forward
+    (FusedRollout.values) instead of ActorCritic.evaluate's layer GEMMs: the same bits, and
+    the same GAE results as the evaluate path."""
+    torch.manual_seed(0)
+    N, T, O, A = 4096, 4, 48, 12
+    alg = PPO(ActorCritic(O, O, A, [512, 256, 128], [512, 256, 128]).cuda(), device="cuda")
+    alg.init_storage(N, T, [O], [None], [A])
+    assert isinstance(alg._rollout, fused_step.FusedRollout)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    cobs = torch.randn(N, O, device="cuda", generator=g)
+    with torch.inference_mode():
+        v = alg._rollout.values(cobs).clone()
+        ref = alg.actor_critic.evaluate(cobs).detach()
+    assert v.shape == ref.shape and torch.equal(v, ref)
+    st = alg.storage
+    for k in ("values", "rewards"):
+        getattr(st, k).copy_(torch.randn(getattr(st, k).shape, device="cuda", generator=g))
+    st.dones.copy_(torch.rand(st.dones.shape, device="cuda", generator=g) < 0.1)
+    st.step = T
+    with torch.inference_mode():
+        alg.compute_returns(cobs)
+    got = (st.returns.clone(), st.advantages.clone())
+    ro, alg._rollout = alg._rollout, None  # the evaluate path
+    with torch.inference_mode():
+        alg.compute_returns(cobs)
+    alg._rollout = ro
+    assert torch.equal(got[0], st.returns) and torch.equal(got[1], st.advantages)
+
+
 @pytest.mark.parametrize("K,ks", [(24576, 1152), (1000, 320)])
 def test_partial_tn_gemm_matches_transposed_partial_and_fp32(K, ks):
     """Weight-gradient GEMM read from the row-major activations (PARTIAL_TN, LDS-transposed

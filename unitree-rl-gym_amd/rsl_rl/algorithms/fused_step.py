@@ -409,6 +409,20 @@ class FusedRollout:
             mm._gemm(mm.EPI_FWD_OUT if last else mm.EPI_FWD_HIDDEN, gj)
         return self.out
 
+    def values(self, cobs):
+        """ActorCritic.evaluate on N rows (compute_returns' last values) as ONE launch of the
+        critic's fused forward (bitwise the per-layer GEMMs evaluate runs: 4-5 launches), or
+        None when the rows do not fit the fused path."""
+        f = self.f
+        if not (f.fused_fwd and cobs.is_cuda and cobs.dtype == torch.float32 and cobs.dim() == 2 and
+                cobs.shape == (self.N, f.lins[1][0].in_features) and cobs.is_contiguous()):
+            return None
+        f.ensure_weights()
+        mm.mlp_forward([dict(x=cobs, kx=f.lins[1][0].in_features, K0=f.k0p[1], W=f.wb[1],
+                             Wf=f.wf[1] if f.wf else None, b=[lin.bias.detach() for lin in f.lins[1]],
+                             N=[lin.out_features for lin in f.lins[1]], out=self.out[1])], self.N)
+        return self.out[1]
+
     def act(self, obs, cobs, storage, t):
         """PPO.act + add_transitions for storage step t, and the previous step's deferred
         process_env_step, in the forward's launch (pmlp_rollout_forward): one launch per env

@@ -213,7 +213,11 @@ class PPO:
 
     def compute_returns(self, last_critic_obs):
         self.flush_rollout()
-        last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        last_values = None
+        if isinstance(self._rollout, fused_step.FusedRollout):  # one launch instead of the layer GEMMs
+            last_values = self._rollout.values(last_critic_obs)
+        if last_values is None:
+            last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         if self._fused is not None or (str(self.device).startswith("cuda") and last_values.is_cuda):
             # GAE + normalisation: two launches (+ a moments all-reduce across ranks)
             fused_step.gae(self.storage, last_values, self.gamma, self.lam, self.world_size)
