@@ -2136,6 +2136,15 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     const lgs_task_params& T = *Tp;
     const int lane = hl<EPW>();
     load_model(mc, md);
+#ifdef LGS_DIAG_MULTISTEP
+    // diagnostic build (never the shipped library): LGS_DIAG_MULTISTEP control steps per launch
+    // on the same actions, no kernel boundary between them -- what a multi-step rollout kernel
+    // would save of the per-launch barrier (the launch ends with its slowest wave)
+    const uint32_t step0 = step;
+    for (int tt = 0; tt < LGS_DIAG_MULTISTEP; ++tt) {
+    step = step0 + (uint32_t)tt;
+    __syncthreads();
+#endif
     load_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
     const int A = T.num_actions;
     const int Ad = PAD ? A : D, Br = PAD ? md.Br : B;  // (unpadded: compile-time bounds)
@@ -2194,6 +2203,9 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     STAMP(17);
     STAMP_END();
     STAMP_FLUSH(e);
+#ifdef LGS_DIAG_MULTISTEP
+    }
+#endif
 }
 
 // reset_idx: every env (mask == NULL, BaseTask.reset) or the envs whose mask byte is set
