@@ -145,6 +145,23 @@ def load_sq_valu(kernel_ms):
             "valu_insts_per_launch": sq["valu_insts_per_launch"], "share_of_wave_time": sq.get("share_of_wave_time")}
 
 
+def load_wave_timeline():
+    """The env-step launch's wave timeline from the committed stamps-build summary
+    (profiles/round5/env_go2_4096/wave_timeline.txt, tools/wave_timeline.py): the launch ends
+    with its slowest wave, so the median wave's duration against the span is the share of the
+    launch the per-step barrier costs."""
+    import re
+    try:
+        txt = open(os.path.join(PROFILE_DIR, "wave_timeline.txt")).read()
+        span = float(re.search(r"launch span ([\d.]+) us", txt).group(1))
+        med = float(re.search(r"median ([\d.]+) p90", txt).group(1))
+        mx = float(re.search(r"p90 [\d.]+ max ([\d.]+)", txt).group(1))
+    except Exception:
+        return None
+    return {"median_wave_us": med, "max_wave_us": mx, "span_us": span, "median_over_span": round(med / span, 3),
+            "source": os.path.relpath(os.path.join(PROFILE_DIR, "wave_timeline.txt"), ROOT)}
+
+
 def _cpu_share():
     """The CPUs this process may use: its affinity mask and the cgroup v2 cpu.max quota."""
     try:
@@ -482,7 +499,8 @@ def main():
                      "traffic_profile_avg_ns": pmc.get("avg_ns"), "traffic_calibration": pmc.get("calibration"),
                      "traffic_profile": os.path.relpath(PROFILE_DIR, ROOT),
                      "kernel": pmc.get("kernel", "k_step (fused Go2 control step)"),
-                     "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms)},
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "valu": load_sq_valu(kernel_ms),
+                     "waves": load_wave_timeline()},
     }
     if world == 1 and not args.no_other_configs:
         # the other BASELINE configs on this GPU (not this line's metric): G1 rough heightfield
