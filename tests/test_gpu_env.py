@@ -161,6 +161,26 @@ def test_ppo_training_smoke():
         assert torch.isfinite(p).all()
 
 
+def test_runner_without_device_syncs_trains_the_same_parameters():
+    """OnPolicyRunner.learn without the device sync after the collection and without the loss
+    read-back (no log directory: the host runs ahead of the device) trains bitwise the same
+    parameters as with the syncs (sync_phase_times = True)."""
+    from legged_gym.utils.helpers import class_to_dict
+    from rsl_rl.runners import OnPolicyRunner
+    params = []
+    for exact in (True, False):
+        env = make("go2", 512)
+        _, train_cfg = task_registry.get_cfgs("go2")
+        runner = OnPolicyRunner(env, class_to_dict(train_cfg), log_dir=None, device="cuda:0")
+        runner.sync_phase_times = exact
+        torch.manual_seed(123)
+        runner.learn(3, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+        params.append([p.detach().clone() for p in runner.alg.actor_critic.parameters()])
+    for a, b in zip(*params):
+        assert torch.equal(a, b)
+
+
 def test_recurrent_humanoid_training_smoke():
     from legged_gym.utils.helpers import class_to_dict
     from rsl_rl.runners import OnPolicyRunner
