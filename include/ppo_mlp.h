@@ -258,6 +258,13 @@ PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, co
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream);
+/* pmlp_store_step plus ActorCriticRecurrent.reset(dones) (each memory's Memory.reset:
+ * hidden_state.masked_fill_(dones, 0)) in the same launch: the nstates (<= PMLP_MAX_MEM_STATES)
+ * state buffers [N, H] (H a multiple of 4, 16-byte aligned) get zero rows for the done envs. */
+#define PMLP_MAX_MEM_STATES 4
+PMLP_API int pmlp_store_step_reset(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                                   const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                                   int64_t* draw, int32_t nstates, float* const* states, int32_t H, void* stream);
 /* The update's mini-batch permutation (RolloutStorage.mini_batch_generator's
  * torch.randperm(num_mini_batches * mini_batch_size)): out[i], i < n, a keyed pseudo-random
  * permutation of [0, n) (4-round alternating Feistel on the ceil(log2 n)-bit domain, Philox

@@ -452,3 +452,20 @@ def test_name_queries_match_the_model(task):
     assert env.sim.find_dof(env.model.dof_names[-1]) == len(env.model.dof_names) - 1
     lib = env.sim.lib
     assert lib.lgs_get_body_name(env.sim.handle, len(env.model.body_names)) is None
+
+
+def test_humanoid_feet_state_is_the_feet_rows_after_each_step():
+    """h1_env.py:48-56's feet_state / feet_pos / feet_vel: the feet rows of the rigid body
+    states after the step (gathered when read, no launch per step), and a task's own
+    assignment is kept."""
+    env = make("h1", 64)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(3):
+        env.step(0.3 * torch.randn(env.num_envs, env.num_actions, device="cuda", generator=g))
+        rows = env.rigid_body_states_view[:, env.feet_indices, :]
+        assert env.feet_state.shape == (env.num_envs, len(env.feet_indices), 13)
+        assert torch.equal(env.feet_state, rows)
+        assert torch.equal(env.feet_pos, rows[:, :, :3]) and torch.equal(env.feet_vel, rows[:, :, 7:10])
+    own = torch.zeros(3)
+    env.feet_pos = own
+    assert env.feet_pos is own

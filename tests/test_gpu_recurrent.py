@@ -500,3 +500,34 @@ def test_recurrent_rollout_draws_fresh_noise_every_step_and_iteration():
             assert same < 0.01, (i, j, same)
     z = torch.stack(zs)
     assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1.0) < 0.02
+
+
+def test_recurrent_store_zeroes_the_done_envs_memories_as_reset():
+    """The recurrent rollout's store launch zeroes the done envs' (h, c) of both memories
+    itself (pmlp_store_step_reset): bitwise ActorCriticRecurrent.reset(dones) (masked_fill_
+    with 0), the other envs' states untouched, and PPO.process_env_step then skips the
+    torch statement."""
+    torch.manual_seed(5)
+    N, T, O, P, A, H = 256, 3, 47, 50, 12, 64
+    ac = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                              rnn_hidden_size=H, rnn_num_layers=1).cuda()
+    alg = PPO(ac, device="cuda")
+    alg.init_storage(N, T, [O], [P], [A])
+    g = torch.Generator(device="cuda").manual_seed(2)
+    obs, cobs = torch.randn(N, O, device="cuda", generator=g), torch.randn(N, P, device="cuda", generator=g)
+    calls = []
+    real_reset = ac.reset
+    ac.reset = lambda dones=None: (calls.append(1), real_reset(dones))[1]
+    for t in range(T):
+        with torch.inference_mode():
+            alg.act(obs, cobs)
+            before = [h.clone() for m in (ac.memory_a, ac.memory_c) for h in m.hidden_states]
+            assert all(bool((h != 0).any()) for h in before)
+            dones = torch.rand(N, device="cuda", generator=g) < 0.2
+            alg.process_env_step(torch.zeros(N, device="cuda"), dones,
+                                 {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+            after = [h for m in (ac.memory_a, ac.memory_c) for h in m.hidden_states]
+        for b, a in zip(before, after):
+            ref = b.masked_fill(dones.view(1, -1, 1), 0.0)
+            assert torch.equal(a, ref)
+    assert not calls  # the torch reset was not needed

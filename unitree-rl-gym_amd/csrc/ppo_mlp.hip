@@ -2241,18 +2241,30 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
 
 // rewards[i] + gamma * (value[i] * time_out[i]) and dones into the storage row;
 // then the policy-noise draw counter advances (one thread, after k_act)
+// the recurrent memories' states [N, H] zeroed on the done envs (Memory.reset's masked_fill_)
+struct MemReset {
+    float* s[PMLP_MAX_MEM_STATES];
+    int n, H;
+};
+
 __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ rew, const uint8_t* __restrict__ dones,
                                                     const uint8_t* __restrict__ time_outs,
                                                     const float* __restrict__ st_value, float* __restrict__ st_rew,
                                                     uint8_t* __restrict__ st_dones, int N, float gamma,
-                                                    int64_t* draw) {
+                                                    int64_t* draw, MemReset mr) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < N) {
         float r = rew[i];
         if (time_outs) r = r + gamma * (st_value[i] * (time_outs[i] ? 1.f : 0.f));
         st_rew[i] = r;
-        st_dones[i] = dones[i] ? 1 : 0;
+        const bool d = dones[i] != 0;
+        st_dones[i] = d ? 1 : 0;
+        if (d)
+            for (int k = 0; k < mr.n; ++k) {
+                float4* h = (float4*)(mr.s[k] + (size_t)i * mr.H);
+                for (int j = 0; j < mr.H / 4; ++j) h[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
     }
     if (i == 0 && draw) *draw += 1;
 }
@@ -2905,15 +2917,31 @@ PMLP_API int pmlp_permutation(int64_t* out, int64_t n, uint64_t seed, void* stre
     return 0;
 }
 
+PMLP_API int pmlp_store_step_reset(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                                   const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                                   int64_t* draw, int32_t nstates, float* const* states, int32_t H, void* stream) {
+    if (!rewards || !dones || !st_value || !st_rewards || !st_dones || N <= 0)
+        return fail(-1, "pmlp_store_step: null buffer or empty batch");
+    MemReset mr{};
+    if (nstates < 0 || nstates > PMLP_MAX_MEM_STATES || (nstates && (!states || H <= 0 || H % 4)))
+        return fail(-1, "pmlp_store_step_reset: 0..PMLP_MAX_MEM_STATES states of H (a multiple of 4) floats per env");
+    for (int k = 0; k < nstates; ++k) {
+        if (!states[k] || ((uintptr_t)states[k] & 15)) return fail(-1, "pmlp_store_step_reset: null or unaligned state");
+        mr.s[k] = states[k];
+    }
+    mr.n = nstates;
+    mr.H = H;
+    hipLaunchKernelGGL(k_store_step, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
+                       time_outs, st_value, st_rewards, st_dones, N, gamma, draw, mr);
+    PMLP_CHECK_LAUNCH("pmlp_store_step");
+    return 0;
+}
+
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream) {
-    if (!rewards || !dones || !st_value || !st_rewards || !st_dones || N <= 0)
-        return fail(-1, "pmlp_store_step: null buffer or empty batch");
-    hipLaunchKernelGGL(k_store_step, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
-                       time_outs, st_value, st_rewards, st_dones, N, gamma, draw);
-    PMLP_CHECK_LAUNCH("pmlp_store_step");
-    return 0;
+    return pmlp_store_step_reset(rewards, dones, time_outs, st_value, st_rewards, st_dones, N, gamma, draw, 0, nullptr,
+                                 0, stream);
 }
 
 

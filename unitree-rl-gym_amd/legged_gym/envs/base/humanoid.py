@@ -25,16 +25,40 @@ class HumanoidRobot(LeggedRobot):
         self._init_foot()
 
     def _init_foot(self):
-        """h1_env.py:34-46: feet views into the rigid body state tensor."""
+        """h1_env.py:34-46: the feet's rows of the rigid body state tensor."""
         self.feet_num = len(self.feet_indices)
-        self.update_feet_state()
 
     def update_feet_state(self):
-        self.feet_state = self.rigid_body_states_view[:, self.feet_indices, :]
-        self.feet_pos = self.feet_state[:, :, :3]
-        self.feet_vel = self.feet_state[:, :, 7:10]
+        """h1_env.py:48-56 copies the feet rows after every step.  Here feet_state / feet_pos /
+        feet_vel are gathered when read (the rows the step refreshed), so a training loop
+        that never reads them (the rewards using them run in the native step) issues no
+        gather launch per step; the values are the same as the reference's copies."""
 
-    def step(self, actions):
-        out = super().step(actions)
-        self.update_feet_state()
-        return out
+    # (a task subclass that assigns these attributes itself, as the reference's
+    # update_feet_state does, gets its own tensors back)
+    @property
+    def feet_state(self):
+        own = self.__dict__.get("_feet_state")
+        return own if own is not None else self.rigid_body_states_view[:, self.feet_indices, :]
+
+    @feet_state.setter
+    def feet_state(self, v):
+        self.__dict__["_feet_state"] = v
+
+    @property
+    def feet_pos(self):
+        own = self.__dict__.get("_feet_pos")
+        return own if own is not None else self.feet_state[:, :, :3]
+
+    @feet_pos.setter
+    def feet_pos(self, v):
+        self.__dict__["_feet_pos"] = v
+
+    @property
+    def feet_vel(self):
+        own = self.__dict__.get("_feet_vel")
+        return own if own is not None else self.feet_state[:, :, 7:10]
+
+    @feet_vel.setter
+    def feet_vel(self, v):
+        self.__dict__["_feet_vel"] = v

@@ -25,6 +25,7 @@ of the flat moments.  With torch.distributed the gradient (and the statistics
 tail) is all-reduced as one bucket and averaged inside the kernels.
 """
 
+import ctypes as C
 import os
 
 import torch
@@ -587,14 +588,44 @@ class RecurrentRollout:
     def flush(self, storage):
         pass  # nothing is deferred: store() issues its launch at once
 
+    def _reset_states(self):
+        """The memories' (h, c) buffers [1, N, H] that ActorCriticRecurrent.reset(dones) masks,
+        when the store launch can zero them itself (static contiguous fp32 LSTM states of one
+        width), else None."""
+        ac = self.alg.actor_critic
+        out, H = [], None
+        for mem in (ac.memory_a, ac.memory_c):
+            hs = mem.hidden_states
+            if not isinstance(mem.rnn, torch.nn.LSTM) or not isinstance(hs, tuple):
+                return None
+            for h in hs:
+                if not (h.is_cuda and h.dtype == torch.float32 and h.is_contiguous() and h.dim() == 3 and
+                        h.shape[1] == self.N and h.shape[2] % 4 == 0 and (H is None or h.shape[2] == H)):
+                    return None
+                H = h.shape[2]
+                out.append(h)
+        return out, H
+
     def store(self, rewards, dones, time_outs, storage, t, gamma):
         """PPO.process_env_step: pmlp_store_step at once (no forward launch to ride in).
         The launch also advances the policy-noise draw counter pmlp_act read (one thread,
-        after the store), so every step and every iteration samples fresh noise."""
+        after the store), so every step and every iteration samples fresh noise, and zeroes
+        the done envs' memory states (ActorCriticRecurrent.reset(dones), four masked_fill_
+        launches in the reference statement).  Returns True when it did that reset."""
         P = mm._p
-        mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
-                                         P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
-                                         P(self.draw), mm._stream()), "pmlp_store_step")
+        rs = self._reset_states()
+        if rs is None:
+            mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+                                             P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
+                                             P(self.draw), mm._stream()), "pmlp_store_step")
+            return False
+        states, H = rs
+        ptrs = (C.c_void_p * len(states))(*[h.data_ptr() for h in states])
+        mm._ok(mm.load().pmlp_store_step_reset(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+                                               P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
+                                               P(self.draw), len(states), ptrs, H, mm._stream()),
+               "pmlp_store_step_reset")
+        return True
 
 
 def gae(storage, last_values, gamma, lam, world_size=1):

@@ -184,10 +184,11 @@ class PPO:
         time_outs = infos["time_outs"] if "time_outs" in infos else None
         if t is not None and t == self.storage.step and \
                 fused_step.FusedRollout.storable(rewards, dones, time_outs, self.storage.num_envs):
-            self._rollout.store(rewards, dones, time_outs, self.storage, t, self.gamma)
+            reset_done = self._rollout.store(rewards, dones, time_outs, self.storage, t, self.gamma)
             self.storage.step += 1
             self.transition.clear()
-            self.actor_critic.reset(dones)
+            if not reset_done:  # (the recurrent store launch zeroes the done envs' memories itself)
+                self.actor_critic.reset(dones)
             return
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones

@@ -137,6 +137,7 @@ def load():
                                                      i32, vp]
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
+        L.pmlp_store_step_reset.argtypes = [vp] * 6 + [i32, f32, vp, i32, vp, i32, vp]
         L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
         if hasattr(L, "pmlp_mlp_forward_ppo_loss"):  # (absent from builds before round 4's end)
             L.pmlp_mlp_forward_ppo_loss_parts.argtypes = [i32, i32]
