@@ -387,7 +387,8 @@ PMLP_API int pmlp_mlp_forward_ppo_loss(const pmlp_mlp_fwd_job* jobs, int32_t M, 
                                        pmlp_bf16* dmu, pmlp_bf16* dmu_t, int32_t Ap, pmlp_bf16* dvalue,
                                        pmlp_bf16* dvalue_t, int32_t Vp, void* stream);
 /* The same step with fp32 output gradients dmu [M, A] (16-byte aligned when A % 4 == 0) and
- * dvalue [M] (the recurrent heads' fp32 backward, pmlp_heads_backward).                */
+ * dvalue [M] (the recurrent heads' fp32 backward, pmlp_heads_backward).  stats = dstd = NULL:
+ * partials only, pmlp_reduce_slabs_step finishes the loss.                             */
 PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const float* value, const float* actions,
                                     const float* old_logp, const float* old_mu, const float* old_sigma,
                                     const float* adv, const float* ret, const float* target, const int64_t* rows,

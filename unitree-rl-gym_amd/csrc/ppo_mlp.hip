@@ -3020,7 +3020,8 @@ PMLP_API int pmlp_ppo_loss_step_f32(const float* mu, const float* stdv, const fl
     if (int e = loss_args(a, mu, stdv, value, actions, old_logp, old_mu, old_sigma, adv, ret, target, rows, M, A, clip,
                           clipped_value, vcoef, ecoef))
         return e;
-    if (!partial || !stats || !dstd || !dmu || !dvalue) return fail(-1, "pmlp_ppo_loss_step_f32: null output");
+    if (!partial || !dmu || !dvalue || (!stats) != (!dstd))
+        return fail(-1, "pmlp_ppo_loss_step_f32: null output (stats and dstd both set, or both NULL)");
     if (A % 4 == 0 && ((uintptr_t)dmu & 15)) return fail(-1, "pmlp_ppo_loss_step_f32: dmu 16-byte aligned");
     LossStepOut o{partial, nullptr, nullptr, nullptr, nullptr, 0, 0, dmu, dvalue};
     return loss_step_launch(a, o, M, A, 0, partial, stats, dstd, stream);

@@ -22,6 +22,8 @@ gradient a view of another (its 4-float tail: the loss statistics, all-reduced w
 world > 1), Adam's moments flat too -- as FusedPPOStep (fused_step.py).
 """
 
+import ctypes as C
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -130,6 +132,10 @@ class FusedRecurrentStep:
         self.slab = [f(self.nblk, self.nh[n]) for n in range(2)]
         self.loss_partial = f(lib.pmlp_ppo_loss_step_parts(M, self.N1[0]))
         self.opt_partial = f(lib.pmlp_opt_parts())
+        # the loss end (and at world size 1 the grad-norm partials and the step / LR / loss
+        # bookkeeping) ride in the slab-reduce launch (pmlp_reduce_slabs_step), as in the MLP
+        # step: two launches fewer per optimizer step
+        self.norm_partial = f(16384)
         self.mfma = [self.mfma_of(n) for n in range(2)]
         self._head_jobs = (mm.HeadJob * 2)(*[self._head_job(n) for n in range(2)])
         # the memories' weight gradients: accumulated inside the matrix-core backward (one slab
@@ -217,8 +223,7 @@ class FusedRecurrentStep:
                                           P(fl(mu_old)), P(fl(sigma_old)), P(fl(adv)), P(fl(ret)), P(fl(values)), None,
                                           M, A, float(alg.clip_param), int(bool(alg.use_clipped_value_loss)),
                                           float(alg.value_loss_coef), float(alg.entropy_coef), P(self.loss_partial),
-                                          P(self.stats), P(self._gview[id(ac.std)]), P(self.dout[0]),
-                                          P(self.dout[1]), st), "pmlp_ppo_loss_step_f32")
+                                          None, None, P(self.dout[0]), P(self.dout[1]), st), "pmlp_ppo_loss_step_f32")
         # 4. both heads backward: the memories' output gradients + weight-gradient partials
         mm._ok(lib.pmlp_heads_backward(2, self._head_jobs, M, H, st), "pmlp_heads_backward")
         # 5. the memories backward, with their weight gradients (slab partials) on the matrix cores
@@ -239,8 +244,20 @@ class FusedRecurrentStep:
             self._gview[id(r.weight_hh_l0)].copy_(dw[:, I:I + H])
             self._gview[id(r.bias_ih_l0)].copy_(dw[:, I + H])
             self._gview[id(r.bias_hh_l0)].copy_(dw[:, I + H])
-        # every slab (heads, memories) summed into the flat gradient in one launch
-        mm._ok(lib.pmlp_reduce_slabs(len(self._red_jobs), self._red_jobs, st), "pmlp_reduce_slabs")
+        # every slab (heads, memories) summed into the flat gradient in one launch, with the
+        # loss end (the statistics tail, the std gradient) and at world size 1 the grad-norm
+        # partials and the step / LR / loss bookkeeping (k_opt_prepare's work)
+        adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
+        dkl = float(alg.desired_kl if alg.desired_kl is not None else 0.0)
+        # (the memories' gradients go through the reduce only on the matrix-core path: their
+        # squares must be in the partials the clip reads)
+        fold_opt = alg.world_size == 1 and all(self.mfma)
+        rs = mm.ReduceStep(P(self.loss_partial), self.loss_partial.numel() // (3 + A), A, M, float(alg.entropy_coef),
+                           P(ac.std), P(self.stats), P(self._gview[id(ac.std)]),
+                           P(self.norm_partial) if fold_opt else None, P(self.step_t), P(alg._lr), P(acc), dkl,
+                           adaptive, self.norm_partial.numel() if fold_opt else 0)
+        mm._ok(lib.pmlp_reduce_slabs_step(len(self._red_jobs), self._red_jobs, C.byref(rs), st),
+               "pmlp_reduce_slabs_step")
         # 6. data-parallel: one bucket (gradient + loss statistics)
         scale = 1.0
         if alg.world_size > 1:
@@ -250,11 +267,11 @@ class FusedRecurrentStep:
         grp = alg.optimizer.param_groups[0]
         b1, b2 = grp.get("betas", (0.9, 0.999))
         eps = grp.get("eps", 1e-8)
-        adaptive = int(alg.desired_kl is not None and alg.schedule == "adaptive")
-        mm._ok(lib.pmlp_opt_prepare(P(self.grad), self.n, scale, P(self.opt_partial), P(self.step_t), P(self.stats),
-                                    P(alg._lr), P(acc), float(alg.desired_kl if alg.desired_kl is not None else 0.0),
-                                    adaptive, st), "pmlp_opt_prepare")
+        if not fold_opt:  # the norm of the SUMMED gradient, the step count, the LR from the global KL
+            mm._ok(lib.pmlp_opt_prepare(P(self.grad), self.n, scale, P(self.opt_partial), P(self.step_t),
+                                        P(self.stats), P(alg._lr), P(acc), dkl, adaptive, st), "pmlp_opt_prepare")
+        part, nparts = (self.norm_partial, rs.nparts) if fold_opt else (self.opt_partial, self.opt_partial.numel())
         max_norm = float(alg.max_grad_norm) if alg.max_grad_norm is not None else 0.0
-        mm._ok(lib.pmlp_adam(P(self.flat), P(self.grad), P(self.exp_avg), P(self.exp_avg_sq), self.n, scale,
-                             P(self.opt_partial), P(self.step_t), P(alg._lr), max_norm, float(b1), float(b2),
-                             float(eps), st), "pmlp_adam")
+        mm._ok(lib.pmlp_adam_mirror_n(P(self.flat), P(self.grad), P(self.exp_avg), P(self.exp_avg_sq), self.n, scale,
+                                      P(part), nparts, P(self.step_t), P(alg._lr), max_norm, float(b1), float(b2),
+                                      float(eps), 0, None, st), "pmlp_adam_mirror_n")
