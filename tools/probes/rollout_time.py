@@ -1,0 +1,43 @@
+"""Captured Go2 rollout (4096 envs, 24 steps: fused forward + k_step + k_step_extras per step)
+with the libppomlp.so named by PPOMLP_LIB: median time of graph replays, and the rollout
+storage + parameters after two seeded learning iterations digested (sha256) into argv[1] (for a bitwise
+comparison of two builds, tools/gpu_rollout_ab.sh).
+usage: PPOMLP_LIB=... python tools/probes/rollout_time.py out.json"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "unitree-rl-gym_amd"))
+import torch  # noqa: E402
+import isaacgym  # noqa: F401,E402
+from legged_gym.envs import task_registry  # noqa: E402
+from legged_gym.utils import get_args  # noqa: E402
+
+args = get_args(["--task", "go2", "--num_envs", "4096", "--headless"])
+env, _ = task_registry.make_env(name="go2", args=args)
+r, _ = task_registry.make_alg_runner(env=env, name="go2", args=args, log_root=None)
+r.learn(2)  # the second iteration captures the rollout graph
+assert r._rollout_graph is not None
+torch.cuda.synchronize()
+st = r.alg.storage
+out = {k: getattr(st, k).detach().cpu().numpy() for k in ("actions", "actions_log_prob", "values", "mu", "rewards")}
+out.update({f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(r.alg.actor_critic.parameters())})
+with open(sys.argv[1], "w") as f:  # a digest per array (the arrays themselves are ~100 MB per run)
+    json.dump({k: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() for k, v in out.items()}, f)
+ts = []
+with torch.inference_mode(False):
+    for rnd in range(9):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(4):
+            r._rollout_graph.graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 4)
+ts.sort()
+print(f"{os.path.basename(os.environ.get('PPOMLP_LIB', 'libppomlp.so'))}: rollout {ts[len(ts) // 2]:.3f} ms median, "
+      f"{ts[0]:.3f} min", flush=True)
