@@ -67,15 +67,17 @@ def self_launch(args):
 
 
 def setup_dist(args):
+    """This rank's world, rank and device through the package's own launcher hook
+    (legged_gym.utils.distributed.init_from_env, the one train.py uses): RCCL when every rank
+    owns a GPU, gloo when ranks share one; LEGGED_GYM_DIST_BACKEND overrides."""
     import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    return world, rank, local
+    from legged_gym.utils.distributed import init_from_env, rank_device, world_from_env
+    world, rank, local, _ = world_from_env()
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+        world = init_from_env(None)
+    dev = f"cuda:{rank_device(local, torch.cuda.device_count())}"
+    torch.cuda.set_device(dev)
+    return world, rank, dev
 
 
 def barrier(world):
@@ -89,7 +91,9 @@ def max_over_ranks(x, world):
     import torch.distributed as dist
     if world == 1:
         return x
-    t = torch.tensor([x], device="cuda", dtype=torch.float64)
+    # gloo reduces host tensors; RCCL device tensors
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([x], device="cuda" if on_dev else "cpu", dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -392,16 +396,15 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     import torch
-    world, rank, local = setup_dist(args)
+    import isaacgym  # noqa: F401
+    from legged_gym.envs import task_registry  # noqa: F401  (before legged_gym.utils: the registry's import order)
+    world, rank, dev = setup_dist(args)
     if args.gpus != world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    import isaacgym  # noqa: F401
-    from legged_gym.envs import task_registry  # noqa: F401
     from legged_gym.utils import get_args
     from legged_gym.utils.helpers import class_to_dict
     from rsl_rl.runners import OnPolicyRunner
 
-    dev = f"cuda:{local}"
     gargs = get_args(["--task", "go2", "--num_envs", str(args.num_envs), "--headless", "--sim_device", dev,
                       "--rl_device", dev])
     with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line

@@ -325,6 +325,17 @@ LGS_API int lgs_post_physics(lgs_sim* sim, const lgs_env_buffers* env, int64_t s
  * lgs_post_physics == _rewards then _finish (without deferred rewards).                        */
 LGS_API int lgs_post_physics_rewards(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 LGS_API int lgs_post_physics_finish(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* lgs_post_physics_rewards in two parts around a task's Python _post_physics_step_callback
+ * (legged_robot.py:692; the reference's H1Robot / G1Robot override it, h1_env.py:55-65,
+ * g1_env.py:56-105):
+ *  - _prepare: episode length + 1, base-frame state (:681-690 into env->base_lin_vel,
+ *    base_ang_vel, projected_gravity, rpy), the native callback (:488-517: command resampling,
+ *    heading; the humanoid gait phase into env->phase / leg_phase);
+ *  - _term_rewards: check_termination (:711-721) and the native reward terms on what the env
+ *    buffers hold now (commands, phase, leg_phase, base-frame state, episode length).
+ * _prepare then _term_rewards == _rewards, bit for bit, when the caller changes nothing.       */
+LGS_API int lgs_post_physics_prepare(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+LGS_API int lgs_post_physics_term_rewards(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(all) as used by BaseTask.reset (base_task.py:82-86) */
 LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
 /* reset_idx(env_ids) (legged_robot.py:723-768) for an arbitrary subset: env_mask is a DEVICE

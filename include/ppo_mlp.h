@@ -145,6 +145,9 @@ typedef struct pmlp_reduce_step {
                                    -1 when short); out: the partials written           */
 } pmlp_reduce_step;
 PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, pmlp_reduce_step* r, void* stream);
+/* The norm partials pmlp_reduce_slabs_step writes for these jobs (its nparts after the call;
+ * the capacity its norm_partial buffer needs), or -1 for malformed jobs. */
+PMLP_API int64_t pmlp_reduce_slabs_parts(int32_t njobs, const pmlp_reduce_job* jobs);
 
 /* out[r] = sum_c x[r*ld + c], c < cols (bf16 in, fp32 sum): bias gradients. */
 typedef struct {

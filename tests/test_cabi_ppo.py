@@ -121,3 +121,24 @@ def test_recurrent_and_bookkeeping_entries_refuse_bad_arguments(lib):
     lib.pmlp_loss_bookkeeping.restype = C.c_int
     assert lib.pmlp_loss_bookkeeping(None, None, None, C.c_float(0.01), 1, None) != 0
     assert b"pmlp_loss_bookkeeping" in lib.pmlp_last_error()
+
+
+def test_reduce_slabs_parts_sizes_the_norm_partials(lib):
+    """the grad-norm partial buffer of the folded reduce step is sized from its jobs
+    (pmlp_reduce_slabs_parts = the launch's workgroups + the loss-finishing one), and a step
+    whose buffer is smaller is refused before launch."""
+    from rsl_rl.modules import mfma_mlp as mm
+    # one job of 64 floats, 2 slabs: 16 element quads, G = 1 -> 256 quads per block: 1 block
+    job = (mm.ReduceJob * 1)(mm.ReduceJob(16, 16, None, 64, 64, 2, 0, 0))
+    assert lib.pmlp_reduce_slabs_parts(1, job) == 2
+    # 2M floats over 96 slabs (G = 16: 16 quads per block): 500k / 16 blocks, + 1 + 1
+    big = (mm.ReduceJob * 2)(mm.ReduceJob(16, 16, None, 2_000_000, 2_000_000, 96, 0, 0),
+                             mm.ReduceJob(16, 16, None, 64, 64, 2, 0, 0))
+    n = lib.pmlp_reduce_slabs_parts(2, big)
+    assert n == 500_000 // 16 + 1 + 1 and n > 16384  # (the fixed buffer held 16384)
+    assert lib.pmlp_reduce_slabs_parts(0, big) == -1
+    rs = mm.ReduceStep()
+    rs.loss_partial, rs.loss_blocks, rs.A, rs.M, rs.stdv, rs.stats, rs.dstd = 16, 4, 12, 256, 16, 16, 16
+    rs.norm_partial, rs.step, rs.lr, rs.nparts = 16, 16, 16, n - 1
+    assert lib.pmlp_reduce_slabs_step(2, big, C.byref(rs), None) != 0
+    assert b"capacity" in lib.pmlp_last_error()

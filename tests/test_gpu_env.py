@@ -104,13 +104,18 @@ def test_drop_in_semantics():
     assert o2.data_ptr() != o1.data_ptr() and torch.equal(o1, kept)  # previous obs not overwritten
     assert d2.dtype == torch.bool and r2.dtype == torch.float32
     assert "time_outs" in x2 and "episode" in x2
-    # stale extras when no env resets (legged_robot.py:742-743)
+    # stale extras when no env resets (legged_robot.py:742-743): a settled env (zero actions,
+    # episode lengths held at 0, so no time-out and no fall) takes a step without a reset
+    zero = torch.zeros(64, 12, device="cuda")
+    for _ in range(10):
+        env.episode_length_buf = torch.zeros_like(env.episode_length_buf)
+        env.step(zero)
     env.episode_length_buf = torch.zeros_like(env.episode_length_buf)
     env.extras["time_outs"][:] = True
-    prev = env.extras["time_outs"]
-    _, _, _, d3, x3 = env.step(torch.zeros(64, 12, device="cuda"))
-    if not d3.any():
-        assert torch.equal(x3["time_outs"], prev)
+    prev = env.extras["time_outs"].clone()
+    _, _, _, d3, x3 = env.step(zero)
+    assert not d3.any()
+    assert torch.equal(x3["time_outs"], prev)  # carried, not recomputed (all False otherwise)
 
 
 def test_gymapi_style_substep_matches_oracle():

@@ -470,10 +470,13 @@ def test_lstm_rollout_step_mfma_in_place_matches_nn_lstm():
         torch.testing.assert_close(c, c_new, rtol=2e-5, atol=2e-5)
 
 
-def test_recurrent_rollout_draws_fresh_noise_every_step_and_iteration():
+@pytest.mark.parametrize("done_dtype", [torch.bool, torch.int64])
+def test_recurrent_rollout_draws_fresh_noise_every_step_and_iteration(done_dtype):
     """the recurrent rollout's Philox draw counter advances after every
     pmlp_act (in pmlp_store_step), so the standardised noise (a - mu) / sigma differs between
-    consecutive steps and between iterations (storage cleared, same obs)."""
+    consecutive steps and between iterations (storage cleared, same obs).  ADVICE r5: long
+    dones (the reference's reset_buf dtype) take process_env_step's generic branch, which
+    advances the counter itself."""
     torch.manual_seed(4)
     N, T, O, P, A, H = 256, 3, 47, 50, 12, 64
     ac = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
@@ -489,7 +492,7 @@ def test_recurrent_rollout_draws_fresh_noise_every_step_and_iteration():
         for t in range(T):
             with torch.inference_mode():
                 alg.act(obs, cobs)
-                alg.process_env_step(torch.zeros(N, device="cuda"), torch.zeros(N, dtype=torch.bool, device="cuda"),
+                alg.process_env_step(torch.zeros(N, device="cuda"), torch.zeros(N, dtype=done_dtype, device="cuda"),
                                      {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
             zs.append(((st.actions[t] - st.mu[t]) / st.sigma[t]).clone())
         alg.flush_rollout()

@@ -79,36 +79,55 @@ def test_mlp_policy_export(tmp_path):
     torch.testing.assert_close(m(x), ac.actor(x))
 
 
-# --- plugin API: overrides the native step would silently ignore are refused
+# --- plugin API: the reference's per-step hooks run in Python; overrides the
+# native step would silently ignore are refused
 
-def test_task_overriding_a_native_step_method_is_refused():
+def test_task_step_hooks_accepted_native_overrides_refused():
     from legged_gym.envs.base.legged_robot import LeggedRobot
     from legged_gym.envs.h1.h1_env import H1Robot
 
-    class G1Style(H1Robot):  # the reference's G1Robot pattern (g1_env.py:56-141)
+    class G1Style(H1Robot):  # the reference's G1Robot pattern (g1_env.py:10-141)
+        def _get_noise_scale_vec(self, cfg):
+            pass
+
+        def _init_foot(self):
+            pass
+
+        def update_feet_state(self):
+            pass
+
         def compute_observations(self):
             pass
 
         def _post_physics_step_callback(self):
             pass
 
-    with pytest.raises(NotImplementedError, match="compute_observations.*_post_physics_step_callback|"
-                                                  "_post_physics_step_callback.*compute_observations"):
-        G1Style._refuse_native_step_overrides()
-    # refused at construction, before anything touches a device
-    with pytest.raises(NotImplementedError, match="silently ignored"):
-        G1Style(cfg=None, sim_params=None, physics_engine=None, sim_device="cuda:0", headless=True)
+    G1Style._refuse_native_step_overrides()  # accepted
+    assert G1Style.python_step_hooks() == {"compute_observations", "_post_physics_step_callback"}
+    for name in LeggedRobot.PYTHON_STEP_HOOKS:
+        cls = type("Hook_" + name, (LeggedRobot,), {name: lambda self, *a: None})
+        cls._refuse_native_step_overrides()
+        assert cls.python_step_hooks() == {name}
+    # what stays inside the kernel is refused, at construction, before anything touches a device
+    assert set(LeggedRobot.NATIVE_STEP_METHODS) == {"_compute_torques", "_resample_commands", "_push_robots",
+                                                    "compute_reward", "post_physics_step", "_reset_dofs",
+                                                    "_reset_root_states"}
     for name in LeggedRobot.NATIVE_STEP_METHODS:
         cls = type("Override_" + name, (LeggedRobot,), {name: lambda self, *a: None})
         with pytest.raises(NotImplementedError, match=name):
             cls._refuse_native_step_overrides()
+    Torques = type("Torques", (G1Style,), {"_compute_torques": lambda self, a: a})
+    with pytest.raises(NotImplementedError, match="silently ignored"):
+        Torques(cfg=None, sim_params=None, physics_engine=None, sim_device="cuda:0", headless=True)
 
-    class WithPythonTerm(LeggedRobot):  # the supported plugin point
+    class WithPythonTerm(LeggedRobot):  # the reward plugin point
         def _reward_knee_height(self):
             return None
     WithPythonTerm._refuse_native_step_overrides()
-    for t in ("go2", "g1", "h1", "h1_2"):  # the registered tasks themselves pass
+    assert WithPythonTerm.python_step_hooks() == frozenset()
+    for t in ("go2", "g1", "h1", "h1_2"):  # the registered tasks themselves: native, no hooks
         task_registry.get_task_class(t)._refuse_native_step_overrides()
+        assert task_registry.get_task_class(t).python_step_hooks() == frozenset()
 
 
 def test_python_reward_terms_refresh_every_body_row():

@@ -1874,11 +1874,40 @@ __device__ __forceinline__ float reward_term(Smem<D, B, ROWS>& s, const lgs_task
     return r;
 }
 
+// post_physics parts: everything, only up to the rewards (lgs_post_physics_rewards), or
+// the rest from the state the first part left in the env buffers (lgs_post_physics_finish);
+// the rewards part itself in two: the base-frame state and _post_physics_step_callback's
+// commands / gait phase (lgs_post_physics_prepare), then termination and the rewards on
+// what the env buffers hold after a task's Python callback (lgs_post_physics_term_rewards)
+enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2, PART_PREPARE = 3, PART_TERM_REWARDS = 4 };
+
 template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
-                                    const float* rbs, int N, int e, uint32_t step) {
+                                    const float* rbs, int N, int e, uint32_t step, int part) {
     const int lane = hl<EPW>();
-    if (lane == 0) {
+    if (lane == 0 && part == PART_TERM_REWARDS) {
+        // the prepare part's results, as a Python callback may have left them
+        const int64_t ep = E.episode_length[e];
+        int reset = 0;
+        for (int i = 0; i < T.num_termination; ++i) {
+            const float* F = s.cf[T.termination_idx[i]];
+            if (sqrtf(F[0] * F[0] + F[1] * F[1] + F[2] * F[2]) > 1.f) reset = 1;
+        }
+        if (fabsf(E.rpy[3 * e + 1]) > 1.0f || fabsf(E.rpy[3 * e]) > 0.8f) reset = 1;
+        const int timeout = (float)ep > T.max_episode_length;
+        reset |= timeout;
+        for (int i = 0; i < 3; ++i) {
+            s.u.post.misc[i] = E.base_lin_vel[3 * e + i];
+            s.u.post.misc[3 + i] = E.base_ang_vel[3 * e + i];
+            s.u.post.misc[6 + i] = E.projected_gravity[3 * e + i];
+        }
+        s.u.post.misc[9] = E.phase ? E.phase[e] : 0.f;
+        s.u.post.misc[10] = E.leg_phase ? E.leg_phase[2 * e] : 0.f;
+        s.u.post.misc[11] = E.leg_phase ? E.leg_phase[2 * e + 1] : 0.f;
+        for (int i = 0; i < 4; ++i) s.u.post.misc[12 + i] = E.commands[4 * e + i];
+        s.flags[0] = reset;
+        s.flags[1] = timeout;
+    } else if (lane == 0) {
         float* root = s.root;
         float* cmd = E.commands + 4 * e;
         int64_t* ep = E.episode_length + e;
@@ -1947,6 +1976,7 @@ __device__ void post_physics_scalar(Smem<D, B, ROWS>& s, const lgs_task_params& 
         s.flags[0] = reset;
         s.flags[1] = timeout;
     }
+    if (part == PART_PREPARE) return;  // (the base-frame state and commands are in E)
     __syncthreads();
     // rewards: lane k evaluates active term k (alphabetical order, legged_robot.py:770-787)
     if (lane < T.num_rewards) {
@@ -1982,10 +2012,6 @@ __device__ __forceinline__ int num_sums(const lgs_task_params& T) {
 // episode sums into the extras accumulator, reset_buf set, legged_robot.py:723-768)
 enum { RESET_STEP = 0, RESET_ALL = 1, RESET_IDS = 2 };
 
-// post_physics parts: everything, only up to the rewards (lgs_post_physics_rewards), or
-// the rest from the state the first part left in the env buffers (lgs_post_physics_finish)
-enum { PART_ALL = 0, PART_REWARDS = 1, PART_FINISH = 2 };
-
 template <int D, int B, int ROWS, int EPW, bool PAD = false>
 __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, const lgs_env_buffers& E,
                              const float* rbs, int N, int e, uint32_t step, int reset_mode, int part = PART_ALL,
@@ -1998,8 +2024,8 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
     if (force_reset) {
         if (lane == 0) s.flags[0] = 1;
     } else if (part != PART_FINISH) {
-        post_physics_scalar<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step);
-        if (part == PART_REWARDS) return;
+        post_physics_scalar<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step, part);
+        if (part != PART_ALL) return;
     } else if (lane == 0) {  // the first part's results: reset decision, base-frame state, commands
         s.flags[0] = E.reset[e];
         s.flags[1] = E.time_out[e];
@@ -2117,7 +2143,14 @@ __device__ void post_physics(Smem<D, B, ROWS>& s, const lgs_task_params& T, cons
 // (clip, decimation x (PD + substep), torques, body states: lgs_step_physics) and the
 // post-physics stack on the bound state (lgs_post_physics).  STEP == PHYSICS then POST,
 // bit for bit: the post half reads back exactly what the physics half stored.
-enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MODE_POST_FINISH = 4 };
+enum { MODE_STEP = 0, MODE_PHYSICS = 1, MODE_POST = 2, MODE_POST_REWARDS = 3, MODE_POST_FINISH = 4,
+       MODE_POST_PREPARE = 5, MODE_POST_TERM_REWARDS = 6 };
+__host__ __device__ constexpr int mode_part(int mode) {
+    return mode == MODE_POST_REWARDS ? PART_REWARDS
+         : mode == MODE_POST_FINISH ? PART_FINISH
+         : mode == MODE_POST_PREPARE ? PART_PREPARE
+         : mode == MODE_POST_TERM_REWARDS ? PART_TERM_REWARDS : PART_ALL;
+}
 
 // EPW envs per workgroup (one wave): env EPW * xcd_env(block) + hh; with EPW = 2 the grid
 // has N / 2 workgroups (N even) and every wave carries two envs.
@@ -2194,9 +2227,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     __syncthreads();
     STAMP(15);
     if (mode != MODE_PHYSICS)
-        post_physics<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step, RESET_STEP,
-                                      mode == MODE_POST_REWARDS ? PART_REWARDS : (mode == MODE_POST_FINISH ? PART_FINISH : PART_ALL),
-                                      st.vsim, st.pushed);
+        post_physics<D, B, ROWS, EPW, PAD>(s, T, E, rbs, N, e, step, RESET_STEP, mode_part(mode), st.vsim, st.pushed);
     __syncthreads();
     STAMP(16);
     store_state<D, B, ROWS, EPW, PAD>(s, st, md, e);
@@ -2911,7 +2942,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
         LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     }
     HIP_TRY(hipGetLastError());
-    if (mode != MODE_PHYSICS && mode != MODE_POST_REWARDS) {  // extras, episode_acc zeroed, counter advanced
+    if (mode == MODE_STEP || mode == MODE_POST || mode == MODE_POST_FINISH) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
                            (uint32_t)step_counter, (const float*)s->vsim, s->pushed);
         HIP_TRY(hipGetLastError());
@@ -2937,6 +2968,14 @@ LGS_API int lgs_post_physics_rewards(lgs_sim* s, const lgs_env_buffers* env, int
 
 LGS_API int lgs_post_physics_finish(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
     return launch_step(s, env, step_counter, MODE_POST_FINISH, "lgs_post_physics_finish");
+}
+
+LGS_API int lgs_post_physics_prepare(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_POST_PREPARE, "lgs_post_physics_prepare");
+}
+
+LGS_API int lgs_post_physics_term_rewards(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_POST_TERM_REWARDS, "lgs_post_physics_term_rewards");
 }
 
 LGS_API int lgs_reset_all(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {

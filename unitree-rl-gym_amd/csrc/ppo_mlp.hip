@@ -2568,6 +2568,13 @@ PMLP_API int pmlp_reduce_slabs(int32_t njobs, const pmlp_reduce_job* jobs, void*
     return 0;
 }
 
+PMLP_API int64_t pmlp_reduce_slabs_parts(int32_t njobs, const pmlp_reduce_job* jobs) {
+    RedJobs rj;
+    int64_t nb;
+    if (reduce_pack(njobs, jobs, rj, nb)) return -1;
+    return nb + 1;  // every workgroup + the loss-finishing one
+}
+
 PMLP_API int pmlp_reduce_slabs_step(int32_t njobs, const pmlp_reduce_job* jobs, pmlp_reduce_step* r, void* stream) {
     RedJobs rj;
     int64_t nb;

@@ -7,6 +7,8 @@ from leggedsim import cabi
 
 from .legged_robot import LeggedRobot
 
+_OWN_FEET = ("_feet_state", "_feet_pos", "_feet_vel")
+
 
 class HumanoidRobot(LeggedRobot):
     obs_layout = cabi.OBS_HUMANOID
@@ -32,10 +34,22 @@ class HumanoidRobot(LeggedRobot):
         """h1_env.py:48-56 copies the feet rows after every step.  Here feet_state / feet_pos /
         feet_vel are gathered when read (the rows the step refreshed), so a training loop
         that never reads them (the rewards using them run in the native step) issues no
-        gather launch per step; the values are the same as the reference's copies."""
+        gather launch per step; the values are the same as the reference's copies.  Copies a
+        task assigned itself (the reference's _init_foot body) are dropped: the next read
+        gathers the current rows."""
+        for k in _OWN_FEET:
+            self.__dict__.pop(k, None)
+
+    def _refresh_task_views(self):
+        """The reference refreshes the feet copies every step (h1_env.py:56, from the
+        callback): a task holding its own copies (its _init_foot / update_feet_state assign
+        them) gets its update_feet_state called at that point of every step."""
+        d = self.__dict__
+        if "_feet_state" in d or "_feet_pos" in d or "_feet_vel" in d:
+            self.update_feet_state()
 
     # (a task subclass that assigns these attributes itself, as the reference's
-    # update_feet_state does, gets its own tensors back)
+    # _init_foot / update_feet_state do, gets its own tensors back until the next refresh)
     @property
     def feet_state(self):
         own = self.__dict__.get("_feet_state")

@@ -60,6 +60,21 @@ class _GymTensorAPI:
         self._env._sync_stream()
         self._env.sim.forward_kinematics()
 
+    # acquire_*_tensor (legged_robot.py:83-86, h1_env.py:37): the bound state tensors
+    # themselves (gymtorch.wrap_tensor returns its argument), so a task's own _init_foot
+    # written against gym gets views of the live state
+    def acquire_actor_root_state_tensor(self, sim):
+        return self._env.root_states
+
+    def acquire_dof_state_tensor(self, sim):
+        return self._env.dof_state
+
+    def acquire_net_contact_force_tensor(self, sim):
+        return self._env._contact_forces
+
+    def acquire_rigid_body_state_tensor(self, sim):
+        return self._env.rigid_body_states
+
 
 class LeggedRobot(BaseTask):
     obs_layout = cabi.OBS_QUADRUPED
@@ -72,17 +87,26 @@ class LeggedRobot(BaseTask):
     max_contacts = 8
     max_rows = 32
     max_self_contacts = 4  # contact slots self contacts may take per substep (cfg.asset.self_collisions == 0)
-    # The reference's per-step methods that the native step replaces (legged_robot.py:649-671,
-    # 488-555, 557-594, 711-721, 770-811, 188-219).  The kernel never calls a Python method, so a
-    # task subclass overriding one of them (the reference's G1Robot does, g1_env.py:56-141)
-    # would train as if it had not: construction refuses it instead.  Python `_reward_<name>`
-    # terms ARE supported (_prepare_reward_function).
-    NATIVE_STEP_METHODS = ("_compute_torques", "_post_physics_step_callback", "_resample_commands", "_push_robots",
-                           "check_termination", "compute_reward", "compute_observations", "_get_noise_scale_vec",
+    # The reference's per-step methods a task may override in Python, as its H1Robot / G1Robot
+    # do (h1_env.py:55-95, g1_env.py:56-141): the step then takes its split path and calls the
+    # override at the reference's point of post_physics_step (:692, :695, :704), between native
+    # launches (_split_post_physics).  _get_noise_scale_vec may be overridden too: its vector is
+    # the one the kernel's observation noise uses (leggedsim/task.py).
+    PYTHON_STEP_HOOKS = ("_post_physics_step_callback", "check_termination", "compute_observations")
+    # The per-step methods that stay inside the kernel (legged_robot.py:649-671, 519-555,
+    # 557-594, 770-787, 673-709): _compute_torques runs in the substep loop, the rest inside
+    # the reset / push / reward stages of the same launch.  The kernel never calls a Python
+    # method there, so an override would train as if it had not: construction refuses it.
+    # Python `_reward_<name>` terms ARE supported (_prepare_reward_function).
+    NATIVE_STEP_METHODS = ("_compute_torques", "_resample_commands", "_push_robots", "compute_reward",
                            "post_physics_step", "_reset_dofs", "_reset_root_states")
+    # env buffers the kernel reads after _post_physics_step_callback: a callback that rebinds
+    # one (the reference's assigns fresh phase / leg_phase tensors) is copied into it
+    CALLBACK_BUFFERS = ("commands", "phase", "leg_phase", "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy")
 
     def __init__(self, cfg: LeggedRobotCfg, sim_params, physics_engine, sim_device, headless):
         self._refuse_native_step_overrides()
+        self._hooks = self.python_step_hooks()
         self.cfg = cfg
         self.sim_params = sim_params
         self.gym = _GymTensorAPI(self)
@@ -97,21 +121,33 @@ class LeggedRobot(BaseTask):
         self.init_done = True
 
     @classmethod
-    def _refuse_native_step_overrides(cls):
+    def _overridden(cls, names):
+        """(name, owner) of each of `names` a task class defines outside the build's own classes."""
         from .humanoid import HumanoidRobot
         native = (BaseTask, LeggedRobot, HumanoidRobot)
-        bad = []
-        for name in cls.NATIVE_STEP_METHODS:
+        out = []
+        for name in names:
             owner = next((k for k in cls.__mro__ if name in vars(k)), None)
             if owner is not None and owner not in native:
-                bad.append(f"{owner.__module__}.{owner.__qualname__}.{name}")
+                out.append((name, owner))
+        return out
+
+    @classmethod
+    def python_step_hooks(cls):
+        """The PYTHON_STEP_HOOKS this task class overrides (the step's split path calls them)."""
+        return frozenset(name for name, _ in cls._overridden(cls.PYTHON_STEP_HOOKS))
+
+    @classmethod
+    def _refuse_native_step_overrides(cls):
+        bad = [f"{owner.__module__}.{owner.__qualname__}.{name}" for name, owner in cls._overridden(cls.NATIVE_STEP_METHODS)]
         if bad:
             raise NotImplementedError(
                 f"{cls.__name__} overrides {', '.join(bad)}: the native step (one lgs_step launch) computes "
-                "torques, commands, pushes, termination, rewards, resets and observations in a HIP kernel and "
-                "never calls these methods, so the override would be silently ignored.  Supported plugin "
-                "points: cfg values, Python `_reward_<name>` terms (scaled like the reference's), and "
-                "reset_idx(env_ids); see INTEGRATION.md.")
+                "torques, command resampling, pushes, rewards and resets in a HIP kernel and never calls these "
+                "methods, so the override would be silently ignored.  Supported plugin points: cfg values, "
+                "Python `_reward_<name>` terms (scaled like the reference's), overrides of "
+                f"{', '.join(cls.PYTHON_STEP_HOOKS)} and _get_noise_scale_vec, and reset_idx(env_ids); "
+                "see INTEGRATION.md.")
 
     # ------------------------------------------------------------ config ----
     def _parse_cfg(self, cfg):
@@ -315,9 +351,29 @@ class LeggedRobot(BaseTask):
         self._episode_length.copy_(value.to(device=self.device, dtype=torch.long))
 
     def _get_noise_scale_vec(self, cfg):
-        """legged_robot.py:188-219 (quadruped) / h1_env.py:10-31 (humanoid layout)."""
+        """legged_robot.py:188-219 (quadruped) / h1_env.py:10-31 (humanoid layout).  A task's
+        override returns the vector the kernel's observation noise then uses (task params)."""
         self.add_noise = self.cfg.noise.add_noise
         return torch.tensor(self.spec.noise_scale_vec, device=self.device)
+
+    # ------------------------------------------- per-step Python hooks -----
+    # The native step has done each of these when a task override runs (the override's
+    # super() call therefore adds nothing): the split path (_split_post_physics) calls the
+    # override at the reference's point of post_physics_step.
+    def _post_physics_step_callback(self):
+        """legged_robot.py:488-517: command resampling and heading (and the humanoid gait
+        phase, h1_env.py:55-65) are computed by lgs_post_physics_prepare before an override runs."""
+
+    def check_termination(self):
+        """legged_robot.py:711-721: reset_buf / time_out_buf hold the kernel's termination when
+        an override runs; whatever the override leaves in them decides the resets."""
+
+    def compute_observations(self):
+        """legged_robot.py:789-811: obs_buf / privileged_obs_buf hold the kernel's observations
+        (noise added) when an override runs; what it leaves there is clipped and returned."""
+
+    def _refresh_task_views(self):
+        """Per-step refresh of tensors a task derived from the state (HumanoidRobot: feet)."""
 
     def _prepare_reward_function(self):
         """Drop zero scales, multiply the rest by dt; dict order = alphabetical (:817-840).
@@ -346,9 +402,14 @@ class LeggedRobot(BaseTask):
 
     # ------------------------------------------------------ native task -----
     def _build_task(self):
+        nvec = torch.as_tensor(self.noise_scale_vec).reshape(-1)
+        if nvec.numel() != self.num_obs:
+            raise ValueError(f"_get_noise_scale_vec returned {nvec.numel()} entries for {self.num_obs} observations")
         self.task_params = build_task_params(self)
         self.sim.set_task(self.task_params)
         self._env_structs = [self._make_env_struct(i) for i in range(2)]
+        self._bound = {name: getattr(self, name) for name in self.CALLBACK_BUFFERS}
+        self._split_step = bool(self._py_rewards or self._hooks)
 
     def _make_env_struct(self, i):
         E = cabi.EnvBuffers()
@@ -428,14 +489,11 @@ class LeggedRobot(BaseTask):
         # reference's per-reset tensors; inside a captured rollout, one per step)
         snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
         E.ep_snapshot = snap.data_ptr()
-        if self._py_rewards:
-            self.sim.step_physics(E, self._step_mirror)
-            self.sim.post_physics_rewards(E, self._step_mirror)
-            self.reset_buf, self.time_out_buf = self._reset_bufs[i], self._timeout_bufs[i]
-            self._python_rewards()
-            self.sim.post_physics_finish(E, self._step_mirror)
+        if self._split_step:
+            self._split_post_physics(E, i)
         else:
             self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
+            self._refresh_task_views()
         self._step_mirror += 1
         if self.cfg.env.test:
             self._pace_to_real_time()
@@ -447,6 +505,60 @@ class LeggedRobot(BaseTask):
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self._time_outs
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    def _split_post_physics(self, E, i):
+        """step() for a task with Python reward terms or step hooks: the native launches of
+        post_physics_step (legged_robot.py:673-709) with the task's Python code between them, in
+        the reference's order -- physics; base-frame state and the native callback
+        (lgs_post_physics_prepare); the task's _post_physics_step_callback; termination and the
+        native rewards (lgs_post_physics_term_rewards); the task's check_termination; the
+        Python reward terms, only_positive_rewards and the termination term; reset, push,
+        observations and bookkeeping (lgs_post_physics_finish); the task's compute_observations.
+        Without a callback override the first two native parts are one launch
+        (lgs_post_physics_rewards)."""
+        k, hooks = self._step_mirror, self._hooks
+        self.sim.step_physics(E, k)
+        self.reset_buf, self.time_out_buf = self._reset_bufs[i], self._timeout_bufs[i]
+        if "_post_physics_step_callback" in hooks:
+            self.sim.post_physics_prepare(E, k)
+            self._post_physics_step_callback()
+            self._rebind(self.CALLBACK_BUFFERS)
+            self.sim.post_physics_term_rewards(E, k)
+        else:
+            self.sim.post_physics_rewards(E, k)
+            self._refresh_task_views()
+        if "check_termination" in hooks:
+            self.check_termination()
+            # the reference's assigns fresh tensors (torch.any / a comparison): the kernel's
+            # reset and time-out bytes take their values
+            for name, buf in (("reset_buf", self._reset_bufs[i]), ("time_out_buf", self._timeout_bufs[i])):
+                cur = getattr(self, name)
+                if cur is not buf:
+                    buf.copy_(cur.reshape(buf.shape))
+                    setattr(self, name, buf)
+        if self.task_params.defer_reward_total:
+            self._python_rewards()
+        self.sim.post_physics_finish(E, k)
+        if "compute_observations" in hooks:
+            self.obs_buf, self.privileged_obs_buf = self._obs_bufs[i], self._priv_bufs[i]
+            self.compute_observations()
+            clip = self.cfg.normalization.clip_observations  # step()'s clip (legged_robot.py:643-646)
+            for name, buf in (("obs_buf", self._obs_bufs[i]), ("privileged_obs_buf", self._priv_bufs[i])):
+                cur = getattr(self, name)
+                if buf is None:
+                    continue
+                if cur is not buf:
+                    buf.copy_(cur.reshape(buf.shape))
+                buf.clamp_(-clip, clip)
+                setattr(self, name, buf)
+
+    def _rebind(self, names):
+        """A hook that assigned a fresh tensor to a buffer the kernel reads: copy it in."""
+        for name in names:
+            bound, cur = self._bound[name], getattr(self, name)
+            if cur is not bound:
+                bound.copy_(cur.reshape(bound.shape))
+                setattr(self, name, bound)
 
     def _pace_to_real_time(self):
         """cfg.env.test (play.py): simulated time does not run ahead of the wall clock

@@ -67,6 +67,8 @@ def load():
     lib.lgs_reset_idx.argtypes = [vp, C.POINTER(cabi.EnvBuffers), vp, C.c_int64]
     lib.lgs_post_physics_rewards.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_post_physics_finish.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_post_physics_prepare.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    lib.lgs_post_physics_term_rewards.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     lib.lgs_set_self_collision.argtypes = [vp, C.POINTER(cabi.SelfCollisionDesc)]
@@ -90,7 +92,8 @@ def load():
                  "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed",
                  "lgs_set_task", "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_set_heightfield",
                  "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards",
-                 "lgs_post_physics_finish", "lgs_set_self_collision"):
+                 "lgs_post_physics_finish", "lgs_post_physics_prepare", "lgs_post_physics_term_rewards",
+                 "lgs_set_self_collision"):
         getattr(lib, name).restype = C.c_int
     _LIB = lib
     return lib
@@ -107,6 +110,7 @@ EXPORTED_SYMBOLS = [
     "lgs_forward_kinematics", "lgs_set_actor_root_state_indexed", "lgs_set_dof_state_indexed", "lgs_set_task",
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
+    "lgs_post_physics_prepare", "lgs_post_physics_term_rewards",
     "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
     "lgs_get_contact_stats", "lgs_get_instantiation", "lgs_get_factor_chain",
 ]
@@ -183,6 +187,14 @@ class Sim:
     def post_physics_rewards(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_post_physics_rewards(self.handle, C.byref(env_bufs), step_counter),
               "lgs_post_physics_rewards")
+
+    def post_physics_prepare(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_post_physics_prepare(self.handle, C.byref(env_bufs), step_counter),
+              "lgs_post_physics_prepare")
+
+    def post_physics_term_rewards(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        check(self.lib, self.lib.lgs_post_physics_term_rewards(self.handle, C.byref(env_bufs), step_counter),
+              "lgs_post_physics_term_rewards")
 
     def post_physics_finish(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_post_physics_finish(self.handle, C.byref(env_bufs), step_counter),

@@ -85,8 +85,11 @@ def build_task_params(env) -> cabi.TaskParams:
     T.hip_dofs[: len(hip)] = hip
     native = list(getattr(env, "_native_reward_names", env.reward_names))
     py = [n for n, _ in getattr(env, "_py_rewards", [])]
+    hooks = getattr(env, "_hooks", frozenset())
     T.num_rewards = len(native)
-    T.defer_reward_total = int(bool(py))
+    # the reward total (only_positive_rewards, the termination term) is finished in Python when
+    # Python terms add to it or a Python check_termination decides the resets
+    T.defer_reward_total = int(bool(py) or "check_termination" in hooks)
     T.num_extra_sums = len(py)
     for k, n in enumerate(native):
         T.reward_ids[k] = cabi.REWARD_ID[cabi.REWARD_ALIASES.get(n, n)]
@@ -107,14 +110,14 @@ def build_task_params(env) -> cabi.TaskParams:
     T.seed = (seed & 0xFFFFFFFF) | (rank << 32)
     # the rows the step refreshes: the feet (all the reference's humanoid envs read, h1_env.py:34-52)
     # unless the task asks for every body (rigid_body_state_bodies = "all"); by default every
-    # body when the task has Python reward terms, which may read any row
+    # body when the task has Python reward terms or step hooks, which may read any row
     bodies = getattr(env, "rigid_body_state_bodies", None)
     if bodies is None:
-        bodies = "all" if py else "feet"
+        bodies = "all" if (py or hooks) else "feet"
     if bodies not in ("all", "feet"):
         raise ValueError(f"rigid_body_state_bodies must be 'all', 'feet' or None, not {bodies!r}")
     T.write_body_states = int(bool(getattr(env, "uses_rigid_body_states", env.obs_layout == cabi.OBS_HUMANOID)) or
-                              bool(py))
+                              bool(py) or bool(hooks))
     if bodies == "all":
         T.body_state_mask = 0
     else:

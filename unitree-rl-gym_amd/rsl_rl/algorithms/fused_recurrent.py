@@ -132,10 +132,6 @@ class FusedRecurrentStep:
         self.slab = [f(self.nblk, self.nh[n]) for n in range(2)]
         self.loss_partial = f(lib.pmlp_ppo_loss_step_parts(M, self.N1[0]))
         self.opt_partial = f(lib.pmlp_opt_parts())
-        # the loss end (and at world size 1 the grad-norm partials and the step / LR / loss
-        # bookkeeping) ride in the slab-reduce launch (pmlp_reduce_slabs_step), as in the MLP
-        # step: two launches fewer per optimizer step
-        self.norm_partial = f(16384)
         self.mfma = [self.mfma_of(n) for n in range(2)]
         self._head_jobs = (mm.HeadJob * 2)(*[self._head_job(n) for n in range(2)])
         # the memories' weight gradients: accumulated inside the matrix-core backward (one slab
@@ -155,6 +151,14 @@ class FusedRecurrentStep:
                                         mm._p(self.grad) + 4 * self._offset[id(r.bias_hh_l0)], None, self.lrow[n],
                                         4 * H, self.lblk, 0, 0))
         self._red_jobs = (mm.ReduceJob * len(red))(*red)
+        # the loss end (and at world size 1 the grad-norm partials and the step / LR / loss
+        # bookkeeping) ride in the slab-reduce launch (pmlp_reduce_slabs_step), as in the MLP
+        # step: two launches fewer per optimizer step.  One norm partial per workgroup of that
+        # launch: sized from its jobs, so any memory / head width fits
+        nparts = lib.pmlp_reduce_slabs_parts(len(red), self._red_jobs)
+        if nparts <= 0:
+            raise ValueError("fused recurrent step: malformed slab-reduce jobs")
+        self.norm_partial = f(int(nparts))
 
     def mfma_of(self, n):
         return lstm_seq.mfma_usable(self.rnns[n], torch.empty(1, self.rnns[n].input_size)) and \

@@ -190,6 +190,9 @@ class PPO:
             if not reset_done:  # (the recurrent store launch zeroes the done envs' memories itself)
                 self.actor_critic.reset(dones)
             return
+        if t is not None and isinstance(self._rollout, fused_step.RecurrentRollout):
+            # the act sampled with the draw counter the skipped store launch would advance
+            self._rollout.draw += 1
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones
         if "time_outs" in infos:  # bootstrap on time-outs

@@ -110,6 +110,8 @@ def load():
         L.pmlp_gemm_pair.argtypes = [i32, C.POINTER(GemmJob), i32, i32, C.POINTER(GemmJob), vp]
         L.pmlp_reduce_slabs.argtypes = [i32, C.POINTER(ReduceJob), vp]
         L.pmlp_reduce_slabs_step.argtypes = [i32, C.POINTER(ReduceJob), C.POINTER(ReduceStep), vp]
+        L.pmlp_reduce_slabs_parts.argtypes = [i32, C.POINTER(ReduceJob)]
+        L.pmlp_reduce_slabs_parts.restype = C.c_int64
         L.pmlp_permutation.argtypes = [vp, C.c_int64, C.c_uint64, vp]
         L.pmlp_rowsum.argtypes = [i32, C.POINTER(RowsumJob), vp]
         f32 = C.c_float
