@@ -165,6 +165,10 @@ class LeggedRobotCfg(BaseConfig):
             max_gpu_contact_pairs = 2 ** 23
             default_buffer_size_multiplier = 5
             contact_collection = 2
+            # (this build) Gauss-Seidel sweeps of the contact solve per substep; None: the budget
+            # 2 x num_position_iterations + num_velocity_iterations.  A task sets the fewest sweeps
+            # that meet the convergence bar on its own contacts (tools/pgs_sweeps)
+            pgs_sweeps = None
 
 
 class LeggedRobotCfgPPO(BaseConfig):

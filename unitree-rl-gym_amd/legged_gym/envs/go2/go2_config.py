@@ -35,6 +35,14 @@ class GO2RoughCfg(LeggedRobotCfg):
             dof_pos_limits = -10.0
 
 
+    class sim(LeggedRobotCfg.sim):
+        class physx(LeggedRobotCfg.sim.physx):
+            # 5 contact sweeps: the fewest whose solve is within 1 % of the converged one (mean
+            # relative error of its velocity change, kinetic-energy norm) on Go2's contacts, open
+            # and closed loop (profiles/round6/pgs_sweeps: 0.56 % / 0.83 % at 5, 1.24 % closed at 4)
+            pgs_sweeps = 5
+
+
 class GO2RoughCfgPPO(LeggedRobotCfgPPO):
     class algorithm(LeggedRobotCfgPPO.algorithm):
         entropy_coef = 0.01

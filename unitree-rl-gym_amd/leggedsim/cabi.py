@@ -181,9 +181,13 @@ def sim_params_from_cfg(sim_cfg=None, asset_cfg=None, **over):
         p.gravity[:] = tuple(float(x) for x in sim_cfg.gravity)
         px = getattr(sim_cfg, "physx", None)
         if px is not None:
-            # PhysX runs num_position_iterations TGS sweeps; a plain PGS sweep converges
-            # more slowly, so two sweeps are spent per PhysX position iteration.
-            p.solver_iterations = max(1, 2 * int(px.num_position_iterations) + int(px.num_velocity_iterations))
+            # PhysX runs num_position_iterations TGS iterations; the budget here is two plain
+            # Gauss-Seidel sweeps per position iteration.  A task's physx.pgs_sweeps (the fewest
+            # sweeps that meet the convergence bar on its contacts, measured with
+            # tools/pgs_sweeps: DESIGN 3.2) replaces it.
+            sweeps = getattr(px, "pgs_sweeps", None)
+            p.solver_iterations = int(sweeps) if sweeps else \
+                max(1, 2 * int(px.num_position_iterations) + int(px.num_velocity_iterations))
             p.contact_offset = float(px.contact_offset)
             p.rest_offset = float(px.rest_offset)
             p.max_depenetration_velocity = float(px.max_depenetration_velocity)
