@@ -66,6 +66,20 @@ def self_launch(args):
     return subprocess.call(cmd, env=env)
 
 
+@contextlib.contextmanager
+def _stdout_fd_to_stderr():
+    """File descriptor 1 onto 2 for the block: Python prints and native libraries' writes alike."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def setup_dist(args):
     """This rank's world, rank and device through the package's own launcher hook
     (legged_gym.utils.distributed.init_from_env, the one train.py uses): RCCL when every rank
@@ -73,7 +87,7 @@ def setup_dist(args):
     import torch
     from legged_gym.utils.distributed import init_from_env, rank_device, world_from_env
     world, rank, local, _ = world_from_env()
-    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+    with _stdout_fd_to_stderr():  # stdout carries only the JSON line (gloo's C++ connect log too)
         world = init_from_env(None)
     dev = f"cuda:{rank_device(local, torch.cuda.device_count())}"
     torch.cuda.set_device(dev)
@@ -98,9 +112,9 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-# the committed rocprofv3 summaries of the current build (tools/gpu_round5_profile.sh; the
+# the committed rocprofv3 summaries of the current build (tools/gpu_env_profile.sh; the
 # newest round that has them)
-PROFILE_DIR = next((d for d in (os.path.join(ROOT, "profiles", r, "env_go2_4096") for r in ("round5", "round4", "round3"))
+PROFILE_DIR = next((d for d in (os.path.join(ROOT, "profiles", r, "env_go2_4096") for r in ("round6", "round5", "round4", "round3"))
                     if os.path.exists(os.path.join(d, "pmc_k_step.json"))),
                    os.path.join(ROOT, "profiles", "round3", "env_go2_4096"))
 

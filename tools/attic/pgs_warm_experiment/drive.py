@@ -3,7 +3,7 @@ under random PD gaits, every substep also solved with 200 cold sweeps; prints th
 constraint-velocity and impulse error of each sweep / warm-start setting against it."""
 import ctypes as C, sys, os, time
 import numpy as np
-ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..', '..'))
 sys.path[:0] = [os.path.join(ROOT, d) for d in ('unitree-rl-gym_amd', 'tests', 'oracle')]
 from hostspec import make_spec
 from leggedsim import cabi

@@ -4,7 +4,7 @@ existed only in the dropped round-5 warm-start build; on the shipped oracle ever
 import sys, copy
 import numpy as np
 import os
-ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..'))
+ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..', '..'))
 sys.path[:0] = [os.path.join(ROOT, d) for d in ('unitree-rl-gym_amd', 'tests', 'oracle')]
 from hostspec import make_spec, host_buffers
 from leggedsim import cabi

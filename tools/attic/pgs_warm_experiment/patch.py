@@ -5,7 +5,7 @@ substep for the convergence error.  Build: gcc -O3 -march=native -ffp-contract=o
 -std=gnu11 -shared -o libexp.so exp.c -lm; then drive.py / ws2.py / kneel2.py."""
 import os
 import re
-ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+ROOT = os.path.abspath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", ".."))
 HERE = os.path.dirname(os.path.abspath(__file__))
 s = open(os.path.join(ROOT, "oracle", "lgs_oracle.c")).read().replace("\"../include/leggedsim.h\"", "\"" + ROOT + "/include/leggedsim.h\"").replace("\"../unitree-rl-gym_amd/csrc/lgs_detmath.h\"", "\"" + ROOT + "/unitree-rl-gym_amd/csrc/lgs_detmath.h\"")
 s = s.replace('#include "leggedsim.h"', '#include "/root/repo/include/leggedsim.h"') if '#include "leggedsim.h"' in s else s

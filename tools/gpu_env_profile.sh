@@ -1,10 +1,10 @@
-# Round-5 profile set of the fused env step: per config a kernel trace, FETCH_SIZE / WRITE_SIZE
+# Profile set of the fused env step (rounds 5-6): per config a kernel trace, FETCH_SIZE / WRITE_SIZE
 # passes (separate, each with a 1 GiB reference copy), two SQ instruction-mix passes and the
 # per-phase stamps build; for Go2 also the traffic passes of the I/O-only diagnostic build
 # (make -C unitree-rl-gym_amd/csrc iodiag: the step's global loads and stores without the
 # physics), the known-byte calibration of the counters for this access pattern
 # (tools/traffic_calib.py).
-# usage: bash tools/gpu_round5_profile.sh [task:envs ...]
+# usage: [PROF=gpurun_out/prof] bash tools/gpu_env_profile.sh [task:envs ...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -12,7 +12,7 @@ CFGS="${@:-go2:4096 h1:8192 h1_2:8192 g1:4096}"
 B=unitree-rl-gym_amd/csrc/build
 for cfg in $CFGS; do
   task=${cfg%%:*}; n=${cfg##*:}
-  O=gpurun_out/r5prof/${task}_$n
+  O=${PROF:-gpurun_out/prof}/${task}_$n
   rm -rf $O && mkdir -p $O
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python tools/profile_env.py $task $n 60 > $O/trace.log 2>&1 || exit 2
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python tools/profile_env.py $task $n 20 > $O/fetch.log 2>&1 || exit 3

@@ -1,5 +1,5 @@
 """Instruction mix of the env-step kernel from two rocprofv3 SQ counter passes
-(tools/gpu_round5_profile.sh): per-launch instruction counts, per-wave counts per control step,
+(tools/gpu_env_profile.sh): per-launch instruction counts, per-wave counts per control step,
 and the wave-time shares (quad-cycle counters over SQ_WAVE_CYCLES; MI355X_MICROARCH.md
 constants table).  Written to a JSON that bench.py reads for roofline["valu"].
 
