@@ -165,7 +165,27 @@ class FusedPPOStep:
         covered = sum(lin.out_features * (lin.in_features + 1) for ls in self.lins for lin in ls) + A
         self.fold_loss = 2 * L <= mm.MAX_JOBS
         self.fold_opt = self.fold_loss and covered == self.n and all(d is None for ds in self.dw_stage for d in ds)
-        self.norm_partial = torch.empty(16384, device=dev) if self.fold_opt else None
+        # the slab-combine jobs (layer L-1 .. 0, actor then critic: run()'s order) and the
+        # staged weight gradients' copies
+        self.red, self.copies = [], []
+        for l in range(L - 1, -1, -1):
+            for n in range(2):
+                lin = self.lins[n][l]
+                kp = self.k0p[n] if l == 0 else lin.in_features
+                slab = self.slab[l][n]
+                dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
+                self.red.append((slab, dw, lin.out_features * (kp + 8), slab.shape[0], self._gview[id(lin.bias)],
+                                 kp + 8, kp))
+                if self.dw_stage[l][n] is not None:
+                    self.copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
+        # one grad-norm partial per workgroup of the combine launch (sized from its jobs)
+        self.norm_partial = None
+        if self.fold_opt:
+            arr = (mm.ReduceJob * len(self.red))(*[mm._reduce_job(j) for j in self.red])
+            nparts = mm.load().pmlp_reduce_slabs_parts(len(self.red), arr)
+            if nparts <= 0:
+                raise ValueError("fused PPO step: malformed slab-combine jobs")
+            self.norm_partial = torch.empty(int(nparts), device=dev)
         self.nparts = 0
         # the loss in the forward's launch (pmlp_mlp_forward_ppo_loss: 96-row partials, fewer
         # than pmlp_ppo_loss_step's 64-row ones, so loss_partial holds them) where it applies
@@ -278,21 +298,15 @@ class FusedPPOStep:
         #    launch for both (pmlp_gemm_pair) where their tiles pair.  (dW_l beside dX_l on a
         #    second stream measured slower)
         dz = list(self.dz_out)
-        red, copies = [], []
+        red, copies = self.red, self.copies
         for l in range(L - 1, -1, -1):
             gj = []
             for n in range(2):
                 lin = self.lins[n][l]
                 kp = self.k0p[n] if l == 0 else lin.in_features
-                slab = self.slab[l][n]
                 # A = dz [M, out], B = activations [M, kp] (row-major)
                 B = xb[n] if l == 0 else self.y[n][l - 1]
-                gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp, K=M, cf=slab, sum_col=kp))
-                dw = self._gview[id(lin.weight)] if self.dw_stage[l][n] is None else self.dw_stage[l][n]
-                red.append((slab, dw, lin.out_features * (kp + 8), slab.shape[0], self._gview[id(lin.bias)],
-                            kp + 8, kp))
-                if self.dw_stage[l][n] is not None:
-                    copies.append((self._gview[id(lin.weight)], self.dw_stage[l][n][:, :lin.in_features]))
+                gj.append(dict(A=dz[n], B=B, M=lin.out_features, N=kp, K=M, cf=self.slab[l][n], sum_col=kp))
             if l == 0:
                 mm._gemm(mm.EPI_PARTIAL_TN, gj, ksplit=self.ks[l])
             else:
