@@ -27,7 +27,7 @@ hdr = r'''
 #define EXP_KMAX 24
 #define EXP_NM 12
 #define EXP_THREADS 256
-int g_variant = 0;      /* 0 PGS, 1 symmetric PGS, 2 block 3x3, 3 block 3x3 symmetric, 4 PGS stopped at a
+int g_variant = 0;      /* 8 / 9 group sweeps (g_group); 0 PGS, 1 symmetric PGS, 2 block 3x3, 3 block 3x3 symmetric, 4 PGS stopped at a
                            residual, 5 PGS over-relaxed (exp_omega), 7 normals pass then friction pass */
 float g_tol = 1e-3f;    /* variant 4: stop after the sweep whose largest row residual |dlam_r| A_rr is <= g_tol (m/s) */
 void exp_tol(float t) { g_tol = t; }
@@ -51,11 +51,54 @@ void exp_stats(double* out) {
         for (int k = 0; k <= EXP_KMAX; ++k)
             for (int m = 0; m < EXP_NM; ++m) out[k * EXP_NM + m] += g_acc[t][k][m];
 }
+static int g_group = 0;        /* variants 8 / 9: a body's ground contacts as one group per sweep: their normal
+                                  rows (g_group inner passes: 8 solves the group's normal LCP, 9 is one pass,
+                                  i.e. only the order changes), then their friction pairs */
+static const int* g_cbp = NULL; static const int* g_cb2p = NULL; static int g_nc = 0;
+#pragma omp threadprivate(g_group, g_cbp, g_cb2p, g_nc)
+static void exp_sweep_group(int nr, const int* kind, const float* tgt, const float* inv, const float* cmu,
+                            float A[][ROWMAX], float* lam, float* v) {
+    int done[ROWMAX / 3 + 1];
+    for (int c = 0; c < g_nc; ++c) done[c] = 0;
+    for (int r = 0; r < nr; ++r) {
+        if (kind[r] != 0) continue;
+        if (r >= 3 * g_nc) {  /* a limit row */
+            float ln = fmaxf(0.f, lam[r] + (tgt[r] - v[r]) * inv[r]);
+            float d = ln - lam[r]; lam[r] = ln;
+            for (int s2 = 0; s2 < nr; ++s2) v[s2] = fmaf(A[s2][r], d, v[s2]);
+            continue;
+        }
+        const int c = r / 3;
+        if (done[c]) continue;
+        int g[ROWMAX / 3 + 1], k = 0;
+        if (g_cb2p[c] < 0) {
+            for (int c2 = c; c2 < g_nc; ++c2) if (g_cb2p[c2] < 0 && g_cbp[c2] == g_cbp[c]) g[k++] = c2;
+        } else g[k++] = c;
+        for (int it = 0; it < (k > 1 ? g_group : 1); ++it)
+            for (int i = 0; i < k; ++i) {
+                const int rr = 3 * g[i];
+                float ln = fmaxf(0.f, lam[rr] + (tgt[rr] - v[rr]) * inv[rr]);
+                float d = ln - lam[rr]; lam[rr] = ln;
+                for (int s2 = 0; s2 < nr; ++s2) v[s2] = fmaf(A[s2][rr], d, v[s2]);
+            }
+        for (int i = 0; i < k; ++i) {
+            const int rr = 3 * g[i] + 1;
+            float lim = cmu[g[i]] * lam[rr - 1];
+            float l1 = lam[rr] - v[rr] * inv[rr], l2 = lam[rr + 1] - v[rr + 1] * inv[rr + 1];
+            float n2 = l1 * l1 + l2 * l2;
+            if (n2 > lim * lim) { float nrm = sqrtf(n2); float sc = nrm > 0.f ? lim / nrm : 0.f; l1 *= sc; l2 *= sc; }
+            float d1 = l1 - lam[rr], d2 = l2 - lam[rr + 1]; lam[rr] = l1; lam[rr + 1] = l2;
+            for (int s2 = 0; s2 < nr; ++s2) v[s2] = fmaf(A[s2][rr + 1], d2, fmaf(A[s2][rr], d1, v[s2]));
+            done[g[i]] = 1;
+        }
+    }
+}
 static int g_split_pass = 0;  /* variant 7: a sweep visits every normal / limit row, then every friction pair */
 #pragma omp threadprivate(g_split_pass)
 static void exp_sweep(int nr, const int* kind, const float* tgt, const float* inv, const float* cmu,
                       float A[][ROWMAX], float* lam, float* v, int backward, int block, const float (*binv)[9]) {
     float mres = 0.f;
+    if (g_group) { exp_sweep_group(nr, kind, tgt, inv, cmu, A, lam, v); return; }
     if (g_split_pass) {  /* every normal / limit row first, then every friction pair */
         for (int r = 0; r < nr; ++r) if (kind[r] == 0) {
             float ln = fmaxf(0.f, lam[r] + (tgt[r] - v[r]) * inv[r]);
@@ -163,12 +206,15 @@ i1 = s.index("    /* qd' = qf + L^-T (Y lambda) */", i0)
 new_loop = '''    {
         float v0[ROWMAX], lr[ROWMAX], vr[ROWMAX], lkeep[ROWMAX];
         for (int r = 0; r < nr; ++r) { v0[r] = v[r]; lr[r] = 0.f; vr[r] = v[r]; }
+        g_split_pass = 0; g_group = 0;
+        g_cbp = cb; g_cb2p = cb2; g_nc = nc;
         if (g_ref > 0 && nr > 0)  /* the converged reference: plain PGS from zero */
             for (int it = 0; it < g_ref; ++it) exp_sweep(nr, kind, tgt, inv, cmu, A, lr, vr, 0, 0, NULL);
         float binv[ROWMAX / 3 + 1][9];
         const int block = g_variant == 2 || g_variant == 3, sym = g_variant == 1 || g_variant == 3;
         const int adaptive = g_variant == 4;
         g_split_pass = g_variant == 7;
+        g_group = g_variant == 8 ? 30 : g_variant == 9 ? 1 : 0;
         int stopped = 0, used = 0;
         float lstop[ROWMAX], vstop[ROWMAX];
         if (block)

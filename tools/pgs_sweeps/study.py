@@ -33,6 +33,11 @@ METRICS = ["solves", "lam_rel_normal", "lam_rel_friction", "v_err_max", "p_v_err
            "total_normal_rel", "p_energy_rel_gt_5pct", "normal_v_residual_max", "solves_loaded", "sweeps_used",
            "p_at_cap"]
 VARIANTS = {0: "pgs", 1: "pgs_symmetric", 2: "block3", 3: "block3_symmetric"}
+# grouped sweeps (make_exp.py variants 8 / 9): a body's ground contacts' normals solved jointly, or
+# only visited together; selected with VARIANTS_SEL=0,8,9
+EXTRA_VARIANTS = {8: "group_normal_lcp", 9: "group_order"}
+if os.environ.get("VARIANTS_SEL"):
+    VARIANTS = {int(v): {**VARIANTS, **EXTRA_VARIANTS}[int(v)] for v in os.environ["VARIANTS_SEL"].split(",")}
 
 
 def build():
