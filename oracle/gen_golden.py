@@ -376,11 +376,11 @@ def main(out_dir):
     # The recurrent-policy fixtures (tests/golden/lstm_policy_*.npz: the weights and 20-step
     # outputs of deploy/pre_train/*/motion.pt) are not regenerated here.  They were extracted
     # in round 1 with a loader that runs the archive's serialized code; the committed files
-    # hold arrays only and are read with np.load(allow_pickle=False).  Their outputs are
-    # re-derived from their weights with torch's nn.LSTM by tests/test_rsl_rl.py (CPU) and
-    # tests/test_gpu_recurrent.py (the HIP LSTM kernels), so they stay pinned without
-    # executing anything from the archive.
-
+    # hold arrays only and are read with np.load(allow_pickle=False).  They are pinned without
+    # executing anything from the archive: oracle/check_lstm_fixtures.py compares every
+    # parameter, byte for byte, with the archive's raw tensor storages (zip entries), and the
+    # outputs are re-derived from those weights with torch's nn.LSTM by tests/test_rsl_rl.py
+    # (CPU) and tests/test_gpu_recurrent.py (the HIP LSTM kernels).
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "..", "tests", "golden"))
