@@ -185,3 +185,61 @@ def test_task_feet_copies_are_refreshed_every_step():
         if first is None:
             first = env.feet_pos.clone()
     assert not torch.equal(env.feet_pos, first)  # not frozen at the first step's copy
+
+
+class H1HookCounter(H1PyPhase):
+    """H1PyPhase plus a device-side count of the callback's executions (an in-place add,
+    so a captured rollout replays it)."""
+
+    def _post_physics_step_callback(self):
+        if not hasattr(self, "hook_steps"):
+            self.hook_steps = torch.zeros((), dtype=torch.int64, device=self.device)
+        self.hook_steps += 1
+        return super()._post_physics_step_callback()
+
+
+class H1HostSyncHook(H1PyPhase):
+    """A callback the collection graph cannot capture: the reference's resampling idiom,
+    env ids through .nonzero() (legged_robot.py:492-494), reads the device from the host."""
+
+    def _post_physics_step_callback(self):
+        ids = (self.episode_length_buf % 50 == 0).nonzero(as_tuple=False).flatten()
+        self.resample_count = int(ids.numel())
+        return super()._post_physics_step_callback()
+
+
+def _runner(name, cls, rollout_graph=True):
+    env_cfg, train_cfg = task_registry.get_cfgs("h1")
+    env_cfg, train_cfg = copy.deepcopy(env_cfg), copy.deepcopy(train_cfg)
+    train_cfg.runner.rollout_graph = rollout_graph
+    task_registry.register(name, cls, env_cfg, train_cfg)
+    args = get_args(["--task", name, "--num_envs", str(N), "--headless"])
+    env, _ = task_registry.make_env(name=name, args=args)
+    runner, _ = task_registry.make_alg_runner(env=env, name=name, args=args, log_root=None)
+    return env, runner
+
+
+def test_runner_captures_and_replays_the_python_hooks():
+    env, runner = _runner("h1_hook_graph", H1HookCounter)
+    c0, h0 = env.common_step_counter, int(env.hook_steps)
+    runner.learn(3)  # eager, then captured and replayed twice
+    assert runner._rollout_graph is not None
+    torch.cuda.synchronize()
+    assert env.common_step_counter - c0 == 3 * runner.num_steps_per_env
+    assert int(env.hook_steps) - h0 == 3 * runner.num_steps_per_env  # the hook ran inside every replay
+
+
+def test_runner_collects_eagerly_when_a_hook_cannot_be_captured():
+    """The failed capture leaves no trace: the run equals one that never tried (same seeds)."""
+    with pytest.warns(UserWarning, match="collecting eagerly"):
+        env_a, ra = _runner("h1_hostsync_try", H1HostSyncHook)
+        ra.learn(3)
+    assert ra._rollout_graph is None and ra._rollout_graph_failed
+    env_b, rb = _runner("h1_hostsync_eager", H1HostSyncHook, rollout_graph=False)
+    rb.learn(3)
+    torch.cuda.synchronize()
+    assert env_a.common_step_counter == env_b.common_step_counter
+    for pa, pb in zip(ra.alg.actor_critic.parameters(), rb.alg.actor_critic.parameters()):
+        assert torch.equal(pa, pb)
+    for k in ("rewards", "actions", "values", "dones"):
+        assert torch.equal(getattr(ra.alg.storage, k), getattr(rb.alg.storage, k))

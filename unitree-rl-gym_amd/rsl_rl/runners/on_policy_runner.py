@@ -4,6 +4,7 @@ import json
 import os
 import statistics
 import time
+import warnings
 from collections import deque
 
 import torch
@@ -180,8 +181,8 @@ class OnPolicyRunner:
                     graph = self._rollout_graph = None
                 if graph is None and self._eager_rollouts > 0 and self._rollout_graph_ok():
                     # captured after one eager rollout has initialised everything lazily built
-                    graph = self._rollout_graph = _RolloutGraph(self, obs, critic_obs, cur_reward_sum,
-                                                                cur_episode_length)
+                    graph = self._rollout_graph = self._capture_rollout(obs, critic_obs, cur_reward_sum,
+                                                                        cur_episode_length)
                 if graph is not None:
                     fused = getattr(self.alg, "_fused", None)
                     if fused is not None:  # a load() since the capture: the graph reads the bf16 copies
@@ -236,6 +237,29 @@ class OnPolicyRunner:
         self.alg.process_env_step(rewards, dones, infos)
         return obs, critic_obs, rewards, dones, infos
 
+    def _capture_rollout(self, obs, critic_obs, cur_reward_sum, cur_episode_length):
+        """_RolloutGraph, or None when the loop cannot be captured (e.g. a task's Python step
+        hook that synchronises with the host, such as a .nonzero()): nothing inside a failed
+        capture has executed on the device, so the host-side state the captured steps advanced
+        (the env's buffer parity and step counter, the storage index, the rollout's deferred
+        store) is put back as it was and the collection runs eagerly from then on."""
+        objs = [o for o in (self.env, self.alg, self.alg.storage, getattr(self.alg, "_rollout", None))
+                if o is not None]
+        saved = [(o, dict(o.__dict__)) for o in objs]
+        try:
+            return _RolloutGraph(self, obs, critic_obs, cur_reward_sum, cur_episode_length)
+        except RuntimeError as e:
+            for o, d in saved:
+                o.__dict__.clear()
+                o.__dict__.update(d)
+            if hasattr(self.env, "_stream"):
+                # the native sim was pointed at the capture's stream: re-point it at the next step
+                self.env._stream = None
+            torch.cuda.synchronize(self.device)
+            self._rollout_graph_failed = True
+            warnings.warn(f"OnPolicyRunner: capturing the collection loop failed ({e}); collecting eagerly")
+            return None
+
     def _rollout_graph_ok(self):
         """The whole collection loop replays as one HIP graph when nothing in it needs
         the host: a CUDA device, a feed-forward policy or a recurrent one whose memory
@@ -244,6 +268,7 @@ class OnPolicyRunner:
         (LeggedRobot.account_replayed_steps)."""
         ac = self.alg.actor_critic
         return (bool(self.cfg.get("rollout_graph", True)) and str(self.device).startswith("cuda")
+                and not getattr(self, "_rollout_graph_failed", False)
                 and (not ac.is_recurrent or (hasattr(ac, "rollout_capturable") and ac.rollout_capturable()))
                 and hasattr(self.env, "account_replayed_steps") and self.alg.storage is not None)
 
