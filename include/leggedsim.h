@@ -266,6 +266,9 @@ typedef struct lgs_env_buffers {
        receives the clipped copy, legged_robot.py:623-624): the caller's tensor is read
        directly, with no separate copy launch; NULL: the actions are already in `actions`. */
     const float* actions_in;
+    /* optional [num_sums + 1]: the accumulator the NEXT control step adds into, when the caller
+       alternates two episode_acc slots (lgs_step_deferred); the extras zero it with episode_acc */
+    float* episode_acc_next;
 } lgs_env_buffers;
 
 typedef struct lgs_sim lgs_sim;
@@ -343,6 +346,21 @@ LGS_API int lgs_reset_all(lgs_sim* sim, const lgs_env_buffers* env, int64_t step
  * reset byte, and fills the extras like lgs_step (episode means over the reset envs, carried
  * time-outs); the step counter is not advanced. */
 LGS_API int lgs_reset_idx(lgs_sim* sim, const lgs_env_buffers* env, const uint8_t* env_mask, int64_t step_counter);
+
+/* lgs_step with its extras left to the step's consumer: the rollout's next policy launch
+ * (include/ppo_mlp.h, pmlp_env_extras: pmlp_rollout_forward / pmlp_store_step_env), which does
+ * k_step_extras' work on its own rows and once.  Until the consumer (or lgs_step_extras) has run,
+ * env->ep_means / ep_snapshot / time_outs_carry hold the previous step's extras, episode_acc
+ * holds this step's sums, last_root_vel[:, 0:2] every env's push draw, and the step counter is
+ * not advanced.  The consumer zeroes episode_acc_next, not episode_acc (its other workgroups
+ * still read that), so the caller alternates two slots: the next step's episode_acc is this
+ * step's episode_acc_next.  lgs_step == lgs_step_deferred then lgs_step_extras, bit for bit.  */
+LGS_API int lgs_step_deferred(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+LGS_API int lgs_step_extras(lgs_sim* sim, const lgs_env_buffers* env, int64_t step_counter);
+/* the push bookkeeping a deferred step's consumer reads (device pointers owned by the sim):
+ * vsim [N, 2] (the simulated xy base velocity before the all-env push draw) and pushed [3]
+ * (the push flags of the two step-key parities, then the key of the last control step)      */
+LGS_API int lgs_get_push_state(lgs_sim* sim, float** vsim, uint32_t** pushed);
 
 /* gym.add_heightfield -- the rough-terrain ground of legged_gym (utils/terrain.py builds
  * height_field_raw; the reference's create_sim only ever adds the plane, legged_robot.py:240-257).

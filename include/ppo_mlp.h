@@ -261,6 +261,40 @@ PMLP_API int pmlp_act(const float* mu, const float* stdv, const float* value, co
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
                              const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
                              int64_t* draw, void* stream);
+/* The extras of a control step the env left to the rollout (leggedsim lgs_step_deferred,
+ * include/leggedsim.h; the reference's reset_idx extras and push bookkeeping,
+ * legged_robot.py:540-555, 742-768): the work of lgs_step's k_step_extras, done by the launch
+ * that consumes the step (pmlp_rollout_forward's deferred store, pmlp_store_step_env) on its own
+ * env rows and, in its first workgroup, once.  any = acc[nsum] > 0 (some env reset this step);
+ * slot = pushed[2] & 1 (the parity of the step's key):
+ *   per env i: carry[i] = time_out[i] when any, and the store's bootstrap reads that value;
+ *              last_root_vel[i][0:2] = vsim[i] when push and no env was pushed (!pushed[slot]);
+ *   once:      ep_means[k] = ep_snapshot[k] = acc[k] / max(acc[nsum], 1) / ep_len_s when any;
+ *              acc_next[0..nsum] = 0; pushed[slot ^ 1] = 0; *step_counter += 1.
+ * acc is read by every workgroup, so the launch zeroes acc_next (the next step's slot), never acc.
+ * acc == NULL: no extras.                                                                     */
+typedef struct {
+    const float* acc;            /* [nsum + 1] this step's episode sums, then the reset count */
+    float* acc_next;             /* [nsum + 1] the next step's slot                           */
+    int32_t nsum;
+    float ep_len_s;              /* max_episode_length_s                                       */
+    float* ep_means;             /* [nsum] or NULL                                             */
+    float* ep_snapshot;          /* [nsum] or NULL                                             */
+    const uint8_t* time_out;     /* [N] this step's time-outs                                  */
+    uint8_t* carry;              /* [N] extras["time_outs"], or NULL                           */
+    float* last_root_vel;        /* [N, 6] or NULL                                             */
+    const float* vsim;           /* [N, 2]                                                     */
+    uint32_t* pushed;            /* [3] (lgs_get_push_state)                                   */
+    int32_t push;                /* push_robots                                                */
+    int64_t* step_counter;       /* or NULL                                                    */
+} pmlp_env_extras;
+/* pmlp_store_step_reset with a deferred step's extras (ex may be NULL) in the same launch; the
+ * bootstrap reads the carried time-outs after the launch's own update of them (time_outs is
+ * then ex->carry). */
+PMLP_API int pmlp_store_step_env(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                                 const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                                 int64_t* draw, int32_t nstates, float* const* states, int32_t H,
+                                 const pmlp_env_extras* ex, void* stream);
 /* pmlp_store_step plus ActorCriticRecurrent.reset(dones) (each memory's Memory.reset:
  * hidden_state.masked_fill_(dones, 0)) in the same launch: the nstates (<= PMLP_MAX_MEM_STATES)
  * state buffers [N, H] (H a multiple of 4, 16-byte aligned) get zero rows for the done envs. */
@@ -312,8 +346,9 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
  *    advances the same counter);
  *  - optionally the PREVIOUS env step's PPO.process_env_step (pmlp_store_step without the
  *    draw advance), deferred into this launch: st_rewards = rewards + gamma * (prev_value *
- *    time_outs), st_dones = dones (rewards == NULL: none).  The caller issues the last step's
- *    with pmlp_store_step (draw = NULL) before anything reads the storage.
+ *    time_outs), st_dones = dones (rewards == NULL: none), with that step's deferred env extras
+ *    (pmlp_env_extras) when the env left them.  The caller issues the last step's with
+ *    pmlp_store_step_env (draw = NULL) before anything reads the storage.
  * One launch per env step instead of three (forward, pmlp_act, pmlp_store_step).          */
 typedef struct {
     const float* stdv;                  /* [A]                                              */
@@ -331,6 +366,8 @@ typedef struct {
     float* st_rewards;
     uint8_t* st_dones;
     float gamma;
+    pmlp_env_extras extras;             /* the previous step's deferred extras (acc NULL: none);
+                                           they ride with its deferred store (rewards != NULL) */
 } pmlp_rollout_step;
 PMLP_API int pmlp_rollout_forward(const pmlp_mlp_fwd_job* jobs, int32_t N, const pmlp_rollout_step* rs,
                                   void* stream);

@@ -53,7 +53,7 @@ def snapshot(env):
         "last_contacts": t(env.last_contacts).astype(np.uint8), "episode_length": t(env._episode_length),
         "obs": t(env._obs_bufs[i]), "priv_obs": t(env._priv_bufs[i]), "rew": t(env.rew_buf),
         "reset": t(env._reset_bufs[i]).astype(np.uint8), "time_out": t(env._timeout_bufs[i]).astype(np.uint8),
-        "episode_sums": t(env._episode_sums), "episode_acc": np.zeros_like(t(env._episode_acc)),
+        "episode_sums": t(env._episode_sums), "episode_acc": np.zeros_like(t(env._episode_acc[0])),
         "base_lin_vel": t(env.base_lin_vel), "base_ang_vel": t(env.base_ang_vel),
         "projected_gravity": t(env.projected_gravity), "rpy": t(env.rpy), "env_origins": t(env.env_origins),
         "phase": t(env.phase), "leg_phase": t(env.leg_phase),

@@ -179,7 +179,8 @@ struct DevState {
     const float* added_mass;  // [N]
     const float* torques_in;  // [N,D] (lgs_simulate)
     float* vsim;              // [N,2] the step's base xy velocity before the all-env push draw (k_step_extras)
-    unsigned* pushed;         // [2] "some env was pushed" per step parity (k_step sets, k_step_extras reads)
+    unsigned* pushed;         // [3] "some env was pushed" per step parity (k_step sets, k_step_extras reads),
+                              // then the step key of the last control step (a deferred step's consumer)
 };
 
 __device__ __forceinline__ float rl(float x, int l) {
@@ -2162,10 +2163,13 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? 
     STAMP_BEGIN();
     __shared__ Smem<D, B, ROWS> sm[EPW];
     __shared__ ModelCache<D, B> mc;
+    if (E.step_counter) step = (uint32_t)*E.step_counter;
+    // the step key whose parity indexes this step's push flag, for a deferred step's consumer
+    // (lgs_step_deferred: the consumer advances the counter, so it cannot read the key there)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && st.pushed && mode != MODE_PHYSICS) st.pushed[2] = step;
     const int e = EPW * xcd_env(blockIdx.x, gridDim.x) + hh<EPW>();
     if (EPW * xcd_env(blockIdx.x, gridDim.x) >= N) return;  // (EPW = 2: N is even, both envs exist)
     Smem<D, B, ROWS>& s = sm[hh<EPW>()];
-    if (E.step_counter) step = (uint32_t)*E.step_counter;
     const lgs_task_params& T = *Tp;
     const int lane = hl<EPW>();
     load_model(mc, md);
@@ -2303,6 +2307,7 @@ __global__ __launch_bounds__(1024) void k_step_extras(lgs_env_buffers E, const l
         for (int e = t; e < N; e += blockDim.x) E.time_outs_carry[e] = E.time_out[e];
     __syncthreads();
     if (t <= nsum) E.episode_acc[t] = 0.f;
+    if (E.episode_acc_next && t <= nsum) E.episode_acc_next[t] = 0.f;  // (a deferred consumer's)
     if (t == 0 && advance) pushed_flag[(step + 1u) & 1u] = 0u;  // the next step's flag
     if (t == 0 && E.step_counter && advance) *E.step_counter += 1;
 }
@@ -2327,7 +2332,7 @@ struct lgs_sim {
     float* friction = nullptr;
     float* added_mass = nullptr;
     float* vsim = nullptr;  // [N,2] scratch of the all-env push bookkeeping (DevState::vsim)
-    unsigned* pushed = nullptr;  // [2] the push flags (DevState::pushed)
+    unsigned* pushed = nullptr;  // [3] the push flags and the last step key (DevState::pushed)
     unsigned long long* stats = nullptr;  // [8][LGS_NUM_CONTACT_STATS] capacity-drop counters (DevState::stats)
     float* root = nullptr;
     float* dofs = nullptr;
@@ -2714,8 +2719,8 @@ LGS_API int lgs_create_sim(const lgs_model_desc* m, const lgs_sim_params* p, int
     HIP_TRY(hipMalloc(&s->friction, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->added_mass, sizeof(float) * num_envs));
     HIP_TRY(hipMalloc(&s->vsim, sizeof(float) * 2 * num_envs));
-    HIP_TRY(hipMalloc(&s->pushed, sizeof(unsigned) * 2));
-    HIP_TRY(hipMemset(s->pushed, 0, sizeof(unsigned) * 2));
+    HIP_TRY(hipMalloc(&s->pushed, sizeof(unsigned) * 3));
+    HIP_TRY(hipMemset(s->pushed, 0, sizeof(unsigned) * 3));
     HIP_TRY(hipMalloc(&s->stats, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
     HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * 8 * LGS_NUM_CONTACT_STATS));
     s->sp.stats = s->stats;
@@ -2931,7 +2936,8 @@ LGS_API int lgs_set_task(lgs_sim* s, const lgs_task_params* t) {
     return LGS_OK;
 }
 
-static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter, int mode, const char* what) {
+static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter, int mode, const char* what,
+                       bool extras = true) {
     if (!s || !env) return set_err(LGS_ERR_ARG, std::string(what) + ": null argument");
     if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, std::string(what) + ": state not bound or task not set");
     DevState st = state_of(s);
@@ -2942,7 +2948,7 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
         LGS_DISPATCH_STEP(s, k_step, s->md, s->sp, st, s->task_dev, *env, s->N, (uint32_t)step_counter, mode);
     }
     HIP_TRY(hipGetLastError());
-    if (mode == MODE_STEP || mode == MODE_POST || mode == MODE_POST_FINISH) {  // extras, episode_acc zeroed, counter advanced
+    if (extras && (mode == MODE_STEP || mode == MODE_POST || mode == MODE_POST_FINISH)) {  // extras, episode_acc zeroed, counter advanced
         hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
                            (uint32_t)step_counter, (const float*)s->vsim, s->pushed);
         HIP_TRY(hipGetLastError());
@@ -2952,6 +2958,26 @@ static int launch_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_coun
 
 LGS_API int lgs_step(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
     return launch_step(s, env, step_counter, MODE_STEP, "lgs_step");
+}
+
+LGS_API int lgs_step_deferred(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    return launch_step(s, env, step_counter, MODE_STEP, "lgs_step_deferred", false);
+}
+
+LGS_API int lgs_step_extras(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {
+    if (!s || !env) return set_err(LGS_ERR_ARG, "lgs_step_extras: null argument");
+    if (!s->root || !s->has_task) return set_err(LGS_ERR_STATE, "lgs_step_extras: state not bound or task not set");
+    hipLaunchKernelGGL(k_step_extras, dim3(1), dim3(1024), 0, s->stream, *env, s->task_dev, s->N, 1,
+                       (uint32_t)step_counter, (const float*)s->vsim, s->pushed);
+    HIP_TRY(hipGetLastError());
+    return LGS_OK;
+}
+
+LGS_API int lgs_get_push_state(lgs_sim* s, float** vsim, uint32_t** pushed) {
+    if (!s || !vsim || !pushed) return set_err(LGS_ERR_ARG, "lgs_get_push_state: null argument");
+    *vsim = s->vsim;
+    *pushed = s->pushed;
+    return LGS_OK;
 }
 
 LGS_API int lgs_step_physics(lgs_sim* s, const lgs_env_buffers* env, int64_t step_counter) {

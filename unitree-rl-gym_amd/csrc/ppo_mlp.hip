@@ -1896,7 +1896,45 @@ struct RollStep {
     float* st_rew;
     uint8_t* st_dones;
     float gamma;
+    pmlp_env_extras ex;  // the previous step's deferred env extras (ex.acc == NULL: none)
 };
+
+// A deferred env step's extras (include/ppo_mlp.h pmlp_env_extras; leggedsim's k_step_extras,
+// whose arithmetic this repeats): per env row, and once in the launch's first workgroup.
+__device__ __forceinline__ bool ex_any(const pmlp_env_extras& x) { return x.acc[x.nsum] > 0.f; }
+// row i: the carried time-out byte the bootstrap reads (this step's when any env reset: the
+// carry is updated first), and the push bookkeeping of the step's all-env draw
+__device__ __forceinline__ bool ex_row(const pmlp_env_extras& x, bool any, int i, const uint8_t* time_outs) {
+    bool to = false;
+    if (x.carry && any) {
+        const uint8_t b = x.time_out[i];
+        x.carry[i] = b;
+        to = b != 0;
+    } else if (time_outs) {
+        to = time_outs[i] != 0;
+    }
+    if (x.push && x.last_root_vel && !x.pushed[x.pushed[2] & 1u]) {  // no env pushed: the simulated velocities
+        x.last_root_vel[6 * (size_t)i] = x.vsim[2 * (size_t)i];
+        x.last_root_vel[6 * (size_t)i + 1] = x.vsim[2 * (size_t)i + 1];
+    }
+    return to;
+}
+// once (threads t of one workgroup, t <= nsum < 64 covered): the episode means, the next step's
+// accumulator, the next parity's push flag, the step counter
+__device__ __forceinline__ void ex_once(const pmlp_env_extras& x, bool any, int t) {
+#pragma clang fp contract(off)
+    if (x.ep_means && t < x.nsum) {
+        float m = x.ep_means[t];
+        if (any) m = x.acc[t] / fmaxf(x.acc[x.nsum], 1.f) / x.ep_len_s;
+        x.ep_means[t] = m;
+        if (x.ep_snapshot) x.ep_snapshot[t] = m;
+    }
+    if (t <= x.nsum) x.acc_next[t] = 0.f;
+    if (t == 0) {
+        x.pushed[(x.pushed[2] + 1u) & 1u] = 0u;
+        if (x.step_counter) *x.step_counter += 1;
+    }
+}
 
 // The rollout's work on the workgroup's R rows after job jj's forward (its outputs are in
 // J.out, written by this workgroup before the barrier that precedes this call).  Job 0 (the
@@ -1934,18 +1972,22 @@ __device__ void roll_epilogue(const FmlpJob& J, int jj, const RollStep& rs, int 
             }
         }
         __syncthreads();
+        const bool ex = rs.rew && rs.ex.acc;
+        const bool any = ex && ex_any(rs.ex);
         if (tid < R && r0 + tid < M) {
             const int i = r0 + tid;
             float logp = 0.f;
             for (int k = 0; k < rs.A; ++k) logp += terms[tid * 16 + k];
             rs.st_logp[i] = logp;
             if (rs.rew) {  // the previous step's process_env_step (k_store_step's arithmetic)
+                const bool to = ex ? ex_row(rs.ex, any, i, rs.time_outs) : (rs.time_outs && rs.time_outs[i]);
                 float rw = rs.rew[i];
-                if (rs.time_outs) rw = rw + rs.gamma * (rs.prev_value[i] * (rs.time_outs[i] ? 1.f : 0.f));
+                if (rs.time_outs) rw = rw + rs.gamma * (rs.prev_value[i] * (to ? 1.f : 0.f));
                 rs.st_rew[i] = rw;
                 rs.st_dones[i] = rs.dones[i] ? 1 : 0;
             }
         }
+        if (ex && blockIdx.x == 0) ex_once(rs.ex, any, tid);
         const int nrow = min(R, M - r0);
         for (int q = tid; q < nrow * rs.O; q += FMLP_THREADS)
             rs.st_obs[(size_t)r0 * rs.O + q] = rs.obs[(size_t)r0 * rs.O + q];
@@ -2247,16 +2289,20 @@ struct MemReset {
     int n, H;
 };
 
+// a deferred env step's extras (ex.acc != NULL) on the same rows, and once in block 0
 __global__ __launch_bounds__(256) void k_store_step(const float* __restrict__ rew, const uint8_t* __restrict__ dones,
-                                                    const uint8_t* __restrict__ time_outs,
+                                                    const uint8_t* time_outs,
                                                     const float* __restrict__ st_value, float* __restrict__ st_rew,
                                                     uint8_t* __restrict__ st_dones, int N, float gamma,
-                                                    int64_t* draw, MemReset mr) {
+                                                    int64_t* draw, MemReset mr, pmlp_env_extras ex) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool any = ex.acc && ex_any(ex);
+    if (ex.acc && blockIdx.x == 0) ex_once(ex, any, threadIdx.x);
     if (i < N) {
+        const bool to = ex.acc ? ex_row(ex, any, i, time_outs) : (time_outs && time_outs[i]);
         float r = rew[i];
-        if (time_outs) r = r + gamma * (st_value[i] * (time_outs[i] ? 1.f : 0.f));
+        if (time_outs) r = r + gamma * (st_value[i] * (to ? 1.f : 0.f));
         st_rew[i] = r;
         const bool d = dones[i] != 0;
         st_dones[i] = d ? 1 : 0;
@@ -2842,11 +2888,18 @@ PMLP_API int pmlp_mlp_forward(int32_t njobs, const pmlp_mlp_fwd_job* jobs, int32
     return 0;
 }
 
+// a deferred env step's extras are complete (acc == NULL: none)
+static bool env_extras_ok(const pmlp_env_extras& x) {
+    return !x.acc || (x.acc_next && x.nsum >= 0 && x.nsum < 64 && x.ep_len_s > 0.f && x.time_out && x.pushed &&
+                      (!x.push || !x.last_root_vel || x.vsim));
+}
+
 PMLP_API int pmlp_rollout_forward(const pmlp_mlp_fwd_job* jobs, int32_t N, const pmlp_rollout_step* r, void* stream) {
     if (!r || !r->stdv || !r->obs || r->O <= 0 || r->A <= 0 || r->A > 16 || (r->cobs && r->CO <= 0) || !r->draw ||
         (r->parity & ~1) || !r->actions_out || !r->st_actions || !r->st_logp || !r->st_mu || !r->st_sigma ||
         !r->st_value || !r->st_obs || (r->cobs && !r->st_cobs) ||
-        (r->rewards && (!r->dones || !r->prev_value || !r->st_rewards || !r->st_dones)))
+        (r->rewards && (!r->dones || !r->prev_value || !r->st_rewards || !r->st_dones)) ||
+        (r->extras.acc && (!r->rewards || !env_extras_ok(r->extras))))
         return fail(-1, "pmlp_rollout_forward: bad rollout step arguments");
     if (!jobs || N <= 0 || jobs[0].N[3] != r->A || jobs[1].N[3] != 1)
         return fail(-1, "pmlp_rollout_forward: job 0 = actor [N, A], job 1 = critic [N, 1]");
@@ -2855,7 +2908,8 @@ PMLP_API int pmlp_rollout_forward(const pmlp_mlp_fwd_job* jobs, int32_t N, const
     if (int e = fmlp_pack(2, jobs, N, fj)) return e;
     const RollStep rs{r->stdv, r->obs, r->cobs, r->O, r->CO, r->A, r->actions_out, r->st_actions, r->st_logp,
                       r->st_mu, r->st_sigma, r->st_value, r->st_obs, r->st_cobs, r->draw, r->parity, r->seed,
-                      r->rewards, r->dones, r->time_outs, r->prev_value, r->st_rewards, r->st_dones, r->gamma};
+                      r->rewards, r->dones, r->time_outs, r->prev_value, r->st_rewards, r->st_dones, r->gamma,
+                      r->extras};
     hipLaunchKernelGGL((k_mlp_fwd<32, true>), dim3((N + 31) / 32, 2), dim3(FMLP_THREADS), 0, (hipStream_t)stream,
                        fj, N, rs);
     PMLP_CHECK_LAUNCH("pmlp_rollout_forward");
@@ -2924,11 +2978,14 @@ PMLP_API int pmlp_permutation(int64_t* out, int64_t n, uint64_t seed, void* stre
     return 0;
 }
 
-PMLP_API int pmlp_store_step_reset(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
-                                   const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
-                                   int64_t* draw, int32_t nstates, float* const* states, int32_t H, void* stream) {
+PMLP_API int pmlp_store_step_env(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                                 const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                                 int64_t* draw, int32_t nstates, float* const* states, int32_t H,
+                                 const pmlp_env_extras* ex, void* stream) {
     if (!rewards || !dones || !st_value || !st_rewards || !st_dones || N <= 0)
         return fail(-1, "pmlp_store_step: null buffer or empty batch");
+    const pmlp_env_extras none{};
+    if (ex && !env_extras_ok(*ex)) return fail(-1, "pmlp_store_step_env: bad env extras");
     MemReset mr{};
     if (nstates < 0 || nstates > PMLP_MAX_MEM_STATES || (nstates && (!states || H <= 0 || H % 4)))
         return fail(-1, "pmlp_store_step_reset: 0..PMLP_MAX_MEM_STATES states of H (a multiple of 4) floats per env");
@@ -2939,9 +2996,16 @@ PMLP_API int pmlp_store_step_reset(const float* rewards, const uint8_t* dones, c
     mr.n = nstates;
     mr.H = H;
     hipLaunchKernelGGL(k_store_step, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones,
-                       time_outs, st_value, st_rewards, st_dones, N, gamma, draw, mr);
+                       time_outs, st_value, st_rewards, st_dones, N, gamma, draw, mr, ex ? *ex : none);
     PMLP_CHECK_LAUNCH("pmlp_store_step");
     return 0;
+}
+
+PMLP_API int pmlp_store_step_reset(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,
+                                   const float* st_value, float* st_rewards, uint8_t* st_dones, int32_t N, float gamma,
+                                   int64_t* draw, int32_t nstates, float* const* states, int32_t H, void* stream) {
+    return pmlp_store_step_env(rewards, dones, time_outs, st_value, st_rewards, st_dones, N, gamma, draw, nstates,
+                               states, H, nullptr, stream);
 }
 
 PMLP_API int pmlp_store_step(const float* rewards, const uint8_t* dones, const uint8_t* time_outs,

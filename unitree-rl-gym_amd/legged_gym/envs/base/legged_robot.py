@@ -76,6 +76,34 @@ class _GymTensorAPI:
         return self._env.rigid_body_states
 
 
+class _DeferredExtras:
+    """The extras of a control step issued by lgs_step_deferred, left to the step's consumer
+    (include/leggedsim.h).  `fields` are include/ppo_mlp.h pmlp_env_extras' values, for the
+    rollout's next policy launch to do the work in; run() issues lgs_step_extras instead.
+    Whoever issues the work sets `consumed` (a host flag: a captured rollout replays the
+    consumer's launch on the device without it)."""
+
+    def __init__(self, env, E, k):
+        self.env, self.k = env, k
+        self.E = cabi.EnvBuffers.from_buffer_copy(E)  # this step's pointers (the struct is reused two steps on)
+        if getattr(env, "_push_state", None) is None:
+            env._push_state = env.sim.push_state()
+        vsim, pushed = env._push_state
+        tp = env.task_params
+        self.fields = dict(acc=E.episode_acc, acc_next=E.episode_acc_next,
+                           nsum=tp.num_rewards + (1 if tp.has_termination_reward else 0) + tp.num_extra_sums,
+                           ep_len_s=float(tp.max_episode_length_s), ep_means=E.ep_means, ep_snapshot=E.ep_snapshot,
+                           time_out=E.time_out, carry=E.time_outs_carry, last_root_vel=E.last_root_vel, vsim=vsim,
+                           pushed=pushed, push=int(bool(tp.push_robots)), step_counter=E.step_counter)
+        self.consumed = False
+
+    def run(self):
+        """The work on its own launch (what lgs_step issues after the step)."""
+        if not self.consumed:
+            self.consumed = True
+            self.env.sim.step_extras(self.E, self.k)
+
+
 class LeggedRobot(BaseTask):
     obs_layout = cabi.OBS_QUADRUPED
     # rigid_body_states rows each step refreshes: "feet" (all the reference's humanoid envs
@@ -293,6 +321,8 @@ class LeggedRobot(BaseTask):
         self.sim.bind(self.root_states, self.dof_state, self._contact_forces, self.rigid_body_states)
         self._stream = None
         self._sync_stream()
+        self.defer_extras = False  # OnPolicyRunner sets it around its collection loop (step())
+        self._deferred = None
 
         self.common_step_counter = 0
         self.extras = {}
@@ -396,7 +426,9 @@ class LeggedRobot(BaseTask):
         nsum = len(self._sum_names)
         self._episode_sums = torch.zeros(nsum, self.num_envs, dtype=torch.float, device=self.device)
         self.episode_sums = {name: self._episode_sums[i] for i, name in enumerate(self._sum_names)}
-        self._episode_acc = torch.zeros(nsum + 1, dtype=torch.float, device=self.device)
+        # two accumulator slots, one per env-buffer parity: a deferred step's consumer zeroes the
+        # next step's slot while its workgroups still read this step's (lgs_step_deferred)
+        self._episode_acc = torch.zeros(2, nsum + 1, dtype=torch.float, device=self.device)
         self._ep_means = torch.zeros(nsum, dtype=torch.float, device=self.device)
         self._time_outs = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
 
@@ -429,7 +461,8 @@ class LeggedRobot(BaseTask):
         E.reset = p(self._reset_bufs[i])
         E.time_out = p(self._timeout_bufs[i])
         E.episode_sums = p(self._episode_sums)
-        E.episode_acc = p(self._episode_acc)
+        E.episode_acc = p(self._episode_acc[i])
+        E.episode_acc_next = p(self._episode_acc[i ^ 1])
         E.base_lin_vel = p(self.base_lin_vel)
         E.base_ang_vel = p(self.base_ang_vel)
         E.projected_gravity = p(self.projected_gravity)
@@ -472,8 +505,15 @@ class LeggedRobot(BaseTask):
     # ------------------------------------------------------------ step ------
     def step(self, actions):
         """Apply actions, simulate `decimation` substeps, post-physics; one launch (three
-        launches and the Python terms when the task defines Python reward terms)."""
+        launches and the Python terms when the task defines Python reward terms).
+
+        With `defer_extras` set (OnPolicyRunner, around its collection loop) the step's extras
+        launch is left to the step's consumer: infos["_deferred_extras"] describes it, and the
+        rollout's next policy launch does that work on its own rows (pmlp_env_extras).  Until
+        then extras["episode"] / extras["time_outs"] are the previous step's; a step nobody
+        consumed is completed at the next step, reset_idx or flush_extras()."""
         self._sync_stream()
+        self.flush_extras()
         self._buf_idx ^= 1
         i = self._buf_idx
         E = self._env_structs[i]
@@ -489,8 +529,13 @@ class LeggedRobot(BaseTask):
         # reference's per-reset tensors; inside a captured rollout, one per step)
         snap = torch.empty(len(self._sum_names), dtype=torch.float, device=self.device)
         E.ep_snapshot = snap.data_ptr()
+        job = None
         if self._split_step:
             self._split_post_physics(E, i)
+        elif self.defer_extras:
+            self.sim.step_deferred(E, self._step_mirror)  # the extras: the consumer's (job)
+            job = self._deferred = _DeferredExtras(self, E, self._step_mirror)
+            self._refresh_task_views()
         else:
             self.sim.step(E, self._step_mirror)  # + extras, episode_acc reset, step counter
             self._refresh_task_views()
@@ -504,7 +549,17 @@ class LeggedRobot(BaseTask):
         self.extras["episode"] = {"rew_" + k: snap[j] for j, k in enumerate(self._sum_names)}
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self._time_outs
+        if job is not None:
+            self.extras["_deferred_extras"] = job
+        else:
+            self.extras.pop("_deferred_extras", None)
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    def flush_extras(self):
+        """Complete a deferred step's extras that no consumer has taken (lgs_step_extras)."""
+        job, self._deferred = self._deferred, None
+        if job is not None:
+            job.run()
 
     def _split_post_physics(self, E, i):
         """step() for a task with Python reward terms or step hooks: the native launches of
@@ -597,6 +652,7 @@ class LeggedRobot(BaseTask):
         if len(env_ids) == 0:
             return
         self._sync_stream()
+        self.flush_extras()
         ids = torch.as_tensor(env_ids, device=self.device).long().view(-1)
         mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         mask[ids] = 1

@@ -124,7 +124,8 @@ class EnvBuffers(C.Structure):
         "actions", "last_actions", "last_dof_vel", "last_root_vel", "torques", "commands", "feet_air_time",
         "last_contacts", "episode_length", "obs", "priv_obs", "rew", "reset", "time_out", "episode_sums",
         "episode_acc", "base_lin_vel", "base_ang_vel", "projected_gravity", "rpy", "env_origins", "phase",
-        "leg_phase", "rew_terms", "step_counter", "ep_means", "ep_snapshot", "time_outs_carry", "actions_in")]
+        "leg_phase", "rew_terms", "step_counter", "ep_means", "ep_snapshot", "time_outs_carry", "actions_in",
+        "episode_acc_next")]
 
 
 class ModelHandle:

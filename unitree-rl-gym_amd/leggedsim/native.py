@@ -69,6 +69,12 @@ def load():
     lib.lgs_post_physics_finish.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_post_physics_prepare.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
     lib.lgs_post_physics_term_rewards.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+    if hasattr(lib, "lgs_step_deferred"):  # (absent only from pre-round-6 builds used in A/B timing)
+        lib.lgs_step_deferred.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+        lib.lgs_step_extras.argtypes = [vp, C.POINTER(cabi.EnvBuffers), C.c_int64]
+        lib.lgs_get_push_state.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+        for name in ("lgs_step_deferred", "lgs_step_extras", "lgs_get_push_state"):
+            getattr(lib, name).restype = C.c_int
     lib.lgs_get_counts.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.lgs_set_heightfield.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]
     lib.lgs_set_self_collision.argtypes = [vp, C.POINTER(cabi.SelfCollisionDesc)]
@@ -111,6 +117,7 @@ EXPORTED_SYMBOLS = [
     "lgs_step", "lgs_reset_all", "lgs_get_counts", "lgs_uniform", "lgs_set_heightfield",
     "lgs_step_physics", "lgs_post_physics", "lgs_reset_idx", "lgs_post_physics_rewards", "lgs_post_physics_finish",
     "lgs_post_physics_prepare", "lgs_post_physics_term_rewards",
+    "lgs_step_deferred", "lgs_step_extras", "lgs_get_push_state",
     "lgs_set_self_collision", "lgs_get_body_name", "lgs_get_dof_name", "lgs_find_body", "lgs_find_dof",
     "lgs_get_contact_stats", "lgs_get_instantiation", "lgs_get_factor_chain",
 ]
@@ -177,6 +184,20 @@ class Sim:
 
     def step(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_step(self.handle, C.byref(env_bufs), step_counter), "lgs_step")
+
+    def step_deferred(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        """lgs_step without its extras launch (its consumer does that work)."""
+        check(self.lib, self.lib.lgs_step_deferred(self.handle, C.byref(env_bufs), step_counter), "lgs_step_deferred")
+
+    def step_extras(self, env_bufs: cabi.EnvBuffers, step_counter: int):
+        """The extras of a deferred step, on their own (what lgs_step launches after the step)."""
+        check(self.lib, self.lib.lgs_step_extras(self.handle, C.byref(env_bufs), step_counter), "lgs_step_extras")
+
+    def push_state(self):
+        """(vsim, pushed) device pointers of the push bookkeeping (lgs_get_push_state)."""
+        v, p = C.c_void_p(), C.c_void_p()
+        check(self.lib, self.lib.lgs_get_push_state(self.handle, C.byref(v), C.byref(p)), "lgs_get_push_state")
+        return v.value, p.value
 
     def step_physics(self, env_bufs: cabi.EnvBuffers, step_counter: int):
         check(self.lib, self.lib.lgs_step_physics(self.handle, C.byref(env_bufs), step_counter), "lgs_step_physics")

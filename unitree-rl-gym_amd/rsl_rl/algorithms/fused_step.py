@@ -469,10 +469,13 @@ class FusedRollout:
                             P(storage.values[t]), P(storage.observations[t]), P(priv[t]) if priv is not None else None,
                             P(self.draw), par, self.seed)
         if pend is not None:
-            rew, dones, tout, tp, gamma = pend
+            rew, dones, tout, tp, gamma, job = pend
             rs.rewards, rs.dones, rs.time_outs = P(rew), P(dones), P(tout)
             rs.prev_value, rs.st_rewards, rs.st_dones = P(storage.values[tp]), P(storage.rewards[tp]), P(storage.dones[tp])
             rs.gamma = float(gamma)
+            if job is not None:  # that step's env extras, in this launch (pmlp_env_extras)
+                rs.extras = mm.EnvExtras(**job.fields)
+                job.consumed = True
         xs = [obs, cobs]
         mm.mlp_forward([dict(x=xs[n], kx=f.lins[n][0].in_features, K0=f.k0p[n], W=f.wb[n],
                              Wf=f.wf[n] if f.wf else None, b=[lin.bias.detach() for lin in f.lins[n]],
@@ -480,22 +483,29 @@ class FusedRollout:
                        rollout=rs)
         return self.actions
 
-    def store(self, rewards, dones, time_outs, storage, t, gamma):
+    def store(self, rewards, dones, time_outs, storage, t, gamma, extras=None):
         """PPO.process_env_step: deferred into the next act's launch; flush() issues it alone
         (the buffers are the env's: rewards is overwritten by the next env.step, which runs
-        after that launch)."""
-        self.pending = (rewards, dones, time_outs, t, gamma)
+        after that launch).  `extras`: the env step's own deferred extras (the env's
+        _DeferredExtras), done in the same launch before the bootstrap reads the time-outs."""
+        self.pending = (rewards, dones, time_outs, t, gamma, extras)
 
     def flush(self, storage):
-        """Issue a deferred process_env_step on its own (before the storage is read)."""
+        """Issue a deferred process_env_step (and its env extras) on its own (before the
+        storage is read)."""
         if self.pending is None:
             return
-        rewards, dones, time_outs, t, gamma = self.pending
+        rewards, dones, time_outs, t, gamma, job = self.pending
         self.pending = None
         P = mm._p
-        mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
-                                         P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
-                                         None, mm._stream()), "pmlp_store_step")
+        ex = None
+        if job is not None:
+            ex = mm.EnvExtras(**job.fields)
+            job.consumed = True
+        mm._ok(mm.load().pmlp_store_step_env(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+                                             P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
+                                             None, 0, None, 0, C.byref(ex) if ex is not None else None,
+                                             mm._stream()), "pmlp_store_step_env")
 
     @staticmethod
     def storable(rewards, dones, time_outs, N):
@@ -620,26 +630,28 @@ class RecurrentRollout:
                 out.append(h)
         return out, H
 
-    def store(self, rewards, dones, time_outs, storage, t, gamma):
+    def store(self, rewards, dones, time_outs, storage, t, gamma, extras=None):
         """PPO.process_env_step: pmlp_store_step at once (no forward launch to ride in).
         The launch also advances the policy-noise draw counter pmlp_act read (one thread,
         after the store), so every step and every iteration samples fresh noise, and zeroes
         the done envs' memory states (ActorCriticRecurrent.reset(dones), four masked_fill_
-        launches in the reference statement).  Returns True when it did that reset."""
+        launches in the reference statement), and does the env step's deferred extras
+        (`extras`, the env's _DeferredExtras) before the bootstrap reads the time-outs.
+        Returns True when it did that reset."""
         P = mm._p
         rs = self._reset_states()
-        if rs is None:
-            mm._ok(mm.load().pmlp_store_step(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
+        ex = None
+        if extras is not None:
+            ex = mm.EnvExtras(**extras.fields)
+            extras.consumed = True
+        states, H = rs if rs is not None else ([], 0)
+        ptrs = (C.c_void_p * len(states))(*[h.data_ptr() for h in states]) if states else None
+        mm._ok(mm.load().pmlp_store_step_env(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
                                              P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
-                                             P(self.draw), mm._stream()), "pmlp_store_step")
-            return False
-        states, H = rs
-        ptrs = (C.c_void_p * len(states))(*[h.data_ptr() for h in states])
-        mm._ok(mm.load().pmlp_store_step_reset(P(rewards), P(dones), P(time_outs), P(storage.values[t]),
-                                               P(storage.rewards[t]), P(storage.dones[t]), self.N, float(gamma),
-                                               P(self.draw), len(states), ptrs, H, mm._stream()),
-               "pmlp_store_step_reset")
-        return True
+                                             P(self.draw), len(states), ptrs, H,
+                                             C.byref(ex) if ex is not None else None, mm._stream()),
+               "pmlp_store_step_env")
+        return rs is not None
 
 
 def gae(storage, last_values, gamma, lam, world_size=1):

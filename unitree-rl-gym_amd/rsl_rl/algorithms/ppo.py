@@ -182,9 +182,12 @@ class PPO:
     def process_env_step(self, rewards, dones, infos):
         t, self._stored_t = self._stored_t, None
         time_outs = infos["time_outs"] if "time_outs" in infos else None
+        # the env step's extras, when the env left them to this consumer (LeggedRobot.step,
+        # defer_extras): the fused store does them in its launch, any other path first
+        job = infos.get("_deferred_extras") if isinstance(infos, dict) else None
         if t is not None and t == self.storage.step and \
                 fused_step.FusedRollout.storable(rewards, dones, time_outs, self.storage.num_envs):
-            reset_done = self._rollout.store(rewards, dones, time_outs, self.storage, t, self.gamma)
+            reset_done = self._rollout.store(rewards, dones, time_outs, self.storage, t, self.gamma, job)
             self.storage.step += 1
             self.transition.clear()
             if not reset_done:  # (the recurrent store launch zeroes the done envs' memories itself)
@@ -193,6 +196,8 @@ class PPO:
         if t is not None and isinstance(self._rollout, fused_step.RecurrentRollout):
             # the act sampled with the draw counter the skipped store launch would advance
             self._rollout.draw += 1
+        if job is not None:
+            job.run()
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones
         if "time_outs" in infos:  # bootstrap on time-outs

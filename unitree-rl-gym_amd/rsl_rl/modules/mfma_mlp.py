@@ -75,6 +75,15 @@ class MlpFwdJob(C.Structure):
                 ("ldo", C.c_int32), ("Wf", C.c_void_p * 4)]
 
 
+class EnvExtras(C.Structure):
+    """include/ppo_mlp.h pmlp_env_extras: a deferred env step's extras (leggedsim
+    lgs_step_deferred), done by the launch that consumes the step."""
+    _fields_ = [("acc", C.c_void_p), ("acc_next", C.c_void_p), ("nsum", C.c_int32), ("ep_len_s", C.c_float)] + \
+        [(n, C.c_void_p) for n in ("ep_means", "ep_snapshot", "time_out", "carry", "last_root_vel", "vsim",
+                                   "pushed")] + \
+        [("push", C.c_int32), ("step_counter", C.c_void_p)]
+
+
 class RolloutStep(C.Structure):
     """include/ppo_mlp.h pmlp_rollout_step (pmlp_rollout_forward)."""
     _fields_ = [("stdv", C.c_void_p), ("obs", C.c_void_p), ("cobs", C.c_void_p), ("O", C.c_int32),
@@ -83,7 +92,7 @@ class RolloutStep(C.Structure):
                                    "st_obs", "st_cobs", "draw")] + \
         [("parity", C.c_int32), ("seed", C.c_uint64)] + \
         [(n, C.c_void_p) for n in ("rewards", "dones", "time_outs", "prev_value", "st_rewards", "st_dones")] + \
-        [("gamma", C.c_float)]
+        [("gamma", C.c_float), ("extras", EnvExtras)]
 
 
 class HeadJob(C.Structure):
@@ -140,6 +149,7 @@ def load():
         L.pmlp_act.argtypes = [vp] * 5 + [i32, i32, i32, i32, vp, C.c_uint64] + [vp] * 9
         L.pmlp_store_step.argtypes = [vp] * 6 + [i32, f32, vp, vp]
         L.pmlp_store_step_reset.argtypes = [vp] * 6 + [i32, f32, vp, i32, vp, i32, vp]
+        L.pmlp_store_step_env.argtypes = [vp] * 6 + [i32, f32, vp, i32, vp, i32, C.POINTER(EnvExtras), vp]
         L.pmlp_mlp_forward.argtypes = [i32, C.POINTER(MlpFwdJob), i32, vp]
         if hasattr(L, "pmlp_mlp_forward_ppo_loss"):  # (absent from builds before round 4's end)
             L.pmlp_mlp_forward_ppo_loss_parts.argtypes = [i32, i32]

@@ -176,6 +176,10 @@ class OnPolicyRunner:
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
             with torch.inference_mode():
+                # the env leaves each step's extras to the rollout's next policy launch
+                # (LeggedRobot.defer_extras): one launch fewer per step; off outside collection
+                if hasattr(self.env, "defer_extras"):
+                    self.env.defer_extras = self._defer_env_extras()
                 graph = self._rollout_graph
                 if graph is not None and not graph.matches(obs, critic_obs):
                     graph = self._rollout_graph = None
@@ -205,6 +209,8 @@ class OnPolicyRunner:
                             cur_reward_sum[new_ids] = 0
                             cur_episode_length[new_ids] = 0
                     self._eager_rollouts += 1
+                if hasattr(self.env, "defer_extras"):
+                    self.env.defer_extras = False
                 sync()
                 stop = time.time()
                 collection_time = stop - start
@@ -259,6 +265,11 @@ class OnPolicyRunner:
             self._rollout_graph_failed = True
             warnings.warn(f"OnPolicyRunner: capturing the collection loop failed ({e}); collecting eagerly")
             return None
+
+    def _defer_env_extras(self):
+        """The fused rollout consumes deferred env extras (its store launches do the work);
+        runner cfg `defer_env_extras` = False keeps the env's own extras launch."""
+        return bool(self.cfg.get("defer_env_extras", True)) and getattr(self.alg, "_rollout", None) is not None
 
     def _rollout_graph_ok(self):
         """The whole collection loop replays as one HIP graph when nothing in it needs
