@@ -3,7 +3,7 @@
 and the wave-time shares (quad-cycle counters over SQ_WAVE_CYCLES; MI355X_MICROARCH.md
 constants table).  Written to a JSON that bench.py reads for roofline["valu"].
 
-    python tools/sq_summary.py <pass1_counter_collection.csv> <pass2_counter_collection.csv> out.json
+    python tools/sq_summary.py <pass1_counter_collection.csv> <pass2_counter_collection.csv> out.json [kernel]
 """
 import collections
 import csv
@@ -28,9 +28,9 @@ def load(path, kernel="k_step<"):
     return out
 
 
-def main(p1, p2, out):
-    c = load(p1)
-    c.update(load(p2))
+def main(p1, p2, out, kernel="k_step<"):
+    c = load(p1, kernel)
+    c.update(load(p2, kernel))
     waves = c.get("SQ_WAVES", 4096.0)
     wc = c["SQ_WAVE_CYCLES"]
     res = {
@@ -54,4 +54,4 @@ def main(p1, p2, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -828,6 +828,15 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
 //             order of the Sequential's two Linears) into slab row blockIdx.x.
 // LDS stays under 80 KB at H = 64 (two workgroups, 8 waves per CU).
 constexpr int HR = 128, HT = 256, HN0 = 32, HN1 = 16;  // rows, threads per workgroup; max N0, N1
+// the forward's rows / threads per workgroup (its split of a row never changes a result): 64 rows
+// on 4 threads each fill twice the CUs at the rollout's 4,096-8,192 rows (15.6 -> 10.2 us) and
+// gain 2 us at the update's 49,152 (profiles/round6/heads_fwd_tiling.txt)
+#ifndef PMLP_HEADS_FWD_ROWS
+#define PMLP_HEADS_FWD_ROWS 64
+#endif
+#ifndef PMLP_HEADS_FWD_THREADS
+#define PMLP_HEADS_FWD_THREADS 256
+#endif
 
 struct HeadJob {
     const float *h, *W0, *b0, *W1, *b1;
@@ -844,30 +853,31 @@ struct HeadJobs {
 // thread's loads are issued before any is stored (unrolled to U), unconditionally at clamped
 // addresses (a load under a divergent branch gets a vmcnt(0) at the branch's end), so the
 // round trips overlap instead of a load -> wait -> load chain per element.
-template <int U, typename F>
+template <int U, int NT = HT, typename F>
 __device__ __forceinline__ void stage(const float* __restrict__ src, int n, F&& put) {
     float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = src[min((int)threadIdx.x + u * HT, n - 1)];
+    for (int u = 0; u < U; ++u) v[u] = src[min((int)threadIdx.x + u * NT, n - 1)];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int i = threadIdx.x + u * HT;
+        const int i = threadIdx.x + u * NT;
         if (i < n) put(i, v[u]);
     }
 }
-// the h rows r0 .. r0 + HR of [M, H] into an LDS tile of row stride LH (rows >= M zero)
-template <int H, int LH>
+// the h rows r0 .. r0 + R of [M, H] into an LDS tile of row stride LH (rows >= M zero), NT threads
+template <int H, int LH, int R = HR, int NT = HT>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ h, int r0, int M, float* hs) {
-    constexpr int U = HR * H / 4 / HT;
+    constexpr int U = R * H / 4 / NT;
+    static_assert(U >= 1 && R * H / 4 == U * NT, "whole float4 loads per thread");
     float4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int i = threadIdx.x + u * HT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        const int i = threadIdx.x + u * NT, r = i / (H / 4), c = (i % (H / 4)) * 4;
         v[u] = *(const float4*)(h + (size_t)min(r0 + r, M - 1) * H + c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int i = threadIdx.x + u * HT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        const int i = threadIdx.x + u * NT, r = i / (H / 4), c = (i % (H / 4)) * 4;
         *(float4*)(hs + r * LH + c) = r0 + r < M ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
@@ -879,21 +889,25 @@ __device__ __forceinline__ void stage_span(const float* __restrict__ src, int N,
     stage<UMAX>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
 }
 
-template <int H>
-__global__ __launch_bounds__(HT) void k_heads_fwd(HeadJobs jobs, int M) {
+// R rows per workgroup of NT threads, NT / R threads per row (each a share of the row's units;
+// every unit's and output's sum runs in the same order whatever the split: bitwise one result)
+template <int H, int R = HR, int NT = HT>
+__global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M) {
+    constexpr int PARTS = NT / R;
+    static_assert(PARTS * R == NT && (PARTS == 2 || PARTS == 4), "2 or 4 threads per row");
     const HeadJob& J = jobs.j[blockIdx.y];
-    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
-    const int row = tid & (HR - 1), half = tid / HR;
+    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * R;
+    const int row = tid & (R - 1), half = tid / R;
     constexpr int LH = H + 4, LY = HN0 + 1, LO = HN1 + 1;
-    constexpr int HS = HR * LH > HR * (LY + LO) ? HR * LH : HR * (LY + LO);  // h tile, then y0 + out
+    constexpr int HS = R * LH > R * (LY + LO) ? R * LH : R * (LY + LO);  // h tile, then y0 + out
     __shared__ __attribute__((aligned(16))) float hs[HS];
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float bb0[HN0], w1[HN1 * HN0], bb1[HN1];
-    stage<HN0 * H / HT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
-    stage<(HN1 * HN0 + HT - 1) / HT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
+    stage<HN0 * H / NT, NT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
+    stage<(HN1 * HN0 + NT - 1) / NT, NT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
     if (tid < N0) bb0[tid] = J.b0[tid];
     if (tid < N1) bb1[tid] = J.b1[tid];
-    stage_rows<H, LH>(J.h, r0, M, hs);
+    stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
     __syncthreads();
     float hr[H];
 #pragma unroll
@@ -902,8 +916,8 @@ __global__ __launch_bounds__(HT) void k_heads_fwd(HeadJobs jobs, int M) {
         hr[k] = v.x; hr[k + 1] = v.y; hr[k + 2] = v.z; hr[k + 3] = v.w;
     }
     __syncthreads();  // (hs is reused for the y0 tile below)
-    // y0: this thread's half of the units, one at a time (four FMA chains over k mod 4)
-    const int nh = N0 / 2, jb = half * nh;
+    // y0: this thread's share of the units, one at a time (four FMA chains over k mod 4)
+    const int nh = N0 / PARTS, jb = half * nh;
 #pragma unroll 1
     for (int j = jb; j < jb + nh; ++j) {
         float z[4] = {bb0[j], 0.f, 0.f, 0.f};
@@ -917,10 +931,10 @@ __global__ __launch_bounds__(HT) void k_heads_fwd(HeadJobs jobs, int M) {
         hs[row * LY + j] = zz > 0.f ? zz : expm1f(zz);
     }
     __syncthreads();
-    // out: this thread's outputs i = half, half + 2, ... over the row's y0 (LDS)
-    float* os = hs + HR * LY;  // [HR][LO]
+    // out: this thread's outputs i = half, half + PARTS, ... over the row's y0 (LDS)
+    float* os = hs + R * LY;  // [R][LO]
 #pragma unroll 1
-    for (int i = half; i < N1; i += 2) {
+    for (int i = half; i < N1; i += PARTS) {
         float a[4] = {bb1[i], 0.f, 0.f, 0.f};
 #pragma unroll 1
         for (int j = 0; j < N0; j += 4) {
@@ -930,11 +944,11 @@ __global__ __launch_bounds__(HT) void k_heads_fwd(HeadJobs jobs, int M) {
         os[row * LO + i] = (a[0] + a[1]) + (a[2] + a[3]);
     }
     __syncthreads();
-    for (int i = tid; i < HR * N0; i += HT) {  // coalesced row-major stores
+    for (int i = tid; i < R * N0; i += NT) {  // coalesced row-major stores
         const int r = i / N0, c = i - r * N0;
         if (r0 + r < M) J.y0[(size_t)(r0 + r) * N0 + c] = hs[r * LY + c];
     }
-    for (int i = tid; i < HR * N1; i += HT) {
+    for (int i = tid; i < R * N1; i += NT) {
         const int r = i / N1, c = i - r * N1;
         if (r0 + r < M) J.out[(size_t)(r0 + r) * N1 + c] = os[r * LO + c];
     }
@@ -1241,11 +1255,12 @@ PMLP_API int32_t pmlp_heads_blocks(int32_t M) { return (M + HR - 1) / HR; }
 PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
     if (int e = heads_check("pmlp_heads_forward", njobs, jobs, M, H, false)) return e;
     const HeadJobs hj = heads_pack(njobs, jobs);
-    const dim3 g((M + HR - 1) / HR, njobs);
+    constexpr int FR = PMLP_HEADS_FWD_ROWS, FT = PMLP_HEADS_FWD_THREADS;
+    const dim3 g((M + FR - 1) / FR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL(k_heads_fwd<32>, g, dim3(HT), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL(k_heads_fwd<64>, g, dim3(HT), 0, s, hj, M);
-    else hipLaunchKernelGGL(k_heads_fwd<128>, g, dim3(HT), 0, s, hj, M);
+    if (H == 32) hipLaunchKernelGGL((k_heads_fwd<32, FR, FT>), g, dim3(FT), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL((k_heads_fwd<64, FR, FT>), g, dim3(FT), 0, s, hj, M);
+    else hipLaunchKernelGGL((k_heads_fwd<128, FR, FT>), g, dim3(FT), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward: ") + hipGetErrorString(e));
 }
