@@ -2,7 +2,7 @@
 with the libppomlp.so named by PPOMLP_LIB: median time of graph replays, and the rollout
 storage + parameters after two seeded learning iterations digested (sha256) into argv[1] (for a bitwise
 comparison of two builds, tools/gpu_rollout_ab.sh).
-usage: [PPOMLP_LIB=...] [ROLL_DEFER=0] python tools/probes/rollout_time.py out.json"""
+usage: [PPOMLP_LIB=...] [ROLL_DEFER=0] [ROLL_TASK=h1 ROLL_ENVS=8192] python tools/probes/rollout_time.py out.json"""
 import hashlib
 import json
 import os
@@ -17,12 +17,13 @@ import isaacgym  # noqa: F401,E402
 from legged_gym.envs import task_registry  # noqa: E402
 from legged_gym.utils import get_args  # noqa: E402
 
-args = get_args(["--task", "go2", "--num_envs", "4096", "--headless"])
-env, _ = task_registry.make_env(name="go2", args=args)
-_, train_cfg = task_registry.get_cfgs("go2")
+TASK, NENV = os.environ.get("ROLL_TASK", "go2"), os.environ.get("ROLL_ENVS", "4096")
+args = get_args(["--task", TASK, "--num_envs", NENV, "--headless"])
+env, _ = task_registry.make_env(name=TASK, args=args)
+_, train_cfg = task_registry.get_cfgs(TASK)
 if os.environ.get("ROLL_DEFER") == "0":  # the env's own extras launch (runner cfg defer_env_extras)
     train_cfg.runner.defer_env_extras = False
-r, _ = task_registry.make_alg_runner(env=env, name="go2", args=args, train_cfg=train_cfg, log_root=None)
+r, _ = task_registry.make_alg_runner(env=env, name=TASK, args=args, train_cfg=train_cfg, log_root=None)
 r.learn(2)  # the second iteration captures the rollout graph
 assert r._rollout_graph is not None
 torch.cuda.synchronize()
@@ -42,5 +43,6 @@ with torch.inference_mode(False):
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / 4)
 ts.sort()
-print(f"{os.path.basename(os.environ.get('PPOMLP_LIB', 'libppomlp.so'))} defer={os.environ.get('ROLL_DEFER', '1')}: rollout {ts[len(ts) // 2]:.3f} ms median, "
+print(f"{os.path.basename(os.environ.get('PPOMLP_LIB', 'libppomlp.so'))} defer={os.environ.get('ROLL_DEFER', '1')} "
+      f"tiles={os.environ.get('PMLP_LSTM_STEP_TILES', '-')} {TASK}x{NENV}: rollout {ts[len(ts) // 2]:.3f} ms median, "
       f"{ts[0]:.3f} min", flush=True)

@@ -15,6 +15,7 @@
 // The input projection x W_ih^T + b is one GEMM over all T*B rows beforehand (gx).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -408,15 +409,18 @@ __device__ __forceinline__ float ror8(float v) {
 // blockIdx.y selects the job; a job with fewer workgroups than the grid's x leaves the rest.
 struct MFwdBatch { MFwdArgs m[2]; };
 
+// tiles: consecutive 16-env tiles per workgroup, run one after the other on the weight
+// fragments loaded once (the rollout's single steps: the fragments' 128 KB of loads per
+// workgroup otherwise dominate a T = 1 launch); each tile's arithmetic is the same
 template <int SPLIT>
-__global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab) {
+__global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles) {
     constexpr int NP = SPLIT == 3 ? 2 : 1;  // operand parts (hi, lo)
     __shared__ __attribute__((aligned(16))) mbf16 A[NP][2][ME * MLDA];
     const MFwdArgs a = ab.m[blockIdx.y];
     const int T = a.T, B = a.B, I = a.I, RL = I + MH + 1;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int e0 = blockIdx.x * ME;
-    if (e0 >= B) return;  // (whole workgroup)
+    const int ebase = blockIdx.x * ME * tiles;
+    if (ebase >= B) return;  // (whole workgroup)
     const int j = lane & 15, rg = lane >> 4;  // column in the tile; row group (envs 4 rg .. 4 rg + 3)
     const int hj = j >> 3;                    // 0: this column holds i / g, 1: f / o
     const int uu = 8 * w + (j & 7);           // this lane's unit
@@ -439,6 +443,10 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab) {
                 if constexpr (NP == 2) wf[NP - 1][tt][s][e] = lo;
             }
     }
+    for (int q = 0; q < tiles; ++q) {
+    const int e0 = ebase + q * ME;
+    if (e0 >= B) break;   // (uniform)
+    if (q) __syncthreads();  // the previous tile's last reads of A are done
     auto put = [&](int buf, int idx, float v) {  // operand element (hi, lo)
         mbf16 hi, lo;
         split_bf16(v, hi, lo);
@@ -563,6 +571,7 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab) {
         }
         __syncthreads();
     }
+    }  // tiles
 }
 
 struct MBwdArgs {
@@ -1185,6 +1194,18 @@ PMLP_API int pmlp_lstm_bwd(int32_t T, int32_t B, int32_t H, const float* whh, co
     }
 }
 
+// 16-env tiles per workgroup of a single step (the rollout's): PMLP_LSTM_STEP_TILES overrides
+static int step_tiles(int B) {
+    static const int env = [] {
+        const char* v = std::getenv("PMLP_LSTM_STEP_TILES");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (env > 0) return env;
+    // 128 workgroups per memory (2,048 envs a tile-row): the H1 x 8192 rollout 9.95 -> 9.59 ms at
+    // 4 tiles, G1 x 4096 6.06 -> 5.93 ms at 2 (profiles/round6/lstm_step_tiles.txt)
+    return std::max(1, std::min(4, B / 2048));
+}
+
 PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, const float* x, const float* wih,
                                 const float* bih, const float* bhh, const float* whh, const float* h0, const float* c0,
                                 const uint8_t* reset, float* h_out, float* c_out, float* gact, float* xh, void* stream) {
@@ -1192,7 +1213,7 @@ PMLP_API int pmlp_lstm_fwd_mfma(int32_t T, int32_t B, int32_t H, int32_t I, cons
     if (H != MH || I <= 0 || I > MKX) return fail("pmlp_lstm_fwd_mfma: hidden 64, input 1..64");
     MFwdBatch a{};
     a.m[0] = MFwdArgs{T, B, I, x, wih, bih, bhh, whh, h0, c0, reset, h_out, c_out, gact, xh, nullptr, nullptr};
-    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a, 1);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma: ") + hipGetErrorString(e));
 }
@@ -1289,7 +1310,8 @@ PMLP_API int pmlp_lstm_step_mfma(int32_t B, int32_t H, int32_t I, const float* x
     if ((h_save == nullptr) != (c_save == nullptr)) return fail("pmlp_lstm_step_mfma: h_save and c_save together");
     MFwdBatch a{};
     a.m[0] = MFwdArgs{1, B, I, x, wih, bih, bhh, whh, h, c, nullptr, h, c, nullptr, nullptr, h_save, c_save};
-    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME), dim3(512), 0, (hipStream_t)stream, a);
+    const int nt = step_tiles(B);
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME * nt - 1) / (ME * nt)), dim3(512), 0, (hipStream_t)stream, a, nt);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma: ") + hipGetErrorString(e));
 }
@@ -1319,7 +1341,7 @@ PMLP_API int pmlp_lstm_fwd_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, i
         a.m[i] = MFwdArgs{T, B, J.I, J.x, J.w_ih, J.b_ih, J.b_hh, J.w_hh, J.h0, J.c0, reset,
                           J.h_out, J.c_out, J.gact, J.xh, nullptr, nullptr};
     }
-    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a, 1);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_fwd_mfma_jobs: ") + hipGetErrorString(e));
 }
@@ -1349,7 +1371,8 @@ PMLP_API int pmlp_lstm_step_mfma_jobs(int32_t njobs, const pmlp_lstm_job* jobs, 
         a.m[i] = MFwdArgs{1, B, J.I, J.x, J.w_ih, J.b_ih, J.b_hh, J.w_hh, J.h_out, J.c_out, nullptr,
                           J.h_out, J.c_out, nullptr, nullptr, J.h_save, J.c_save};
     }
-    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME - 1) / ME, njobs), dim3(512), 0, (hipStream_t)stream, a);
+    const int nt = step_tiles(B);
+    hipLaunchKernelGGL(k_lstm_fwd_mfma8<3>, dim3((B + ME * nt - 1) / (ME * nt), njobs), dim3(512), 0, (hipStream_t)stream, a, nt);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_lstm_step_mfma_jobs: ") + hipGetErrorString(e));
 }
