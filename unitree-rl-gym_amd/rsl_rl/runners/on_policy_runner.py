@@ -178,39 +178,15 @@ class OnPolicyRunner:
             with torch.inference_mode():
                 # the env leaves each step's extras to the rollout's next policy launch
                 # (LeggedRobot.defer_extras): one launch fewer per step; off outside collection
-                if hasattr(self.env, "defer_extras"):
+                defer = hasattr(self.env, "defer_extras")
+                if defer:
                     self.env.defer_extras = self._defer_env_extras()
-                graph = self._rollout_graph
-                if graph is not None and not graph.matches(obs, critic_obs):
-                    graph = self._rollout_graph = None
-                if graph is None and self._eager_rollouts > 0 and self._rollout_graph_ok():
-                    # captured after one eager rollout has initialised everything lazily built
-                    graph = self._rollout_graph = self._capture_rollout(obs, critic_obs, cur_reward_sum,
-                                                                        cur_episode_length)
-                if graph is not None:
-                    fused = getattr(self.alg, "_fused", None)
-                    if fused is not None:  # a load() since the capture: the graph reads the bf16 copies
-                        fused.ensure_weights()
-                    obs, critic_obs = graph.replay()
-                    if self.log_dir is not None:
-                        ep_infos.extend(graph.ep_infos)
-                        graph.finished_episodes(rewbuffer, lenbuffer)
-                else:
-                    for _ in range(self.num_steps_per_env):
-                        obs, critic_obs, rewards, dones, infos = self._collect_step(obs, critic_obs)
-                        if self.log_dir is not None:
-                            if "episode" in infos:
-                                ep_infos.append(infos["episode"])
-                            cur_reward_sum += rewards
-                            cur_episode_length += 1
-                            new_ids = (dones > 0).nonzero(as_tuple=False)
-                            rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
-                            lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
-                            cur_reward_sum[new_ids] = 0
-                            cur_episode_length[new_ids] = 0
-                    self._eager_rollouts += 1
-                if hasattr(self.env, "defer_extras"):
-                    self.env.defer_extras = False
+                try:
+                    obs, critic_obs = self._collection(obs, critic_obs, ep_infos, rewbuffer, lenbuffer,
+                                                       cur_reward_sum, cur_episode_length)
+                finally:
+                    if defer:
+                        self.env.defer_extras = False
                 sync()
                 stop = time.time()
                 collection_time = stop - start
@@ -232,6 +208,40 @@ class OnPolicyRunner:
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))
+
+    def _collection(self, obs, critic_obs, ep_infos, rewbuffer, lenbuffer, cur_reward_sum, cur_episode_length):
+        """The num_steps_per_env steps of one iteration's collection (on_policy_runner.py:106-125 of
+        rsl_rl v1.0.2): the captured graph's replay, or the eager loop."""
+        graph = self._rollout_graph
+        if graph is not None and not graph.matches(obs, critic_obs):
+            graph = self._rollout_graph = None
+        if graph is None and self._eager_rollouts > 0 and self._rollout_graph_ok():
+            # captured after one eager rollout has initialised everything lazily built
+            graph = self._rollout_graph = self._capture_rollout(obs, critic_obs, cur_reward_sum,
+                                                                cur_episode_length)
+        if graph is not None:
+            fused = getattr(self.alg, "_fused", None)
+            if fused is not None:  # a load() since the capture: the graph reads the bf16 copies
+                fused.ensure_weights()
+            obs, critic_obs = graph.replay()
+            if self.log_dir is not None:
+                ep_infos.extend(graph.ep_infos)
+                graph.finished_episodes(rewbuffer, lenbuffer)
+        else:
+            for _ in range(self.num_steps_per_env):
+                obs, critic_obs, rewards, dones, infos = self._collect_step(obs, critic_obs)
+                if self.log_dir is not None:
+                    if "episode" in infos:
+                        ep_infos.append(infos["episode"])
+                    cur_reward_sum += rewards
+                    cur_episode_length += 1
+                    new_ids = (dones > 0).nonzero(as_tuple=False)
+                    rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                    lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                    cur_reward_sum[new_ids] = 0
+                    cur_episode_length[new_ids] = 0
+            self._eager_rollouts += 1
+        return obs, critic_obs
 
     def _collect_step(self, obs, critic_obs):
         """One step of the reference's collection loop (on_policy_runner.py:106-114)."""
