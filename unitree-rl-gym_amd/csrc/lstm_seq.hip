@@ -840,6 +840,9 @@ constexpr int HR = 128, HT = 256, HN0 = 32, HN1 = 16;  // rows, threads per work
 // the forward's rows / threads per workgroup (its split of a row never changes a result): 64 rows
 // on 4 threads each fill twice the CUs at the rollout's 4,096-8,192 rows (15.6 -> 10.2 us) and
 // gain 2 us at the update's 49,152 (profiles/round6/heads_fwd_tiling.txt)
+#ifndef PMLP_HEADS_BWD_ROWS
+#define PMLP_HEADS_BWD_ROWS 128
+#endif
 #ifndef PMLP_HEADS_FWD_ROWS
 #define PMLP_HEADS_FWD_ROWS 64
 #endif
@@ -891,11 +894,11 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ h, int r0, 
     }
 }
 // a [rows, N] row-major span (N <= 32 runtime) into an LDS tile of row stride L, zero past M
-template <int UMAX, int L>
+template <int UMAX, int L, int R = HR, int NT = HT>
 __device__ __forceinline__ void stage_span(const float* __restrict__ src, int N, int r0, int M, float* t) {
-    const int nr = min(HR, M - r0);
-    for (int i = threadIdx.x; i < HR * N; i += HT) t[(i / N) * L + i % N] = 0.f;
-    stage<UMAX>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
+    const int nr = min(R, M - r0);
+    for (int i = threadIdx.x; i < R * N; i += NT) t[(i / N) * L + i % N] = 0.f;
+    stage<UMAX, NT>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
 }
 
 // R rows per workgroup of NT threads, NT / R threads per row (each a share of the row's units;
@@ -963,30 +966,33 @@ __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M) {
     }
 }
 
-template <int H>
-__global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
+// R rows per workgroup of 2 R threads (the weight-gradient partial sums run over R-row halves:
+// R sets the slab rows, pmlp_heads_blocks)
+template <int H, int R = HR>
+__global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
+    constexpr int NT = 2 * R;
     const HeadJob& J = jobs.j[blockIdx.y];
-    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * HR;
-    const int row = tid & (HR - 1), half = tid / HR;
+    const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * R;
+    const int row = tid & (R - 1), half = tid / R;
     constexpr int LH = H + 4, LZ = HN0 + 4, LO = HN1 + 1;
-    __shared__ __attribute__((aligned(16))) float hs[HR * LH];   // h, then dW0 halves, then dh
-    __shared__ __attribute__((aligned(16))) float zs[HR * LZ];   // y0, then dz0
-    __shared__ float ds[HR * LO];                                 // dout
+    __shared__ __attribute__((aligned(16))) float hs[R * LH];   // h, then dW0 halves, then dh
+    __shared__ __attribute__((aligned(16))) float zs[R * LZ];   // y0, then dz0
+    __shared__ float ds[R * LO];                                 // dout
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float w1[HN1 * HN0];
-    stage<HN0 * H / HT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
-    stage<(HN1 * HN0 + HT - 1) / HT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
-    stage_rows<H, LH>(J.h, r0, M, hs);
-    stage_span<HR * HN0 / HT, LZ>(J.y0, N0, r0, M, zs);
-    stage_span<HR * HN1 / HT, LO>(J.dout, N1, r0, M, ds);
+    stage<HN0 * H / NT, NT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
+    stage<(HN1 * HN0 + NT - 1) / NT, NT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
+    stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
+    stage_span<(R * HN0 + NT - 1) / NT, LZ, R, NT>(J.y0, N0, r0, M, zs);
+    stage_span<(R * HN1 + NT - 1) / NT, LO, R, NT>(J.dout, N1, r0, M, ds);
     __syncthreads();
     float* sl = J.slab + (size_t)blockIdx.x * (N0 * H + N0 + N1 * N0 + N1);
     // dW1 (+ db1 on j = 0) from the y0 and dout tiles, before y0 is overwritten
-    for (int t = tid; t < N1 * N0; t += HT) {
+    for (int t = tid; t < N1 * N0; t += NT) {
         const int i = t / N0, j = t - i * N0;
         float a = 0.f, b = 0.f;
 #pragma unroll 8
-        for (int r = 0; r < HR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const float d = ds[r * LO + i];
             a = fmaf(d, zs[r * LZ + j], a);
             b += d;
@@ -1020,15 +1026,15 @@ __global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
     // dW0 (+ db0 on k0 = 0): 4 x 4 tiles, each over one half of the rows; the second half's
     // partial goes through LDS (over the h tile) and the first adds it (fixed order)
     const int ntile = (N0 / 4) * (H / 4);  // one tile per thread pair and pass
-    float* part = hs;  // [HR][20]: the h tile, after its last read (dh overwrites it later)
-    static_assert(HR * 20 <= HR * LH, "dW0 partials fit the h tile");
-    for (int tb = 0; tb < ntile; tb += HR) {
+    float* part = hs;  // [R][20]: the h tile, after its last read (dh overwrites it later)
+    static_assert(R * 20 <= R * LH, "dW0 partials fit the h tile");
+    for (int tb = 0; tb < ntile; tb += R) {
         float a[4][4] = {}, bs[4] = {};
         const int t = tb + row, j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
         if (t < ntile) {
-            const int rb = half * (HR / 2);
+            const int rb = half * (R / 2);
 #pragma unroll 4
-            for (int r = rb; r < rb + HR / 2; ++r) {
+            for (int r = rb; r < rb + R / 2; ++r) {
                 const float4 z4 = *(const float4*)(zs + r * LZ + j0);
                 const float4 h4 = *(const float4*)(hs + r * LH + k0);
                 const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
@@ -1062,9 +1068,9 @@ __global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) sl[N0 * H + j0 + u] = bs[u];
         }
-        if (tb + HR < ntile) {  // the next pass reads the h tile again: restage it
+        if (tb + R < ntile) {  // the next pass reads the h tile again: restage it
             __syncthreads();
-            stage_rows<H, LH>(J.h, r0, M, hs);
+            stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
             __syncthreads();
         }
     }
@@ -1091,7 +1097,7 @@ __global__ __launch_bounds__(HT) void k_heads_bwd(HeadJobs jobs, int M) {
             *(float4*)(hs + row * LH + kb + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
     }
     __syncthreads();
-    for (int i = tid; i < HR * (H / 4); i += HT) {
+    for (int i = tid; i < R * (H / 4); i += NT) {
         const int r = i / (H / 4), c = (i % (H / 4)) * 4;
         if (r0 + r < M) *(float4*)(J.dh + (size_t)(r0 + r) * H + c) = *(const float4*)(hs + r * LH + c);
     }
@@ -1271,7 +1277,7 @@ static HeadJobs heads_pack(int njobs, const pmlp_head_job* jobs) {
     return hj;
 }
 
-PMLP_API int32_t pmlp_heads_blocks(int32_t M) { return (M + HR - 1) / HR; }
+PMLP_API int32_t pmlp_heads_blocks(int32_t M) { return (M + PMLP_HEADS_BWD_ROWS - 1) / PMLP_HEADS_BWD_ROWS; }
 
 PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
     if (int e = heads_check("pmlp_heads_forward", njobs, jobs, M, H, false)) return e;
@@ -1289,11 +1295,12 @@ PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_
 PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
     if (int e = heads_check("pmlp_heads_backward", njobs, jobs, M, H, true)) return e;
     const HeadJobs hj = heads_pack(njobs, jobs);
-    const dim3 g((M + HR - 1) / HR, njobs);
+    constexpr int BR = PMLP_HEADS_BWD_ROWS;
+    const dim3 g((M + BR - 1) / BR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL(k_heads_bwd<32>, g, dim3(HT), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL(k_heads_bwd<64>, g, dim3(HT), 0, s, hj, M);
-    else hipLaunchKernelGGL(k_heads_bwd<128>, g, dim3(HT), 0, s, hj, M);
+    if (H == 32) hipLaunchKernelGGL((k_heads_bwd<32, BR>), g, dim3(2 * BR), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL((k_heads_bwd<64, BR>), g, dim3(2 * BR), 0, s, hj, M);
+    else hipLaunchKernelGGL((k_heads_bwd<128, BR>), g, dim3(2 * BR), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_backward: ") + hipGetErrorString(e));
 }
