@@ -57,3 +57,15 @@ def test_name_queries_without_a_sim_are_null_not_a_crash():
     assert lib.lgs_get_body_name(None, 0) is None and lib.lgs_last_error()
     assert lib.lgs_get_dof_name(None, 0) is None
     assert lib.lgs_find_body(None, b"base") == -1 and lib.lgs_find_dof(None, b"x") == -1
+
+
+def test_deferred_step_entries_refuse_null_arguments():
+    """lgs_step_deferred / lgs_step_extras / lgs_get_push_state (the rollout-consumed extras,
+    include/leggedsim.h) on a NULL sim: a status and an error text, no launch."""
+    from leggedsim import native
+    lib = native.load()
+    E = cabi.EnvBuffers()
+    assert lib.lgs_step_deferred(None, C.byref(E), 0) != 0 and lib.lgs_last_error()
+    assert lib.lgs_step_extras(None, C.byref(E), 0) != 0
+    v, p = C.c_void_p(), C.c_void_p()
+    assert lib.lgs_get_push_state(None, C.byref(v), C.byref(p)) != 0

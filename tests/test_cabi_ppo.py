@@ -40,13 +40,15 @@ def test_ctypes_job_structs_match_c_layout(tmp_path):
     src.write_text('#include <stdio.h>\n#include "ppo_mlp.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
                    ' sizeof(pmlp_gemm_job), sizeof(pmlp_mirror_job), sizeof(pmlp_convert_job),'
                    ' sizeof(pmlp_reduce_job)); printf("%zu %zu %zu\\n", sizeof(pmlp_head_job), sizeof(pmlp_lstm_job), sizeof(pmlp_reduce_step));'
+                   ' printf("%zu %zu\\n", sizeof(pmlp_env_extras), sizeof(pmlp_rollout_step));'
                    ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     from rsl_rl.modules import lstm_seq
     assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob),
-                   C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob), C.sizeof(mm.ReduceStep)]
+                   C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob), C.sizeof(mm.ReduceStep),
+                   C.sizeof(mm.EnvExtras), C.sizeof(mm.RolloutStep)]
 
 
 def _job(**kw):
@@ -142,3 +144,14 @@ def test_reduce_slabs_parts_sizes_the_norm_partials(lib):
     rs.norm_partial, rs.step, rs.lr, rs.nparts = 16, 16, 16, n - 1
     assert lib.pmlp_reduce_slabs_step(2, big, C.byref(rs), None) != 0
     assert b"capacity" in lib.pmlp_last_error()
+
+
+def test_store_step_refuses_incomplete_env_extras(lib):
+    """pmlp_store_step_env with a deferred env step's extras missing a buffer (include/ppo_mlp.h
+    pmlp_env_extras): refused before launch."""
+    from rsl_rl.modules import mfma_mlp as mm
+    ex = mm.EnvExtras(acc=16, acc_next=None, nsum=10, ep_len_s=20.0, time_out=16, pushed=16)
+    rc = lib.pmlp_store_step_env(16, 16, 16, 16, 16, 16, 64, 0.99, None, 0, None, 0, C.byref(ex), None)
+    assert rc != 0 and b"env extras" in lib.pmlp_last_error()
+    ex.acc_next, ex.ep_len_s = 16, 0.0  # no episode length
+    assert lib.pmlp_store_step_env(16, 16, 16, 16, 16, 16, 64, 0.99, None, 0, None, 0, C.byref(ex), None) != 0
