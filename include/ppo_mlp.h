@@ -393,6 +393,20 @@ typedef struct {
 PMLP_API int32_t pmlp_heads_blocks(int32_t M);
 PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream);
 PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream);
+/* pmlp_heads_forward of the actor (jobs[0], N1 = A <= 16) and the critic (jobs[1], N1 = 1)
+ * with pmlp_act in the same launch (the recurrent rollout's policy step): each workgroup
+ * samples its rows' actions from the mu it just computed (pmlp_act's Philox counters and
+ * arithmetic: the same bits) and writes the storage rows; the critic's workgroups write the
+ * values and privileged rows.  The draw counter is read, not advanced (the store advances it). */
+typedef struct {
+    const float *stdv, *obs, *cobs;
+    int32_t O, CO, A;
+    const int64_t* draw;
+    uint64_t seed;
+    float *actions_out, *st_actions, *st_logp, *st_mu, *st_sigma, *st_value, *st_obs, *st_cobs;
+} pmlp_head_act;
+PMLP_API int pmlp_heads_forward_act(const pmlp_head_job* jobs, int32_t M, int32_t H, const pmlp_head_act* act,
+                                    void* stream);
 
 /* The same loss for the fused optimizer step (gradient of the loss itself):
  * one pass writes the output gradients straight into the MLP backward's bf16

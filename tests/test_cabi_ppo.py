@@ -40,7 +40,7 @@ def test_ctypes_job_structs_match_c_layout(tmp_path):
     src.write_text('#include <stdio.h>\n#include "ppo_mlp.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
                    ' sizeof(pmlp_gemm_job), sizeof(pmlp_mirror_job), sizeof(pmlp_convert_job),'
                    ' sizeof(pmlp_reduce_job)); printf("%zu %zu %zu\\n", sizeof(pmlp_head_job), sizeof(pmlp_lstm_job), sizeof(pmlp_reduce_step));'
-                   ' printf("%zu %zu\\n", sizeof(pmlp_env_extras), sizeof(pmlp_rollout_step));'
+                   ' printf("%zu %zu %zu\\n", sizeof(pmlp_env_extras), sizeof(pmlp_rollout_step), sizeof(pmlp_head_act));'
                    ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
@@ -48,7 +48,7 @@ def test_ctypes_job_structs_match_c_layout(tmp_path):
     from rsl_rl.modules import lstm_seq
     assert got == [C.sizeof(mm.GemmJob), C.sizeof(mm.MirrorJob), C.sizeof(mm.ConvertJob), C.sizeof(mm.ReduceJob),
                    C.sizeof(mm.HeadJob), C.sizeof(lstm_seq.LstmJob), C.sizeof(mm.ReduceStep),
-                   C.sizeof(mm.EnvExtras), C.sizeof(mm.RolloutStep)]
+                   C.sizeof(mm.EnvExtras), C.sizeof(mm.RolloutStep), C.sizeof(mm.HeadAct)]
 
 
 def _job(**kw):

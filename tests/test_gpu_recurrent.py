@@ -534,3 +534,38 @@ def test_recurrent_store_zeroes_the_done_envs_memories_as_reset():
             ref = b.masked_fill(dones.view(1, -1, 1), 0.0)
             assert torch.equal(a, ref)
     assert not calls  # the torch reset was not needed
+
+
+def test_recurrent_heads_with_fused_sampling_are_bitwise_the_separate_launches():
+    """pmlp_heads_forward_act (the actor's sampling and the storage rows in the heads' launch)
+    against pmlp_heads_forward + pmlp_act: from identical policies, memories and noise keys,
+    the actions and every storage row are bitwise the same over a few steps."""
+    import copy
+    torch.manual_seed(6)
+    N, T, O, P, A, H = 512, 3, 47, 50, 12, 64
+    ac0 = ActorCriticRecurrent(O, P, A, actor_hidden_dims=[32], critic_hidden_dims=[32], rnn_type="lstm",
+                               rnn_hidden_size=H, rnn_num_layers=1).cuda()
+    algs = []
+    for fuse in (False, True):
+        torch.manual_seed(11)  # the rollout's noise seed
+        alg = PPO(copy.deepcopy(ac0), device="cuda")
+        alg.init_storage(N, T, [O], [P], [A])
+        assert alg._rollout is not None and alg._rollout.heads is not None
+        alg._rollout.fuse_act = fuse
+        algs.append(alg)
+    assert algs[0]._rollout.seed == algs[1]._rollout.seed
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for t in range(T):
+        obs, cobs = torch.randn(N, O, device="cuda", generator=g), torch.randn(N, P, device="cuda", generator=g)
+        dones = torch.rand(N, device="cuda", generator=g) < 0.1
+        acts = []
+        for alg in algs:
+            with torch.inference_mode():
+                acts.append(alg.act(obs, cobs).clone())
+                alg.process_env_step(torch.ones(N, device="cuda"), dones,
+                                     {"time_outs": torch.zeros(N, dtype=torch.bool, device="cuda")})
+        assert torch.equal(acts[0], acts[1])
+    sa, sb = algs[0].storage, algs[1].storage
+    for k in ("actions", "actions_log_prob", "mu", "sigma", "values", "observations", "privileged_observations",
+              "rewards", "dones"):
+        assert torch.equal(getattr(sa, k), getattr(sb, k)), k

@@ -30,6 +30,11 @@ torch.cuda.synchronize()
 st = r.alg.storage
 out = {k: getattr(st, k).detach().cpu().numpy() for k in ("actions", "actions_log_prob", "values", "mu", "rewards")}
 out.update({f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(r.alg.actor_critic.parameters())})
+for name in ("saved_hidden_states_a", "saved_hidden_states_c"):  # (recurrent policies)
+    for j, h in enumerate(getattr(st, name, None) or []):
+        out[f"{name}{j}"] = h.detach().cpu().numpy()
+if hasattr(st, "advantages"):
+    out["advantages"], out["returns"] = st.advantages.detach().cpu().numpy(), st.returns.detach().cpu().numpy()
 with open(sys.argv[1], "w") as f:  # a digest per array (the arrays themselves are ~100 MB per run)
     json.dump({k: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() for k, v in out.items()}, f)
 ts = []

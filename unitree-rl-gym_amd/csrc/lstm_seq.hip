@@ -21,6 +21,7 @@
 #include <string>
 
 #include "../../include/ppo_mlp.h"
+#include "pmlp_noise.h"
 
 namespace {
 
@@ -631,7 +632,11 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) dacc[i][r] = 0.f;
-            for (int i = wt; i < NP * 2 * MXC * ME; i += 256) (&XT[0][0][0])[i] = (mbf16)0.f;  // columns >= RL stay 0
+            // columns >= RL stay 0.  Only those: columns < RL are written by the step stores below
+            // from other waves, with no barrier between (a zero landing after one of them would
+            // drop that column of the first step's operand)
+            for (int i = wt; i < NP * 2 * MXC * ME; i += 256)
+                if ((i % (MXC * ME)) / ME >= RL) (&XT[0][0][0])[i] = (mbf16)0.f;
             xload(T - 1);
             for (int t = T - 1; t >= 0; --t) {
                 const int buf = t & 1;
@@ -901,17 +906,31 @@ __device__ __forceinline__ void stage_span(const float* __restrict__ src, int N,
     stage<UMAX, NT>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
 }
 
+// pmlp_heads_forward_act: the rollout's pmlp_act in the heads' launch (job 0 the actor, job 1
+// the critic): each actor workgroup samples its rows' actions from the mu tile still in LDS
+// (act_quad: pmlp_act's arithmetic, the same bits) and writes the storage rows; the critic's
+// workgroups write the values and privileged rows
+struct HeadAct {
+    const float *stdv, *obs, *cobs;
+    int O, CO, A;
+    const int64_t* draw;
+    uint64_t seed;
+    float *actions_out, *st_actions, *st_logp, *st_mu, *st_sigma, *st_value, *st_obs, *st_cobs;
+};
+
 // R rows per workgroup of NT threads, NT / R threads per row (each a share of the row's units;
 // every unit's and output's sum runs in the same order whatever the split: bitwise one result)
-template <int H, int R = HR, int NT = HT>
-__global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M) {
+template <int H, int R = HR, int NT = HT, bool ACT = false>
+__global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M, HeadAct ha = {}) {
     constexpr int PARTS = NT / R;
     static_assert(PARTS * R == NT && (PARTS == 2 || PARTS == 4), "2 or 4 threads per row");
     const HeadJob& J = jobs.j[blockIdx.y];
     const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * R;
     const int row = tid & (R - 1), half = tid / R;
     constexpr int LH = H + 4, LY = HN0 + 1, LO = HN1 + 1;
-    constexpr int HS = R * LH > R * (LY + LO) ? R * LH : R * (LY + LO);  // h tile, then y0 + out
+    // h tile, then y0 + out (+ the log-density terms [R][16] with ACT)
+    constexpr int HS0 = R * LH > R * (LY + LO) ? R * LH : R * (LY + LO);
+    constexpr int HS = ACT && HS0 < R * (LY + LO + 16) ? R * (LY + LO + 16) : HS0;
     __shared__ __attribute__((aligned(16))) float hs[HS];
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float bb0[HN0], w1[HN1 * HN0], bb1[HN1];
@@ -963,6 +982,45 @@ __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M) {
     for (int i = tid; i < R * N1; i += NT) {
         const int r = i / N1, c = i - r * N1;
         if (r0 + r < M) J.out[(size_t)(r0 + r) * N1 + c] = os[r * LO + c];
+    }
+    if constexpr (ACT) {
+        const int nrow = min(R, M - r0);
+        if (blockIdx.y == 0) {  // the actor: sampling, log-probability, the storage rows
+            float* terms = hs + R * (LY + LO);  // [R][16]
+            const uint32_t draw = (uint32_t)*ha.draw;
+            const uint2 key = make_uint2((uint32_t)ha.seed, (uint32_t)(ha.seed >> 32));
+            for (int q = tid; q < R * 4; q += NT) {
+                const int rl = q >> 2, c = q & 3, k0 = 4 * c;
+                if (rl >= nrow || k0 >= ha.A) continue;
+                const int i = r0 + rl;
+                float act[4], mu[4], sg[4], tm[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) mu[u] = k0 + u < ha.A ? os[rl * LO + k0 + u] : 0.f;
+                act_quad(draw, key, (uint32_t)i, c, ha.A, ha.stdv, mu, act, sg, tm);
+                const size_t o = (size_t)i * ha.A + k0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k0 + u < ha.A) {
+                        terms[rl * 16 + k0 + u] = tm[u];
+                        ha.actions_out[o + u] = act[u];
+                        ha.st_actions[o + u] = act[u];
+                        ha.st_mu[o + u] = mu[u];
+                        ha.st_sigma[o + u] = sg[u];
+                    }
+            }
+            __syncthreads();
+            if (tid < nrow) {
+                float logp = 0.f;
+                for (int k = 0; k < ha.A; ++k) logp += terms[tid * 16 + k];
+                ha.st_logp[r0 + tid] = logp;
+            }
+            for (int q = tid; q < nrow * ha.O; q += NT) ha.st_obs[(size_t)r0 * ha.O + q] = ha.obs[(size_t)r0 * ha.O + q];
+        } else {  // the critic: the values and the privileged rows
+            if (tid < nrow) ha.st_value[r0 + tid] = os[tid * LO];
+            if (ha.st_cobs)
+                for (int q = tid; q < nrow * ha.CO; q += NT)
+                    ha.st_cobs[(size_t)r0 * ha.CO + q] = ha.cobs[(size_t)r0 * ha.CO + q];
+        }
     }
 }
 
@@ -1290,6 +1348,28 @@ PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_
     else hipLaunchKernelGGL((k_heads_fwd<128, FR, FT>), g, dim3(FT), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward: ") + hipGetErrorString(e));
+}
+
+PMLP_API int pmlp_heads_forward_act(const pmlp_head_job* jobs, int32_t M, int32_t H, const pmlp_head_act* act,
+                                    void* stream) {
+    if (int e = heads_check("pmlp_heads_forward_act", 2, jobs, M, H, false)) return e;
+    if (!act || !act->stdv || !act->obs || !act->draw || !act->actions_out || !act->st_actions || !act->st_logp ||
+        !act->st_mu || !act->st_sigma || !act->st_value || !act->st_obs || act->O <= 0 || act->A <= 0 ||
+        act->A > 16 || act->A != jobs[0].N1 || jobs[1].N1 != 1 || (act->st_cobs && (!act->cobs || act->CO <= 0)))
+        return fail("pmlp_heads_forward_act: null buffer, A != the actor's N1 (<= 16) or a critic N1 != 1");
+    const HeadJobs hj = heads_pack(2, jobs);
+    const HeadAct ha{act->stdv, act->obs, act->cobs, act->O, act->CO, act->A, act->draw, act->seed,
+                     act->actions_out, act->st_actions, act->st_logp, act->st_mu, act->st_sigma, act->st_value,
+                     act->st_obs, act->st_cobs};
+    constexpr int FR = PMLP_HEADS_FWD_ROWS, FT = PMLP_HEADS_FWD_THREADS;
+    static_assert(FR * 4 <= FT * 4 && FR <= FT, "one (row, quad) item per thread pass");
+    const dim3 g((M + FR - 1) / FR, 2);
+    hipStream_t s = (hipStream_t)stream;
+    if (H == 32) hipLaunchKernelGGL((k_heads_fwd<32, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
+    else if (H == 64) hipLaunchKernelGGL((k_heads_fwd<64, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
+    else hipLaunchKernelGGL((k_heads_fwd<128, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward_act: ") + hipGetErrorString(e));
 }
 
 PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {

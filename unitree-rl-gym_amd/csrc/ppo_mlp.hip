@@ -27,6 +27,7 @@
 #include <string>
 
 #include "../../include/ppo_mlp.h"
+#include "pmlp_noise.h"
 
 typedef __bf16 bf16;
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1029,7 +1030,6 @@ struct LossArgs {
     float clip, vcoef, ecoef;
     __device__ size_t src(int i) const { return rows ? (size_t)rows[i] : (size_t)i; }
 };
-static constexpr float kHalfLog2Pi = 0.91893853320467274f;  // log(sqrt(2 pi))
 
 __device__ __forceinline__ float block_sum(float v, float* sh) {
 #pragma unroll
@@ -1689,19 +1689,7 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
     }
 }
 
-// Philox4x32-10 (the rollout's policy noise: k_act, k_act4 and the rollout forward)
-__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
-__device__ __forceinline__ float u01(uint32_t x) { return ((float)x + 0.5f) * 2.3283064365386963e-10f; }
+// (Philox4x32-10, the rollout's policy noise of k_act, k_act4 and the rollout forward: pmlp_noise.h)
 
 // ------------------------------------------------------------ fused MLP forward --
 // The whole forward of a 4-layer Linear/ELU MLP (rsl_rl's actor or critic: K0 -> H0 ->
@@ -2226,24 +2214,14 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)a.N * 4; base += nth) {
         const int64_t i = (base + threadIdx.x) >> 2;
         if (i < a.N && k0 < a.A) {
-            const uint4 r = philox4x32(make_uint4(draw, (uint32_t)i, (uint32_t)c, 0x5050u), key);
-            const float rad0 = sqrtf(-2.f * logf(u01(r.x))), rad1 = sqrtf(-2.f * logf(u01(r.z)));
-            float z[4];
-            sincospif(2.f * u01(r.y), &z[1], &z[0]);
-            sincospif(2.f * u01(r.w), &z[3], &z[2]);
-            z[0] *= rad0; z[1] *= rad0; z[2] *= rad1; z[3] *= rad1;
             const size_t o = (size_t)i * a.A + k0;
-            float act[4], mu[4], sg[4];
+            float act[4], mu[4], sg[4], tm[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int k = k0 + u;
-                if (k >= a.A) break;
-                sg[u] = a.stdv[k];
-                mu[u] = a.mu[o + u];
-                act[u] = mu[u] + sg[u] * z[u];
-                const float d = act[u] - mu[u];
-                terms[le][k] = -(d * d) / (2.f * sg[u] * sg[u]) - logf(sg[u]) - kHalfLog2Pi;
-            }
+            for (int u = 0; u < 4; ++u) mu[u] = k0 + u < a.A ? a.mu[o + u] : 0.f;
+            act_quad(draw, key, (uint32_t)i, c, a.A, a.stdv, mu, act, sg, tm);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u < a.A) terms[le][k0 + u] = tm[u];
             if (vec) {
                 const float4 av = make_float4(act[0], act[1], act[2], act[3]);
                 *(float4*)(a.actions_out + o) = av;

@@ -540,6 +540,8 @@ class RecurrentRollout:
         rf = alg._rfused
         self.mfma_step = rf is not None and all(rf.mfma)
         self.heads = None
+        # pmlp_act inside the heads' launch where the shapes allow (PMLP_HEADS_ACT=0: two launches)
+        self.fuse_act = os.environ.get("PMLP_HEADS_ACT", "1") != "0"
         if fused_recurrent.supported(ac, self.N, 1) and ac.memory_a.rnn.hidden_size == ac.memory_c.rnn.hidden_size:
             dev = ac.std.device
             self.heads = [ac.actor, ac.critic]
@@ -585,20 +587,29 @@ class RecurrentRollout:
         else:
             storage._save_hidden_states(ac.get_hidden_states())
             ha, hc = ma(obs), mc(cobs)
+        A = self.actions.shape[1]
+        priv = storage.privileged_observations
+        P = mm._p
         if self.heads is not None and ha.is_contiguous() and hc.is_contiguous():
-            P = mm._p
             jobs = (mm.HeadJob * 2)(*[mm.HeadJob(P(h), P(s[0].weight), P(s[0].bias), P(s[2].weight), P(s[2].bias),
                                                  P(self.y0[n]), P(self.out[n]), None, None, None, s[0].out_features,
                                                  s[2].out_features)
                                       for n, (h, s) in enumerate(zip((ha, hc), self.heads))])
+            if self.fuse_act and A <= 16 and self.heads[1][2].out_features == 1:
+                # the sampling and the storage rows in the heads' launch (pmlp_heads_forward_act)
+                act = mm.HeadAct(P(ac.std.detach()), P(obs), P(cobs) if priv is not None else None, obs.shape[1],
+                                 cobs.shape[1] if priv is not None else 0, A, P(self.draw), self.seed,
+                                 P(self.actions), P(storage.actions[t]), P(storage.actions_log_prob[t]),
+                                 P(storage.mu[t]), P(storage.sigma[t]), P(storage.values[t]),
+                                 P(storage.observations[t]), P(priv[t]) if priv is not None else None)
+                mm._ok(mm.load().pmlp_heads_forward_act(jobs, self.N, H, C.byref(act), mm._stream()),
+                       "pmlp_heads_forward_act")
+                return self.actions
             mm._ok(mm.load().pmlp_heads_forward(2, jobs, self.N, H, mm._stream()), "pmlp_heads_forward")
             mu, value = self.out
         else:
             mu = ac.actor(ha.squeeze(0)).contiguous()
             value = ac.critic(hc.squeeze(0)).contiguous()
-        A = self.actions.shape[1]
-        priv = storage.privileged_observations
-        P = mm._p
         mm._ok(mm.load().pmlp_act(P(mu), P(ac.std.detach()), P(value), P(obs), P(cobs) if priv is not None else None,
                                   self.N, A, obs.shape[1], cobs.shape[1] if priv is not None else 0, P(self.draw),
                                   self.seed, P(self.actions), P(storage.actions[t]), P(storage.actions_log_prob[t]),

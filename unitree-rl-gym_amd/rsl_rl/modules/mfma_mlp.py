@@ -101,6 +101,15 @@ class HeadJob(C.Structure):
                 ("slab", C.c_void_p), ("N0", C.c_int32), ("N1", C.c_int32)]
 
 
+class HeadAct(C.Structure):
+    """include/ppo_mlp.h pmlp_head_act (pmlp_heads_forward_act)."""
+    _fields_ = [("stdv", C.c_void_p), ("obs", C.c_void_p), ("cobs", C.c_void_p), ("O", C.c_int32),
+                ("CO", C.c_int32), ("A", C.c_int32), ("draw", C.c_void_p), ("seed", C.c_uint64),
+                ("actions_out", C.c_void_p), ("st_actions", C.c_void_p), ("st_logp", C.c_void_p),
+                ("st_mu", C.c_void_p), ("st_sigma", C.c_void_p), ("st_value", C.c_void_p), ("st_obs", C.c_void_p),
+                ("st_cobs", C.c_void_p)]
+
+
 MAX_JOBS, MAX_GEMM_JOBS = 16, 4
 PMLP_MAX_MIRROR = 8  # include/ppo_mlp.h: bf16 weight copies one Adam launch writes
 
@@ -162,6 +171,7 @@ def load():
         L.pmlp_heads_blocks.restype = i32
         L.pmlp_heads_forward.argtypes = [i32, C.POINTER(HeadJob), i32, i32, vp]
         L.pmlp_heads_backward.argtypes = [i32, C.POINTER(HeadJob), i32, i32, vp]
+        L.pmlp_heads_forward_act.argtypes = [C.POINTER(HeadJob), i32, i32, C.POINTER(HeadAct), vp]
         _lib = L
     return _lib
 
