@@ -1,5 +1,6 @@
-"""Run-to-run stability of the captured recurrent PPO update (H1 x 8192 by default: 5 epochs x 4
-mini-batches of the fused recurrent step): after two learning iterations, the update graph is
+"""Run-to-run stability of the captured PPO update (H1 x 8192 by default: 5 epochs x 4
+mini-batches of the fused recurrent step; ROLL_TASK=go2 ROLL_ENVS=4096: the fused MLP step): after
+two learning iterations, the update graph is
 replayed N times from the same state (parameters, Adam moments and step, learning rate,
 advantages restored before each replay), counting the replays whose parameters differ from the
 first replay's.  None of the update's kernels uses atomics, so any difference is a race.
@@ -22,10 +23,15 @@ env, _ = task_registry.make_env(name=TASK, args=args)
 r, _ = task_registry.make_alg_runner(env=env, name=TASK, args=args, log_root=None)
 r.learn(2)  # the second iteration captures the update graph
 alg = r.alg
-rf, graph = alg._rfused, alg._rgraph
-assert rf is not None and graph is not None, "the fused recurrent update did not capture"
 st = alg.storage
-state = [rf.flat, rf.exp_avg, rf.exp_avg_sq, rf.step_t, alg._lr, st.advantages, st.returns]
+if alg._rfused is not None:  # recurrent policies
+    rf, graph = alg._rfused, alg._rgraph
+    extra = []
+else:  # the MLP step: also its bf16 weight copies (the Adam mirror rewrites them)
+    rf, graph = alg._fused, alg._fgraph
+    extra = [w for ws in rf.wb for w in ws] + ([w for ws in rf.wf for w in ws] if rf.wf else [])
+assert rf is not None and graph is not None, "the fused update did not capture"
+state = [rf.flat, rf.exp_avg, rf.exp_avg_sq, rf.step_t, alg._lr, st.advantages, st.returns] + extra
 snap = [t.clone() for t in state]
 
 
