@@ -1651,15 +1651,37 @@ struct MirrorJobs {
     bf16* frag[PMLP_MAX_MIRROR];
     int n;
 };
+// One element of torch.optim.Adam after clip_grad_norm_ (coef = clip factor x grad scale):
+// updates m, v and returns the new parameter.  The fused multiply-adds are explicit: left to
+// contraction, the scalar and the packed (vectorised) forms fused different pairs and the
+// kernels disagreed in the last bit.  Shared by k_adam and k_adam_vec.
+__device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float b1, float b2,
+                                           float eps, float step_size, float bc2s) {
+    const float gi = g * coef;
+    m = __builtin_fmaf(1.f - b1, gi - m, m);
+    v = __builtin_fmaf(v, b2, ((1.f - b2) * gi) * gi);
+    return __builtin_fmaf(-step_size, m / (sqrtf(v) / bc2s + eps), p);
+}
+// the grad-norm partials' sum, in the order of k_adam's first form (thread t adds t, t + 256, ...
+// in turn, then block_sum); unrolled so that a thread's loads are in flight together
+__device__ __forceinline__ float norm_partials_sum(const float* __restrict__ partial, int nparts, float* sh) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < nparts; i += PMLP_OPT_THREADS) s += partial[i];
+    return block_sum(s, sh);
+}
+// index of the fragment-packed copy's element (r, c) of a weight with row stride ld
+// (include/ppo_mlp.h pmlp_mirror_job.frag)
+__device__ __forceinline__ size_t frag_index(int r, int c, int ld) {
+    return ((((size_t)(r >> 5) * (ld >> 4) + (c >> 4)) * 64 + (r & 31) + 32 * ((c >> 3) & 1)) << 3) + (c & 7);
+}
 __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p, const float* __restrict__ g,
                                                            float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                            float scale, const float* __restrict__ partial, int nparts,
                                                            const float* step, const float* lr, float max_norm,
                                                            float b1, float b2, float eps, MirrorJobs mj) {
     __shared__ float sh[4];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < nparts; i += PMLP_OPT_THREADS) s += partial[i];
-    s = block_sum(s, sh);
+    const float s = norm_partials_sum(partial, nparts, sh);
     float coef = scale;
     if (max_norm > 0.f) coef = scale * fminf(max_norm / (sqrtf(s) + 1e-6f), 1.f);  // clip_grad_norm_
     const float t = step[0];
@@ -1667,12 +1689,10 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
     const float step_size = lr[0] / bc1;
     for (int64_t i = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * PMLP_OPT_THREADS) {
-        const float gi = g[i] * coef;
-        const float mi = m[i] + (1.f - b1) * (gi - m[i]);
-        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        float mi = m[i], vi = v[i];
+        const float pi = adam_elem(g[i], mi, vi, p[i], coef, b1, b2, eps, step_size, bc2s);
         m[i] = mi;
         v[i] = vi;
-        const float pi = p[i] - step_size * (mi / (sqrtf(vi) / bc2s + eps));
         p[i] = pi;
         for (int j = 0; j < mj.n; ++j) {  // the bf16 GEMM operand copy of a weight
             const int64_t o = i - mj.off[j];
@@ -1681,11 +1701,78 @@ __global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam(float* __restrict__ p
                 // VALU sequence per element)
                 const int oi = (int)o, r = oi / mj.cols[j], c = oi - r * mj.cols[j];
                 mj.dst[j][(size_t)r * mj.ld[j] + c] = (bf16)pi;
-                if (mj.frag[j])  // the fragment-packed copy (include/ppo_mlp.h)
-                    mj.frag[j][((((size_t)(r >> 5) * (mj.ld[j] >> 4) + (c >> 4)) * 64 + (r & 31) + 32 * ((c >> 3) & 1))
-                                << 3) + (c & 7)] = (bf16)pi;
+                if (mj.frag[j]) mj.frag[j][frag_index(r, c, mj.ld[j])] = (bf16)pi;  // the fragment-packed copy
             }
         }
+    }
+}
+
+// k_adam over VEC consecutive elements per thread (VEC = 2 or 4), one group per thread at the
+// host's grid: the thread's loads are issued before the norm partials are summed (one round
+// trip, not two in a row), one mirror-job lookup per group, and the bf16 copies stored VEC at
+// a time.  The host checks the layout it relies on: 4 VEC-byte aligned flat buffers, every
+// mirrored weight's offset, width and row stride multiples of VEC.  Per element the arithmetic
+// of k_adam (adam_elem, same partial-sum order): the same bits.
+template <int VEC>
+__global__ __launch_bounds__(PMLP_OPT_THREADS) void k_adam_vec(float* __restrict__ p, const float* __restrict__ g,
+                                                               float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                               float scale, const float* __restrict__ partial, int nparts,
+                                                               const float* step, const float* lr, float max_norm,
+                                                               float b1, float b2, float eps, MirrorJobs mj) {
+    typedef float vf __attribute__((ext_vector_type(VEC)));
+    typedef bf16 vb __attribute__((ext_vector_type(VEC)));
+    __shared__ float sh[4];
+    const int64_t ng = n / VEC, i0 = (int64_t)blockIdx.x * PMLP_OPT_THREADS + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * PMLP_OPT_THREADS;
+    vf G, M, V, P;
+    if (i0 < ng) {
+        G = ((const vf*)g)[i0];
+        M = ((const vf*)m)[i0];
+        V = ((const vf*)v)[i0];
+        P = ((const vf*)p)[i0];
+    }
+    const float s = norm_partials_sum(partial, nparts, sh);
+    float coef = scale;
+    if (max_norm > 0.f) coef = scale * fminf(max_norm / (sqrtf(s) + 1e-6f), 1.f);  // clip_grad_norm_
+    const float t = step[0];
+    const float bc1 = 1.f - powf(b1, t), bc2s = sqrtf(1.f - powf(b2, t));
+    const float step_size = lr[0] / bc1;
+    for (int64_t i = i0; i < ng; i += stride) {
+        if (i != i0) {
+            G = ((const vf*)g)[i];
+            M = ((const vf*)m)[i];
+            V = ((const vf*)v)[i];
+            P = ((const vf*)p)[i];
+        }
+        vb B;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            float me = M[e], ve = V[e];
+            P[e] = adam_elem(G[e], me, ve, P[e], coef, b1, b2, eps, step_size, bc2s);
+            M[e] = me;
+            V[e] = ve;
+            B[e] = (bf16)P[e];
+        }
+        ((vf*)m)[i] = M;
+        ((vf*)v)[i] = V;
+        ((vf*)p)[i] = P;
+        const int64_t e0 = i * VEC;
+        for (int j = 0; j < mj.n; ++j) {
+            const int64_t o = e0 - mj.off[j];
+            if (o >= 0 && o < (int64_t)mj.rows[j] * mj.cols[j]) {  // the whole group: one row of weight j
+                const int oi = (int)o, r = oi / mj.cols[j], c = oi - r * mj.cols[j];
+                *(vb*)(mj.dst[j] + (size_t)r * mj.ld[j] + c) = B;
+                if (mj.frag[j]) *(vb*)(mj.frag[j] + frag_index(r, c, mj.ld[j])) = B;  // c % 8 + VEC <= 8
+            }
+        }
+    }
+    // the last n % VEC elements (no weight: a mirrored weight ends on a multiple of VEC)
+    if (blockIdx.x == 0 && threadIdx.x < n - ng * VEC) {
+        const int64_t i = ng * VEC + threadIdx.x;
+        float mi = m[i], vi = v[i];
+        p[i] = adam_elem(g[i], mi, vi, p[i], coef, b1, b2, eps, step_size, bc2s);
+        m[i] = mi;
+        v[i] = vi;
     }
 }
 
@@ -2741,6 +2828,37 @@ PMLP_API int pmlp_adam_mirror_n(float* param, const float* grad, float* exp_avg,
             return fail(-1, "pmlp_adam_mirror: bad mirror job " + std::to_string(j));
         mj.off[j] = J.offset; mj.rows[j] = J.rows; mj.cols[j] = J.cols; mj.ld[j] = J.ld; mj.dst[j] = (bf16*)J.dst;
         mj.frag[j] = (bf16*)J.frag;
+    }
+    // VEC consecutive elements per thread where the layout allows (k_adam_vec; PMLP_ADAM_VEC =
+    // 1, 2 or 4, default 4)
+    static const int vec_env = [] {
+        const char* e = getenv("PMLP_ADAM_VEC");
+        const int v = e ? atoi(e) : 4;
+        return v == 1 || v == 2 ? v : 4;
+    }();
+    int vec = vec_env;
+    auto aligned = [](const void* q, int bytes) { return ((uintptr_t)q % bytes) == 0; };
+    for (; vec > 1; vec /= 2) {
+        bool ok = aligned(param, 4 * vec) && aligned(grad, 4 * vec) && aligned(exp_avg, 4 * vec) &&
+                  aligned(exp_avg_sq, 4 * vec);
+        for (int j = 0; j < nmirror && ok; ++j)
+            ok = mj.off[j] % vec == 0 && mj.cols[j] % vec == 0 && mj.ld[j] % vec == 0 && aligned(mj.dst[j], 2 * vec) &&
+                 (!mj.frag[j] || aligned(mj.frag[j], 2 * vec));
+        if (ok) break;
+    }
+    if (vec > 1) {
+        const int64_t groups = n / vec;
+        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (groups + PMLP_OPT_THREADS - 1) / PMLP_OPT_THREADS));
+        if (vec == 4)
+            hipLaunchKernelGGL(k_adam_vec<4>, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad,
+                               exp_avg, exp_avg_sq, n, grad_scale, partial, nparts, step, lr, max_norm, beta1, beta2,
+                               eps, mj);
+        else
+            hipLaunchKernelGGL(k_adam_vec<2>, dim3(blocks), dim3(PMLP_OPT_THREADS), 0, (hipStream_t)stream, param, grad,
+                               exp_avg, exp_avg_sq, n, grad_scale, partial, nparts, step, lr, max_norm, beta1, beta2,
+                               eps, mj);
+        PMLP_CHECK_LAUNCH("pmlp_adam_mirror");
+        return 0;
     }
     // grid cap 1024 blocks: for the Go2 parameters (1,486 blocks at one element per thread)
     // uncapped / 1024 / 512 / 256 measured 9.2-9.5 / 7.5-8.1 / 8.5-10.0 / 12.1-12.7 us
