@@ -353,15 +353,17 @@ def test_hip_lstm_matches_pretrained_policy_golden(robot):
             torch.testing.assert_close(mu[:, r], want, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("M", [1000, 20003])
 @pytest.mark.parametrize("H", [32, 64, 128])
-def test_fused_recurrent_heads_match_torch(H):
+def test_fused_recurrent_heads_match_torch(H, M):
     """pmlp_heads_forward / pmlp_heads_backward (the fused recurrent step's MLP heads, fp32) vs
     torch autograd of Sequential(Linear(H, 32), ELU, Linear(32, N1)) for the actor (N1 = 12)
-    and the critic (N1 = 1) in one launch each, on a row count that is not a multiple of the
-    128-row blocks; the per-block weight-gradient partials summed by pmlp_reduce_slabs."""
+    and the critic (N1 = 1) in one launch each, on row counts that are not a multiple of the
+    64- or 128-row blocks (20,003: the forward's matrix-core form, from 16,384 rows); the
+    per-block weight-gradient partials summed by pmlp_reduce_slabs."""
     from rsl_rl.modules import mfma_mlp as mm
     torch.manual_seed(H)
-    M, N0 = 1000, 32
+    N0 = 32
     nets = [torch.nn.Sequential(torch.nn.Linear(H, N0), torch.nn.ELU(), torch.nn.Linear(N0, n1)).cuda()
             for n1 in (12, 1)]
     hs = [torch.randn(M, H, device="cuda") for _ in range(2)]
@@ -391,8 +393,16 @@ def test_fused_recurrent_heads_match_torch(H):
         params = [net[0].weight, net[0].bias, net[2].weight, net[2].bias]
         g = torch.autograd.grad(out, [h] + params, douts[n])
         torch.testing.assert_close(bufs[n]["dh"], g[0], rtol=1e-5, atol=1e-5)
-        want = torch.cat([t.reshape(-1) for t in g[1:]])
-        torch.testing.assert_close(bufs[n]["grad"], want, rtol=1e-4, atol=1e-4)
+        # the weight gradients are fp32 sums over the M rows, in another order than any fp32
+        # reference's: against fp64, with an absolute tolerance growing as sqrt(M) (1e-4 at
+        # M = 1000; measured 2.2e-4 against torch's fp32 GEMM at M = 20,003)
+        net64 = copy.deepcopy(net).double()
+        h64 = hs[n].double().requires_grad_(True)
+        out64 = net64[2](torch.nn.functional.elu(net64[0](h64)))
+        g64 = torch.autograd.grad(out64, [net64[0].weight, net64[0].bias, net64[2].weight, net64[2].bias],
+                                  douts[n].double())
+        want = torch.cat([t.reshape(-1) for t in g64]).float()
+        torch.testing.assert_close(bufs[n]["grad"], want, rtol=1e-4, atol=1e-4 * max(1.0, M / 1000) ** 0.5)
 
 
 @pytest.mark.parametrize("I", [41, 47, 17, 63])
@@ -569,3 +579,22 @@ def test_recurrent_heads_with_fused_sampling_are_bitwise_the_separate_launches()
     for k in ("actions", "actions_log_prob", "mu", "sigma", "values", "observations", "privileged_observations",
               "rewards", "dones"):
         assert torch.equal(getattr(sa, k), getattr(sb, k)), k
+
+
+def test_recurrent_heads_matrix_core_form_is_bitwise_the_valu_form():
+    """The heads' products on the matrix cores (default) against the VALU form
+    (PMLP_HEADS_MFMA=0, read once per process: two probe processes), y0, out, dh and the
+    weight-gradient slabs digested, on 20,003 rows (the forward's matrix-core form, ragged
+    last tiles).  Each f32 MFMA chain keeps the VALU form's fma order (lstm_seq.hip)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    digests = []
+    for flag in ("1", "0"):
+        env = dict(os.environ, PMLP_HEADS_MFMA=flag)
+        out = subprocess.run([sys.executable, os.path.join(root, "tools", "probes", "heads_time.py"), "20003"],
+                             env=env, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr[-2000:]
+        digests.append(out.stdout.strip().rsplit("outputs ", 1)[1])
+    assert digests[0] == digests[1]

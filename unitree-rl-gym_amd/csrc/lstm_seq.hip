@@ -906,6 +906,58 @@ __device__ __forceinline__ void stage_span(const float* __restrict__ src, int N,
     stage<UMAX, NT>(src + (size_t)r0 * N, nr * N, [&](int i, float v) { t[(i / N) * L + i % N] = v; });
 }
 
+// The same three stagings split into a load phase (registers) and a store phase (LDS), so a
+// kernel issues every tile's loads before its first LDS store: one round trip for all of them
+// instead of one per tile (each store phase ends a basic block the next loads cannot rise above).
+template <int U, int NT>
+__device__ __forceinline__ void flat_load(const float* __restrict__ src, int n, float (&v)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min((int)threadIdx.x + u * NT, n - 1)];
+}
+template <int U, int NT, typename F>
+__device__ __forceinline__ void flat_store(int n, const float (&v)[U], F&& put) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * NT;
+        if (i < n) put(i, v[u]);
+    }
+}
+template <int H, int R, int NT>
+__device__ __forceinline__ void rows_load(const float* __restrict__ h, int r0, int M, float4 (&v)[R * H / 4 / NT]) {
+    constexpr int U = R * H / 4 / NT;
+    static_assert(U >= 1 && R * H / 4 == U * NT, "whole float4 loads per thread");
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * NT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        v[u] = *(const float4*)(h + (size_t)min(r0 + r, M - 1) * H + c);
+    }
+}
+template <int H, int LH, int R, int NT>
+__device__ __forceinline__ void rows_store(int r0, int M, const float4 (&v)[R * H / 4 / NT], float* hs) {
+#pragma unroll
+    for (int u = 0; u < R * H / 4 / NT; ++u) {
+        const int i = threadIdx.x + u * NT, r = i / (H / 4), c = (i % (H / 4)) * 4;
+        *(float4*)(hs + r * LH + c) = r0 + r < M ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+// stage_span's tile: UMAX * NT >= R * N, every (row, column < N) entry written once (0 past M)
+template <int UMAX, int R, int NT>
+__device__ __forceinline__ void span_load(const float* __restrict__ src, int N, int r0, int M, float (&v)[UMAX]) {
+    const int n = min(R, M - r0) * N;
+    const float* s = src + (size_t)r0 * N;
+#pragma unroll
+    for (int u = 0; u < UMAX; ++u) v[u] = s[min((int)threadIdx.x + u * NT, n - 1)];
+}
+template <int UMAX, int L, int R, int NT>
+__device__ __forceinline__ void span_store(int N, int r0, int M, const float (&v)[UMAX], float* t) {
+    const int n = min(R, M - r0) * N;
+#pragma unroll
+    for (int u = 0; u < UMAX; ++u) {
+        const int i = threadIdx.x + u * NT;
+        if (i < R * N) t[(i / N) * L + i % N] = i < n ? v[u] : 0.f;
+    }
+}
+
 // pmlp_heads_forward_act: the rollout's pmlp_act in the heads' launch (job 0 the actor, job 1
 // the critic): each actor workgroup samples its rows' actions from the mu tile still in LDS
 // (act_quad: pmlp_act's arithmetic, the same bits) and writes the storage rows; the critic's
@@ -920,10 +972,12 @@ struct HeadAct {
 
 // R rows per workgroup of NT threads, NT / R threads per row (each a share of the row's units;
 // every unit's and output's sum runs in the same order whatever the split: bitwise one result)
-template <int H, int R = HR, int NT = HT, bool ACT = false>
+// MF: y0 on the matrix cores (NT = 2 R, wave w owns rows 32w .. 32w + 31; see below)
+template <int H, int R = HR, int NT = HT, bool ACT = false, bool MF = false>
 __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M, HeadAct ha = {}) {
     constexpr int PARTS = NT / R;
     static_assert(PARTS * R == NT && (PARTS == 2 || PARTS == 4), "2 or 4 threads per row");
+    static_assert(!MF || (NT == 2 * R && R % 32 == 0 && H % 8 == 0), "MF: one 32-row tile per wave");
     const HeadJob& J = jobs.j[blockIdx.y];
     const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * R;
     const int row = tid & (R - 1), half = tid / R;
@@ -934,32 +988,86 @@ __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M, HeadAct 
     __shared__ __attribute__((aligned(16))) float hs[HS];
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float bb0[HN0], w1[HN1 * HN0], bb1[HN1];
-    stage<HN0 * H / NT, NT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
-    stage<(HN1 * HN0 + NT - 1) / NT, NT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
-    if (tid < N0) bb0[tid] = J.b0[tid];
-    if (tid < N1) bb1[tid] = J.b1[tid];
-    stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
-    __syncthreads();
-    float hr[H];
+    // MF: the lane's W0 operands straight into registers (W0 [N0, H] is L2-resident; from LDS at
+    // a row stride of H floats every lane would read the same banks), in flight with the staging
+    float4 wf[MF ? H / 8 : 1];
+    if constexpr (MF) {
+        const int lane = tid & 63;
+        const float* wrow = J.W0 + min(lane & 31, N0 - 1) * H + 4 * (lane >> 5);  // (units past N0: discarded)
 #pragma unroll
-    for (int k = 0; k < H; k += 4) {
-        const float4 v = *(const float4*)(hs + row * LH + k);
-        hr[k] = v.x; hr[k + 1] = v.y; hr[k + 2] = v.z; hr[k + 3] = v.w;
+        for (int s = 0; s < H / 8; ++s) wf[s] = *(const float4*)(wrow + 8 * s);
     }
-    __syncthreads();  // (hs is reused for the y0 tile below)
-    // y0: this thread's share of the units, one at a time (four FMA chains over k mod 4)
-    const int nh = N0 / PARTS, jb = half * nh;
-#pragma unroll 1
-    for (int j = jb; j < jb + nh; ++j) {
-        float z[4] = {bb0[j], 0.f, 0.f, 0.f};
+    {  // every tile's loads, then every LDS store
+        constexpr int UW0 = MF ? 1 : HN0 * H / NT, UW1 = (HN1 * HN0 + NT - 1) / NT;
+        float vw0[UW0], vw1[UW1];
+        float4 vh[R * H / 4 / NT];
+        if constexpr (!MF) flat_load<UW0, NT>(J.W0, N0 * H, vw0);
+        flat_load<UW1, NT>(J.W1, N1 * N0, vw1);
+        rows_load<H, R, NT>(J.h, r0, M, vh);
+        const float b0v = J.b0[min(tid, N0 - 1)], b1v = J.b1[min(tid, N1 - 1)];
+        if constexpr (!MF) flat_store<UW0, NT>(N0 * H, vw0, [&](int i, float v) { w0[i] = v; });
+        flat_store<UW1, NT>(N1 * N0, vw1, [&](int i, float v) { w1[i] = v; });
+        if (tid < N0) bb0[tid] = b0v;
+        if (tid < N1) bb1[tid] = b1v;
+        rows_store<H, LH, R, NT>(r0, M, vh, hs);
+    }
+    __syncthreads();
+    if constexpr (MF) {
+        // y0 on the matrix cores: wave w, rows 32w .. 32w + 31, all 32 units (one
+        // v_mfma_f32_32x32x2_f32 tile; lane l: A = h[row l & 31][k], B = W0[unit l & 31][k] for
+        // its k slot l >> 5).  Accumulator u takes k = u, u + 4, u + 8, ...: step s's
+        // instruction holds k = u + 8s (slot 0) and u + 8s + 4 (slot 1), and an f32 MFMA is a
+        // k-ordered fmaf chain -- the VALU form's four chains over k mod 4 with the bias at the
+        // start of chain 0, and the same (z0 + z1) + (z2 + z3): the same bits.
+        const int lane = tid & 63, w = tid >> 6, q = lane >> 5, jc = lane & 31;
+        const float bj = jc < N0 ? bb0[jc] : 0.f;
+        mfloatx16 acc[4];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            acc[0][r] = bj;
+            acc[1][r] = acc[2][r] = acc[3][r] = 0.f;
+        }
+        const float* hrow = hs + (32 * w + jc) * LH + 4 * q;
+#pragma unroll
+        for (int s = 0; s < H / 8; ++s) {
+            const float4 hv = *(const float4*)(hrow + 8 * s);
+            const float4 wv = wf[s];
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv.x, wv.x, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv.y, wv.y, acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv.z, wv.z, acc[2], 0, 0, 0);
+            acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv.w, wv.w, acc[3], 0, 0, 0);
+        }
+        __syncthreads();  // every read of the h tile is done (hs takes y0)
+        if (jc < N0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rr = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * q;
+                const float zz = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+                hs[rr * LY + jc] = zz > 0.f ? zz : expm1f(zz);
+            }
+        }
+    } else {
+        float hr[H];
 #pragma unroll
         for (int k = 0; k < H; k += 4) {
-            const float4 w = *(const float4*)(w0 + j * H + k);
-            z[0] = fmaf(w.x, hr[k], z[0]); z[1] = fmaf(w.y, hr[k + 1], z[1]);
-            z[2] = fmaf(w.z, hr[k + 2], z[2]); z[3] = fmaf(w.w, hr[k + 3], z[3]);
+            const float4 v = *(const float4*)(hs + row * LH + k);
+            hr[k] = v.x; hr[k + 1] = v.y; hr[k + 2] = v.z; hr[k + 3] = v.w;
         }
-        const float zz = (z[0] + z[1]) + (z[2] + z[3]);
-        hs[row * LY + j] = zz > 0.f ? zz : expm1f(zz);
+        __syncthreads();  // (hs is reused for the y0 tile below)
+        // y0: this thread's share of the units, one at a time (four FMA chains over k mod 4)
+        const int nh = N0 / PARTS, jb = half * nh;
+#pragma unroll 1
+        for (int j = jb; j < jb + nh; ++j) {
+            float z[4] = {bb0[j], 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < H; k += 4) {
+                const float4 w = *(const float4*)(w0 + j * H + k);
+                z[0] = fmaf(w.x, hr[k], z[0]); z[1] = fmaf(w.y, hr[k + 1], z[1]);
+                z[2] = fmaf(w.z, hr[k + 2], z[2]); z[3] = fmaf(w.w, hr[k + 3], z[3]);
+            }
+            const float zz = (z[0] + z[1]) + (z[2] + z[3]);
+            hs[row * LY + j] = zz > 0.f ? zz : expm1f(zz);
+        }
     }
     __syncthreads();
     // out: this thread's outputs i = half, half + PARTS, ... over the row's y0 (LDS)
@@ -1026,7 +1134,8 @@ __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M, HeadAct 
 
 // R rows per workgroup of 2 R threads (the weight-gradient partial sums run over R-row halves:
 // R sets the slab rows, pmlp_heads_blocks)
-template <int H, int R = HR>
+// MF: dW0 and dh on the matrix cores (see below)
+template <int H, int R = HR, bool MF = false>
 __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
     constexpr int NT = 2 * R;
     const HeadJob& J = jobs.j[blockIdx.y];
@@ -1038,11 +1147,22 @@ __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
     __shared__ float ds[R * LO];                                 // dout
     __shared__ __attribute__((aligned(16))) float w0[HN0 * H];
     __shared__ float w1[HN1 * HN0];
-    stage<HN0 * H / NT, NT>(J.W0, N0 * H, [&](int i, float v) { w0[i] = v; });
-    stage<(HN1 * HN0 + NT - 1) / NT, NT>(J.W1, N1 * N0, [&](int i, float v) { w1[i] = v; });
-    stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
-    stage_span<(R * HN0 + NT - 1) / NT, LZ, R, NT>(J.y0, N0, r0, M, zs);
-    stage_span<(R * HN1 + NT - 1) / NT, LO, R, NT>(J.dout, N1, r0, M, ds);
+    {  // every tile's loads, then every LDS store
+        constexpr int UW0 = HN0 * H / NT, UW1 = (HN1 * HN0 + NT - 1) / NT;
+        constexpr int UY = (R * HN0 + NT - 1) / NT, UD = (R * HN1 + NT - 1) / NT;
+        float vw0[UW0], vw1[UW1], vy[UY], vd[UD];
+        float4 vh[R * H / 4 / NT];
+        flat_load<UW0, NT>(J.W0, N0 * H, vw0);
+        flat_load<UW1, NT>(J.W1, N1 * N0, vw1);
+        rows_load<H, R, NT>(J.h, r0, M, vh);
+        span_load<UY, R, NT>(J.y0, N0, r0, M, vy);
+        span_load<UD, R, NT>(J.dout, N1, r0, M, vd);
+        flat_store<UW0, NT>(N0 * H, vw0, [&](int i, float v) { w0[i] = v; });
+        flat_store<UW1, NT>(N1 * N0, vw1, [&](int i, float v) { w1[i] = v; });
+        rows_store<H, LH, R, NT>(r0, M, vh, hs);
+        span_store<UY, LZ, R, NT>(N0, r0, M, vy, zs);
+        span_store<UD, LO, R, NT>(N1, r0, M, vd, ds);
+    }
     __syncthreads();
     float* sl = J.slab + (size_t)blockIdx.x * (N0 * H + N0 + N1 * N0 + N1);
     // dW1 (+ db1 on j = 0) from the y0 and dout tiles, before y0 is overwritten
@@ -1081,78 +1201,168 @@ __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
     for (int u = 0; u < HN0 / 2; ++u)
         if (u < nh) zs[row * LZ + jb + u] = dz[u];
     __syncthreads();
-    // dW0 (+ db0 on k0 = 0): 4 x 4 tiles, each over one half of the rows; the second half's
-    // partial goes through LDS (over the h tile) and the first adds it (fixed order)
-    const int ntile = (N0 / 4) * (H / 4);  // one tile per thread pair and pass
-    float* part = hs;  // [R][20]: the h tile, after its last read (dh overwrites it later)
-    static_assert(R * 20 <= R * LH, "dW0 partials fit the h tile");
-    for (int tb = 0; tb < ntile; tb += R) {
-        float a[4][4] = {}, bs[4] = {};
-        const int t = tb + row, j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
-        if (t < ntile) {
-            const int rb = half * (R / 2);
-#pragma unroll 4
-            for (int r = rb; r < rb + R / 2; ++r) {
-                const float4 z4 = *(const float4*)(zs + r * LZ + j0);
-                const float4 h4 = *(const float4*)(hs + r * LH + k0);
-                const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
+    if constexpr (MF) {
+        // dW0 and dh as v_mfma_f32_32x32x2_f32 tiles: an f32 MFMA is a k-ordered fmaf chain, and
+        // each chain below keeps the VALU form's order, so the bits are the same.
+        //   dW0 [j][k], per half of the rows: A[j][slot] = dz[r][j], B[slot][k] = h[r][k], step s
+        //   holding rows rb + 2s, rb + 2s + 1.  Item c = (k tile c % KT, half c / KT); wave w
+        //   takes items w, w + NW, ..  The second half's tile goes through LDS and the first adds
+        //   it, as db0's two halves (VALU) do.
+        //   dh [row][k]: A[row][slot] = dz[row][j], B[slot][k] = W0[j][k], step s holding
+        //   j = 2s, 2s + 1 (j < N0).
+        constexpr int KT = H / 32, NW = NT / 64, NI = 2 * KT, IPW = (NI + NW - 1) / NW;
+        constexpr int DT = (R / 32) * KT, DPW = (DT + NW - 1) / NW;
+        static_assert(H % 32 == 0 && R % 64 == 0, "MF: 32 x 32 tiles, two row halves of whole steps");
+        static_assert(KT * 1024 + HN0 <= R * LH, "the second halves' partials fit the h tile");
+        const int lane = tid & 63, w = tid >> 6, q = lane >> 5, l32 = lane & 31;
+        mfloatx16 dw[IPW];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    bs[u] += zz[u];
+        for (int it = 0; it < IPW; ++it) {
+            const int c = w + it * NW;
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) a[u][v] = fmaf(zz[u], hh[v], a[u][v]);
+            for (int r = 0; r < 16; ++r) dw[it][r] = 0.f;
+            if (c < NI) {  // (wave-uniform)
+                const int kt = c % KT, rb = (c / KT) * (R / 2);
+                const float* za = zs + (rb + q) * LZ + l32;
+                const float* hb = hs + (rb + q) * LH + 32 * kt + l32;
+#pragma unroll 8
+                for (int st = 0; st < R / 4; ++st)
+                    dw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(za[2 * st * LZ], hb[2 * st * LH], dw[it], 0, 0, 0);
+            }
+        }
+        float bsum = 0.f;  // db0: thread (unit row, half) over its half's rows in order
+        if (row < N0) {
+            const float* zr = zs + half * (R / 2) * LZ + row;
+#pragma unroll 8
+            for (int r = 0; r < R / 2; ++r) bsum += zr[r * LZ];
+        }
+        // dh: every operand is in LDS already (dz tile, W0)
+        mfloatx16 dha[DPW];
+#pragma unroll
+        for (int it = 0; it < DPW; ++it) {
+            const int c = w + it * NW;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dha[it][r] = 0.f;
+            if (c < DT) {
+                const int rt = c / KT, kt = c % KT;
+                const float* za = zs + (32 * rt + l32) * LZ + q;
+                const float* wb = w0 + q * H + 32 * kt + l32;
+                for (int s4 = 0; s4 < N0 / 2; s4 += 4)  // (N0 % 8 == 0)
+#pragma unroll
+                    for (int st = s4; st < s4 + 4; ++st)
+                        dha[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(za[2 * st], wb[2 * st * H], dha[it], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // every read of the h tile is done: it takes the second halves
+        float* part = hs;  // [KT][16][64] tiles in register order, then db0's second half [HN0]
+#pragma unroll
+        for (int it = 0; it < IPW; ++it) {
+            const int c = w + it * NW;
+            if (c < NI && c / KT == 1)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) part[(c % KT) * 1024 + r * 64 + lane] = dw[it][r];
+        }
+        if (row < N0 && half == 1) part[KT * 1024 + row] = bsum;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < IPW; ++it) {
+            const int c = w + it * NW;
+            if (c < NI && c / KT == 0) {
+                const int kt = c % KT;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int j = (r & 3) + 8 * (r >> 2) + 4 * q;
+                    const float a = dw[it][r] + part[kt * 1024 + r * 64 + lane];
+                    if (j < N0) sl[(size_t)j * H + 32 * kt + l32] = a;
                 }
             }
         }
-        __syncthreads();  // every read of the h tile in this pass is done
-        if (half == 1 && t < ntile) {
+        if (row < N0 && half == 0) sl[N0 * H + row] = bsum + part[KT * 1024 + row];
+        __syncthreads();  // every read of the partials is done: the h tile takes dh
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+        for (int it = 0; it < DPW; ++it) {
+            const int c = w + it * NW;
+            if (c < DT) {
+                const int rt = c / KT, kt = c % KT;
 #pragma unroll
-                for (int v = 0; v < 4; ++v) part[row * 20 + 4 * u + v] = a[u][v];
-                part[row * 20 + 16 + u] = bs[u];
+                for (int r = 0; r < 16; ++r)
+                    hs[(32 * rt + (r & 3) + 8 * (r >> 2) + 4 * q) * LH + 32 * kt + l32] = dha[it][r];
             }
         }
-        __syncthreads();
-        if (half == 0 && t < ntile) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int v = 0; v < 4; ++v) a[u][v] += part[row * 20 + 4 * u + v];
-                bs[u] += part[row * 20 + 16 + u];
-                *(float4*)(sl + (size_t)(j0 + u) * H + k0) = make_float4(a[u][0], a[u][1], a[u][2], a[u][3]);
+    } else {
+        // dW0 (+ db0 on k0 = 0): 4 x 4 tiles, each over one half of the rows; the second half's
+        // partial goes through LDS (over the h tile) and the first adds it (fixed order)
+        const int ntile = (N0 / 4) * (H / 4);  // one tile per thread pair and pass
+        float* part = hs;  // [R][20]: the h tile, after its last read (dh overwrites it later)
+        static_assert(R * 20 <= R * LH, "dW0 partials fit the h tile");
+        for (int tb = 0; tb < ntile; tb += R) {
+            float a[4][4] = {}, bs[4] = {};
+            const int t = tb + row, j0 = 4 * (t / (H / 4)), k0 = 4 * (t % (H / 4));
+            if (t < ntile) {
+                const int rb = half * (R / 2);
+    #pragma unroll 4
+                for (int r = rb; r < rb + R / 2; ++r) {
+                    const float4 z4 = *(const float4*)(zs + r * LZ + j0);
+                    const float4 h4 = *(const float4*)(hs + r * LH + k0);
+                    const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
+    #pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        bs[u] += zz[u];
+    #pragma unroll
+                        for (int v = 0; v < 4; ++v) a[u][v] = fmaf(zz[u], hh[v], a[u][v]);
+                    }
+                }
             }
-            if (k0 == 0)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) sl[N0 * H + j0 + u] = bs[u];
-        }
-        if (tb + R < ntile) {  // the next pass reads the h tile again: restage it
+            __syncthreads();  // every read of the h tile in this pass is done
+            if (half == 1 && t < ntile) {
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+    #pragma unroll
+                    for (int v = 0; v < 4; ++v) part[row * 20 + 4 * u + v] = a[u][v];
+                    part[row * 20 + 16 + u] = bs[u];
+                }
+            }
             __syncthreads();
-            stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
-            __syncthreads();
-        }
-    }
-    // dh: this thread's half of the row's H entries, over all N0 units (dz0 from the tile)
-    {
-        constexpr int HH = H / 2;
-        const int kb = half * HH;
-        float dh[HH];
-#pragma unroll
-        for (int k = 0; k < HH; ++k) dh[k] = 0.f;
-#pragma unroll 1
-        for (int j = 0; j < N0; ++j) {
-            const float zj = zs[row * LZ + j];
-#pragma unroll
-            for (int k = 0; k < HH; k += 4) {
-                const float4 w = *(const float4*)(w0 + j * H + kb + k);
-                dh[k] = fmaf(w.x, zj, dh[k]); dh[k + 1] = fmaf(w.y, zj, dh[k + 1]);
-                dh[k + 2] = fmaf(w.z, zj, dh[k + 2]); dh[k + 3] = fmaf(w.w, zj, dh[k + 3]);
+            if (half == 0 && t < ntile) {
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+    #pragma unroll
+                    for (int v = 0; v < 4; ++v) a[u][v] += part[row * 20 + 4 * u + v];
+                    bs[u] += part[row * 20 + 16 + u];
+                    *(float4*)(sl + (size_t)(j0 + u) * H + k0) = make_float4(a[u][0], a[u][1], a[u][2], a[u][3]);
+                }
+                if (k0 == 0)
+    #pragma unroll
+                    for (int u = 0; u < 4; ++u) sl[N0 * H + j0 + u] = bs[u];
+            }
+            if (tb + R < ntile) {  // the next pass reads the h tile again: restage it
+                __syncthreads();
+                stage_rows<H, LH, R, NT>(J.h, r0, M, hs);
+                __syncthreads();
             }
         }
-        __syncthreads();  // every read of the h tile is done: it takes dh
-#pragma unroll
-        for (int k = 0; k < HH; k += 4)
-            *(float4*)(hs + row * LH + kb + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
+        // dh: this thread's half of the row's H entries, over all N0 units (dz0 from the tile)
+        {
+            constexpr int HH = H / 2;
+            const int kb = half * HH;
+            float dh[HH];
+    #pragma unroll
+            for (int k = 0; k < HH; ++k) dh[k] = 0.f;
+    #pragma unroll 1
+            for (int j = 0; j < N0; ++j) {
+                const float zj = zs[row * LZ + j];
+    #pragma unroll
+                for (int k = 0; k < HH; k += 4) {
+                    const float4 w = *(const float4*)(w0 + j * H + kb + k);
+                    dh[k] = fmaf(w.x, zj, dh[k]); dh[k + 1] = fmaf(w.y, zj, dh[k + 1]);
+                    dh[k + 2] = fmaf(w.z, zj, dh[k + 2]); dh[k + 3] = fmaf(w.w, zj, dh[k + 3]);
+                }
+            }
+            __syncthreads();  // every read of the h tile is done: it takes dh
+    #pragma unroll
+            for (int k = 0; k < HH; k += 4)
+                *(float4*)(hs + row * LH + kb + k) = make_float4(dh[k], dh[k + 1], dh[k + 2], dh[k + 3]);
+        }
     }
     __syncthreads();
     for (int i = tid; i < R * (H / 4); i += NT) {
@@ -1337,15 +1547,38 @@ static HeadJobs heads_pack(int njobs, const pmlp_head_job* jobs) {
 
 PMLP_API int32_t pmlp_heads_blocks(int32_t M) { return (M + PMLP_HEADS_BWD_ROWS - 1) / PMLP_HEADS_BWD_ROWS; }
 
+// the heads' products on the matrix cores (k_heads_fwd<.., MF>: y0, 64 rows x 128 threads;
+// k_heads_bwd<.., MF>: dW0 and dh), the same bits as the VALU forms; PMLP_HEADS_MFMA=0 keeps the
+// VALU forms (the forward at PMLP_HEADS_FWD_ROWS x _THREADS)
+static bool heads_mfma() {
+    static const bool on = [] {
+        const char* e = getenv("PMLP_HEADS_MFMA");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+constexpr int HFR_MF = 64, HFT_MF = 128;
+// below this many rows the forward keeps the VALU form: at the rollout's 8,192 its 64-row x
+// 256-thread workgroups fill the CUs better (10.2 against 11.2 us; the same bits either way)
+constexpr int HF_MF_MIN_ROWS = 16384;
+
+template <int H, bool ACT>
+static void heads_fwd_launch(int njobs, const HeadJobs& hj, int M, const HeadAct& ha, hipStream_t s) {
+    constexpr int FR = PMLP_HEADS_FWD_ROWS, FT = PMLP_HEADS_FWD_THREADS;
+    if (heads_mfma() && M >= HF_MF_MIN_ROWS)
+        hipLaunchKernelGGL((k_heads_fwd<H, HFR_MF, HFT_MF, ACT, true>), dim3((M + HFR_MF - 1) / HFR_MF, njobs),
+                           dim3(HFT_MF), 0, s, hj, M, ha);
+    else
+        hipLaunchKernelGGL((k_heads_fwd<H, FR, FT, ACT>), dim3((M + FR - 1) / FR, njobs), dim3(FT), 0, s, hj, M, ha);
+}
+
 PMLP_API int pmlp_heads_forward(int32_t njobs, const pmlp_head_job* jobs, int32_t M, int32_t H, void* stream) {
     if (int e = heads_check("pmlp_heads_forward", njobs, jobs, M, H, false)) return e;
     const HeadJobs hj = heads_pack(njobs, jobs);
-    constexpr int FR = PMLP_HEADS_FWD_ROWS, FT = PMLP_HEADS_FWD_THREADS;
-    const dim3 g((M + FR - 1) / FR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL((k_heads_fwd<32, FR, FT>), g, dim3(FT), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL((k_heads_fwd<64, FR, FT>), g, dim3(FT), 0, s, hj, M);
-    else hipLaunchKernelGGL((k_heads_fwd<128, FR, FT>), g, dim3(FT), 0, s, hj, M);
+    if (H == 32) heads_fwd_launch<32, false>(njobs, hj, M, HeadAct{}, s);
+    else if (H == 64) heads_fwd_launch<64, false>(njobs, hj, M, HeadAct{}, s);
+    else heads_fwd_launch<128, false>(njobs, hj, M, HeadAct{}, s);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward: ") + hipGetErrorString(e));
 }
@@ -1361,13 +1594,10 @@ PMLP_API int pmlp_heads_forward_act(const pmlp_head_job* jobs, int32_t M, int32_
     const HeadAct ha{act->stdv, act->obs, act->cobs, act->O, act->CO, act->A, act->draw, act->seed,
                      act->actions_out, act->st_actions, act->st_logp, act->st_mu, act->st_sigma, act->st_value,
                      act->st_obs, act->st_cobs};
-    constexpr int FR = PMLP_HEADS_FWD_ROWS, FT = PMLP_HEADS_FWD_THREADS;
-    static_assert(FR * 4 <= FT * 4 && FR <= FT, "one (row, quad) item per thread pass");
-    const dim3 g((M + FR - 1) / FR, 2);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL((k_heads_fwd<32, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
-    else if (H == 64) hipLaunchKernelGGL((k_heads_fwd<64, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
-    else hipLaunchKernelGGL((k_heads_fwd<128, FR, FT, true>), g, dim3(FT), 0, s, hj, M, ha);
+    if (H == 32) heads_fwd_launch<32, true>(2, hj, M, ha, s);
+    else if (H == 64) heads_fwd_launch<64, true>(2, hj, M, ha, s);
+    else heads_fwd_launch<128, true>(2, hj, M, ha, s);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_forward_act: ") + hipGetErrorString(e));
 }
@@ -1378,9 +1608,10 @@ PMLP_API int pmlp_heads_backward(int32_t njobs, const pmlp_head_job* jobs, int32
     constexpr int BR = PMLP_HEADS_BWD_ROWS;
     const dim3 g((M + BR - 1) / BR, njobs);
     hipStream_t s = (hipStream_t)stream;
-    if (H == 32) hipLaunchKernelGGL((k_heads_bwd<32, BR>), g, dim3(2 * BR), 0, s, hj, M);
-    else if (H == 64) hipLaunchKernelGGL((k_heads_bwd<64, BR>), g, dim3(2 * BR), 0, s, hj, M);
-    else hipLaunchKernelGGL((k_heads_bwd<128, BR>), g, dim3(2 * BR), 0, s, hj, M);
+    const bool mf = heads_mfma();
+    if (H == 32) hipLaunchKernelGGL(mf ? (k_heads_bwd<32, BR, true>) : (k_heads_bwd<32, BR>), g, dim3(2 * BR), 0, s, hj, M);
+    else if (H == 64) hipLaunchKernelGGL(mf ? (k_heads_bwd<64, BR, true>) : (k_heads_bwd<64, BR>), g, dim3(2 * BR), 0, s, hj, M);
+    else hipLaunchKernelGGL(mf ? (k_heads_bwd<128, BR, true>) : (k_heads_bwd<128, BR>), g, dim3(2 * BR), 0, s, hj, M);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(std::string("pmlp_heads_backward: ") + hipGetErrorString(e));
 }
