@@ -1138,6 +1138,7 @@ __global__ __launch_bounds__(NT) void k_heads_fwd(HeadJobs jobs, int M, HeadAct 
 template <int H, int R = HR, bool MF = false>
 __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
     constexpr int NT = 2 * R;
+    static_assert(!MF || R >= 128, "MF: dW1 on waves 0 and 1, db1 on wave 2");
     const HeadJob& J = jobs.j[blockIdx.y];
     const int N0 = J.N0, N1 = J.N1, tid = threadIdx.x, r0 = blockIdx.x * R;
     const int row = tid & (R - 1), half = tid / R;
@@ -1165,18 +1166,44 @@ __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
     }
     __syncthreads();
     float* sl = J.slab + (size_t)blockIdx.x * (N0 * H + N0 + N1 * N0 + N1);
-    // dW1 (+ db1 on j = 0) from the y0 and dout tiles, before y0 is overwritten
-    for (int t = tid; t < N1 * N0; t += NT) {
-        const int i = t / N0, j = t - i * N0;
-        float a = 0.f, b = 0.f;
+    // dW1 (+ db1) from the y0 and dout tiles, before y0 is overwritten
+    if constexpr (MF) {
+        // dW1 [i][j] as two v_mfma_f32_16x16x4_f32 tiles (j in 0..15, 16..31) on waves 0 and 1:
+        // A[i][slot] = dout[r][i], B[slot][j] = y0[r][j], step s holding rows 4s .. 4s + 3 -- the
+        // VALU form's chain over the rows in order.  db1 on wave 2 (adds, rows in order).
+        const int lane = tid & 63, w = tid >> 6;
+        if (w < 2) {
+            mfloatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            const float* da = ds + (lane >> 4) * LO + (lane & 15);
+            const float* yb = zs + (lane >> 4) * LZ + 16 * w + (lane & 15);
 #pragma unroll 8
-        for (int r = 0; r < R; ++r) {
-            const float d = ds[r * LO + i];
-            a = fmaf(d, zs[r * LZ + j], a);
-            b += d;
+            for (int st = 0; st < R / 4; ++st)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(da[4 * st * LO], yb[4 * st * LZ], acc, 0, 0, 0);
+            const int j = 16 * w + (lane & 15);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int i = 4 * (lane >> 4) + v;
+                if (i < N1 && j < N0) sl[N0 * H + N0 + i * N0 + j] = acc[v];
+            }
+        } else if (w == 2 && lane < N1) {
+            float b = 0.f;
+#pragma unroll 8
+            for (int r = 0; r < R; ++r) b += ds[r * LO + lane];
+            sl[N0 * H + N0 + N1 * N0 + lane] = b;
         }
-        sl[N0 * H + N0 + t] = a;
-        if (j == 0) sl[N0 * H + N0 + N1 * N0 + i] = b;
+    } else {
+        for (int t = tid; t < N1 * N0; t += NT) {
+            const int i = t / N0, j = t - i * N0;
+            float a = 0.f, b = 0.f;
+#pragma unroll 8
+            for (int r = 0; r < R; ++r) {
+                const float d = ds[r * LO + i];
+                a = fmaf(d, zs[r * LZ + j], a);
+                b += d;
+            }
+            sl[N0 * H + N0 + t] = a;
+            if (j == 0) sl[N0 * H + N0 + N1 * N0 + i] = b;
+        }
     }
     // dz0 of this thread's half of the row's units (registers), W1^T dout over the rows of W1
     const int nh = N0 / 2, jb = half * nh;
@@ -1278,7 +1305,8 @@ __global__ __launch_bounds__(2 * R) void k_heads_bwd(HeadJobs jobs, int M) {
             }
         }
         if (row < N0 && half == 0) sl[N0 * H + row] = bsum + part[KT * 1024 + row];
-        __syncthreads();  // every read of the partials is done: the h tile takes dh
+        __syncthreads();  // every read of the partials is done: the h tile takes dh (then
+        // 16-byte coalesced stores; straight from the accumulators was slower, 41.1 vs 39.1 us)
 #pragma unroll
         for (int it = 0; it < DPW; ++it) {
             const int c = w + it * NW;
