@@ -444,6 +444,35 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
                 if constexpr (NP == 2) wf[NP - 1][tt][s][e] = lo;
             }
     }
+    // a tile's t = 0 inputs (state, reset, x), loaded for tile q + 1 while tile q computes (the
+    // rollout's multi-tile steps: each tile otherwise waits one full round trip on them);
+    // unconditional loads at clamped addresses, masked where used
+    const bool xs = tid < 256;
+    const int xe = (tid & 255) >> 4, xk = (tid & 15) * 4;
+    float pf_h[2], pf_c[2], pf_x[4];
+    uint8_t pf_r[2], pf_rn[2];  // resets at t = 0 and at t = 1 (rload(1))
+    const uint8_t* rbase = a.reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
+    // (absent h0 / c0 / reset: a load of x[0], masked -- no branch, which would put a vmcnt(0)
+    // behind every load)
+    const float* h0p = a.h0 ? a.h0 : a.x;
+    const float* c0p = a.c0 ? a.c0 : a.x;
+    auto in_load = [&](int e0n) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            const int gc = min(e0n + 4 * rg + 2 * hj + pp, B - 1);
+            const float hv = h0p[a.h0 ? (size_t)gc * MH + uu : 0];
+            const float cv = c0p[a.c0 ? (size_t)gc * MH + uu : 0];
+            const uint8_t r0 = rbase[a.reset ? gc : 0];
+            pf_h[pp] = a.h0 ? hv : 0.f;
+            pf_c[pp] = a.c0 ? cv : 0.f;
+            pf_r[pp] = a.reset ? r0 : (uint8_t)0;
+            pf_rn[pp] = rbase[(size_t)min(1, T - 1) * B + gc];
+        }
+        const int gx = min(e0n + xe, B - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pf_x[i] = a.x[(size_t)gx * I + min(xk + i, I - 1)];
+    };
+    in_load(ebase);
     for (int q = 0; q < tiles; ++q) {
     const int e0 = ebase + q * ME;
     if (e0 >= B) break;   // (uniform)
@@ -455,8 +484,6 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
         if constexpr (NP == 2) A[NP - 1][buf][idx] = lo;
     };
     // x staging by the first 256 threads: 4 floats each per step (16 envs x 64 slots)
-    const bool xs = tid < 256;
-    const int xe = (tid & 255) >> 4, xk = (tid & 15) * 4;
     float xr[4];
     auto xload = [&](int t) {
         const int gc = min(e0 + xe, B - 1);
@@ -483,9 +510,9 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
 #pragma unroll
     for (int pp = 0; pp < 2; ++pp) {
         const int p = 2 * hj + pp, ge = e0 + 4 * rg + p;
-        const bool rs = a.reset && ge < B && a.reset[ge];
-        const float h0 = (ge < B && a.h0) ? a.h0[(size_t)ge * MH + uu] : 0.f;
-        const float c0 = (ge < B && a.c0) ? a.c0[(size_t)ge * MH + uu] : 0.f;
+        const bool rs = a.reset && ge < B && pf_r[pp];
+        const float h0 = ge < B ? pf_h[pp] : 0.f;
+        const float c0 = ge < B ? pf_c[pp] : 0.f;
         hp[pp] = rs ? 0.f : h0;
         c[pp] = rs ? 0.f : c0;
         put(0, (4 * rg + p) * MLDA + MKX + uu, hp[pp]);
@@ -495,19 +522,22 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
         }
     }
     const bool has_reset = a.reset != nullptr;
-    const uint8_t* rbase = has_reset ? a.reset : (const uint8_t*)a.x;  // masked when absent
     auto rload = [&](int t, uint8_t* r) {
         const size_t tc = (size_t)min(t, T - 1) * B;
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) r[pp] = rbase[tc + min(e0 + 4 * rg + 2 * hj + pp, B - 1)];
     };
-    uint8_t rnx[2];
-    rload(1, rnx);
+    uint8_t rnx[2] = {pf_rn[0], pf_rn[1]};  // (rload(1), prefetched)
     if (xs) {
-        xload(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = pf_x[i];  // (xload(0), prefetched)
         xstore(0, 0);
         if (T > 1) xload(1);
     }
+    // the next tile's, in flight from here (not hoisted above this tile's last uses of the
+    // prefetched values: vmcnt is in order, so those would then wait for these)
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + 1 < tiles && e0 + ME < B) in_load(e0 + ME);
     __syncthreads();
     for (int t = 0; t < T; ++t) {
         const int cur = t & 1;
