@@ -483,13 +483,16 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
         A[0][buf][idx] = hi;
         if constexpr (NP == 2) A[NP - 1][buf][idx] = lo;
     };
-    // x staging by the first 256 threads: 4 floats each per step (16 envs x 64 slots)
-    float xr[4];
-    auto xload = [&](int t) {
+    // x staging by the first 256 threads: 4 floats each per step (16 envs x 64 slots).  x and
+    // the resets are loaded two steps ahead (xr: step t + 1's, stored at the end of step t; xr2:
+    // step t + 2's): vmcnt counts the per-step stores too and retires in order, so a load issued
+    // after step t's stores and used one step later waited for those stores as well
+    float xr[4], xr2[4];
+    auto xload = [&](int t, float (&dst)[4]) {
         const int gc = min(e0 + xe, B - 1);
         const size_t tc = (size_t)min(t, T - 1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = a.x[(tc * B + gc) * I + min(xk + i, I - 1)];
+        for (int i = 0; i < 4; ++i) dst[i] = a.x[(tc * B + gc) * I + min(xk + i, I - 1)];
     };
     auto xstore = [&](int buf, int t) {
         const int ge = e0 + xe;
@@ -527,12 +530,14 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) r[pp] = rbase[tc + min(e0 + 4 * rg + 2 * hj + pp, B - 1)];
     };
-    uint8_t rnx[2] = {pf_rn[0], pf_rn[1]};  // (rload(1), prefetched)
+    uint8_t rnx[2] = {pf_rn[0], pf_rn[1]};  // reset(t + 1) at step t (rload(1), prefetched)
+    uint8_t rnx2[2];                          // reset(t + 2)
+    rload(2, rnx2);
     if (xs) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) xr[i] = pf_x[i];  // (xload(0), prefetched)
         xstore(0, 0);
-        if (T > 1) xload(1);
+        if (T > 1) xload(1, xr);
     }
     // the next tile's, in flight from here (not hoisted above this tile's last uses of the
     // prefetched values: vmcnt is in order, so those would then wait for these)
@@ -543,8 +548,12 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
         const int cur = t & 1;
         bool rn[2];
 #pragma unroll
-        for (int pp = 0; pp < 2; ++pp) rn[pp] = has_reset && t + 1 < T && rnx[pp] != 0;
-        rload(t + 2, rnx);
+        for (int pp = 0; pp < 2; ++pp) {
+            rn[pp] = has_reset && t + 1 < T && rnx[pp] != 0;
+            rnx[pp] = rnx2[pp];
+        }
+        rload(t + 3, rnx2);
+        if (xs) xload(t + 2, xr2);  // (clamped to T - 1 past the end)
         mfloatx4 acc[2];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
@@ -598,7 +607,8 @@ __global__ __launch_bounds__(512) void k_lstm_fwd_mfma8(MFwdBatch ab, int tiles)
         }
         if (xs) {
             if (t + 1 < T) xstore(nxt, t + 1);
-            xload(t + 2);  // clamped to T - 1 past the end
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] = xr2[i];
         }
         __syncthreads();
     }
@@ -651,11 +661,12 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
             // load instruction reads 64 consecutive columns of one row (coalesced)
             const int RL = a.I + MH + 1, nenv = min(ME, B - e0), nct = (RL + 31) / 32;
             const int xc = wt & (MXC - 1), xg = wt >> 7;
-            float xr[8];
-            auto xload = [&](int t) {
+            // xr: step t's rows, xr2: step t - 1's (loaded two steps ahead)
+            float xr[8], xr2[8];
+            auto xload = [&](int t, float (&dst)[8]) {
                 const float* src = a.xh + ((size_t)max(t, 0) * B + e0) * RL + min(xc, RL - 1);
 #pragma unroll
-                for (int k = 0; k < 8; ++k) xr[k] = src[(size_t)min(8 * xg + k, nenv - 1) * RL];
+                for (int k = 0; k < 8; ++k) dst[k] = src[(size_t)min(8 * xg + k, nenv - 1) * RL];
             };
             mfloatx16 dacc[8];
 #pragma unroll
@@ -667,7 +678,8 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
             // drop that column of the first step's operand)
             for (int i = wt; i < NP * 2 * MXC * ME; i += 256)
                 if ((i % (MXC * ME)) / ME >= RL) (&XT[0][0][0])[i] = (mbf16)0.f;
-            xload(T - 1);
+            xload(T - 1, xr);
+            xload(T - 2, xr2);
             for (int t = T - 1; t >= 0; --t) {
                 const int buf = t & 1;
                 if (xc < RL) {
@@ -682,7 +694,9 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
                     *(mbf16x8*)(&XT[0][buf][xc * ME + 8 * xg]) = hi8;
                     if constexpr (NP == 2) *(mbf16x8*)(&XT[NP - 1][buf][xc * ME + 8 * xg]) = lo8;
                 }
-                xload(t - 1);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xr[k] = xr2[k];
+                xload(t - 2, xr2);
                 __syncthreads();
                 // operands of the wave's 2 x 4 tiles, then the products pass by pass
                 // (consecutive MFMAs on different accumulators)
@@ -778,12 +792,14 @@ __global__ __launch_bounds__(DW ? 512 : 256) void k_lstm_bwd_mfma(MBwdBatch ab) 
         }
     };
     float dhn[4] = {0.f, 0.f, 0.f, 0.f}, dcn[4] = {0.f, 0.f, 0.f, 0.f};
-    In nx;
+    In nx, nx2;  // step t's inputs and step t - 1's, loaded two steps ahead
     load(T - 1, nx);
+    load(T - 2, nx2);
     for (int t = T - 1; t >= 0; --t) {
         const int buf = t & 1;
         const In v = nx;
-        load(t - 1, nx);
+        nx = nx2;
+        load(t - 2, nx2);
         mbf16x4 gth[4], gtl[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
